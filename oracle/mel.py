@@ -1,0 +1,62 @@
+"""ORACLE (test infrastructure only) -- mel/STFT front-end restated on the CPU.
+
+PARITY-UNPINNED: the reference computes these features with torchaudio
+(``scripts/preprocessor/preprocessor.py:22-36,323-337``) and librosa
+(``scripts/audio/stft.py:145-178``); neither is installed here and no file in the
+reference holds their outputs.  This module restates the *published* algorithms
+of those libraries (versions are unpinned in ``requirements.txt``):
+
+* torchaudio ``Spectrogram(n_fft, win_length, hop_length, power=1, center=True)``
+  = ``|torch.stft(x, n_fft, hop, win, hann_window(win, periodic=True),
+  center=True, pad_mode="reflect", onesided=True)|``;
+* torchaudio ``melscale_fbanks(n_freqs, f_min, f_max, n_mels, sr, norm="slaney",
+  mel_scale="htk")``: HTK mel points, triangular filters on
+  ``linspace(0, sr // 2, n_freqs)``, slaney area normalisation 2 / (f[i+2] - f[i]);
+* ``_get_spec``: log(clamp_min(fb^T |X|, 1e-5)); energy = L2 norm of |X| over
+  frequency.
+"""
+
+import numpy as np
+import torch
+
+
+def hz_to_mel_htk(f):
+    return 2595.0 * np.log10(1.0 + np.asarray(f, dtype=np.float64) / 700.0)
+
+
+def mel_to_hz_htk(m):
+    return 700.0 * (10.0 ** (np.asarray(m, dtype=np.float64) / 2595.0) - 1.0)
+
+
+def melscale_fbanks(n_freqs=513, f_min=0.0, f_max=8000.0, n_mels=80, sample_rate=22050):
+    """(n_freqs, n_mels) float32 HTK-scale, slaney-normalised triangular filterbank."""
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_pts = torch.linspace(float(hz_to_mel_htk(f_min)), float(hz_to_mel_htk(f_max)), n_mels + 2)
+    f_pts = 700.0 * (10.0 ** (m_pts / 2595.0) - 1.0)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts[None, :] - all_freqs[:, None]
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    fb = torch.clamp(torch.minimum(down, up), min=0.0)
+    enorm = 2.0 / (f_pts[2: n_mels + 2] - f_pts[:n_mels])
+    return fb * enorm[None, :]
+
+
+def magnitude(wav, n_fft=1024, hop=256, win=1024):
+    """|STFT| (..., n_fft//2+1, frames) as torchaudio Spectrogram(power=1, center=True)."""
+    wav = torch.as_tensor(wav, dtype=torch.float32)
+    window = torch.hann_window(win, periodic=True)
+    X = torch.stft(wav, n_fft, hop_length=hop, win_length=win, window=window, center=True,
+                   pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    return X.abs()
+
+
+def get_spec(wav, n_fft=1024, hop=256, win=1024, n_mels=80, sr=22050, fmin=0.0, fmax=8000.0):
+    """Preprocessor._get_spec, preprocessor.py:323-337 -> (log-mel (..., 80, F), energy (..., F))."""
+    wav = torch.clamp(torch.as_tensor(wav, dtype=torch.float32), -1, 1)
+    mag = magnitude(wav, n_fft, hop, win)
+    fb = melscale_fbanks(n_fft // 2 + 1, fmin, fmax, n_mels, sr)
+    mel = torch.matmul(mag.transpose(-1, -2), fb).transpose(-1, -2)
+    logmel = torch.log(torch.clamp_min(mel, 1.0e-5) * 1.0)
+    energy = torch.linalg.vector_norm(mag, dim=-2)
+    return logmel, energy
