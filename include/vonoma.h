@@ -1,0 +1,203 @@
+/* vonoma.h -- C ABI of the MI355X (gfx950) synthesis-path kernels.
+ *
+ * Drop-in boundary for the reference's visual-onomatopoeia -> mel -> waveform path
+ * (sarulab-speech/visual-onoma-to-wave).  The reference is pure PyTorch: every op on
+ * its path is an implicit ATen kernel launched from the nn.Modules cited below.  Each
+ * entry point here replaces those ATen calls for one reference function; the Python
+ * host layer (visual_onoma_to_wave_amd/, same module/class names as the reference)
+ * binds them through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - plain device pointers and sizes; all buffers are caller-owned (no allocation
+ *    inside, no host synchronisation: every call is stream-ordered and graph-capturable);
+ *  - `stream` is a hipStream_t passed as void*; NULL = the default stream;
+ *  - return 0 (VO_OK) on success, VO_ERR_INVALID on a rejected argument, or the
+ *    hipError_t of a failed launch; vo_last_error() describes the last failure;
+ *  - activations are channels-last ("(B, T, C)", C contiguous) -- the layout the
+ *    reference's transformer side already uses (scripts/transformer/SubLayers.py:85-93
+ *    transposes to (B, C, T) only to call Conv1d) and the one whose 8 consecutive
+ *    channels form one MFMA operand fragment;
+ *  - element types: VO_F32 or VO_BF16 for tensor I/O; VO_BF16 compute = bf16 MFMA with
+ *    fp32 accumulation, VO_F32 compute = exact-f32 MFMA (the parity mode).
+ */
+#ifndef VONOMA_H_
+#define VONOMA_H_
+
+#include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VO_OK 0
+#define VO_ERR_INVALID (-1)
+
+enum vo_dtype { VO_F32 = 0, VO_BF16 = 1 };
+enum vo_act { VO_ACT_NONE = 0, VO_ACT_RELU = 1, VO_ACT_LRELU = 2, VO_ACT_TANH = 3 };
+
+/* ------------------------------------------------------------------ runtime */
+const char* vo_last_error(void);
+int vo_version(void);
+/* number of entry points and their names (used by the loader test) */
+int vo_num_symbols(void);
+const char* vo_symbol_name(int i);
+
+/* ------------------------------------------------------------------ conv1d (implicit GEMM)
+ * y[b, t, co] = post( sum_{k, ci} W[k][co][ci] * pre(x[b, t*1 + k*dil - pad, ci]) + bias[co] )
+ *               (+ res1) * out_scale (+ res2)
+ * Replaces: nn.Conv1d in PositionwiseFeedForward (scripts/transformer/SubLayers.py:60-93),
+ *   PostNet ConvNorm+BatchNorm1d (scripts/transformer/Layers.py:33-137, BN folded),
+ *   VariancePredictor Conv (scripts/model/modules.py:216-259), nn.Linear as K=1
+ *   (SubLayers.py:18-26, vtts.py:23-26, visual_feature_extractor.py:49-55),
+ *   HiFi-GAN conv_pre / ResBlock convs with the lrelu prologue and residual epilogue
+ *   (scripts/hifigan/models.py:96-103,150,155-160).
+ * transposed != 0: ConvTranspose1d(stride=s, padding=p, K_t = 2s) in its polyphase form
+ *   (scripts/hifigan/models.py:124-135,153): W holds the 2-tap phase weights packed by
+ *   vo_pack_weight(..., VO_PACK_CONVT, ...), co spans s*C_out phase-major columns and output
+ *   row m lands at time m*s - p + phase.
+ */
+typedef struct vo_conv1d_desc {
+  const void* x;      /* input (B, T_in, ldx) channels-last, dtype x_dtype            */
+  int x_dtype;
+  int64_t x_bstride;  /* elements between batches (usually T_in * ldx)               */
+  int ldx;            /* elements between rows (>= Ci, multiple of 8)                */
+  const void* w;      /* packed weights [K][Co][Ci], dtype = compute dtype            */
+  const float* bias;  /* [Co] or NULL                                                 */
+  void* y;            /* output, dtype y_dtype                                        */
+  int y_dtype;
+  int64_t y_bstride;
+  int ldy;
+  const void* res1;   /* optional, same layout and dtype as y                        */
+  const void* res2;   /* optional, same layout and dtype as y (may alias y)          */
+  int B, T_in, T_out; /* T_out = output rows (for transposed: T_in + 1 phase rows)   */
+  int Ci, Co;         /* Co = GEMM columns (transposed: s * C_out)                    */
+  int K, dil, pad;
+  int pre_act;  float pre_slope;
+  int post_act; float post_slope;
+  float out_scale;
+  int compute_dtype;  /* VO_BF16 or VO_F32 */
+  int transposed, up_stride, up_pad, up_cout, up_tout; /* polyphase ConvTranspose1d */
+} vo_conv1d_desc;
+int vo_conv1d(const vo_conv1d_desc* d, void* stream);
+
+/* Weight preparation (load time).  Replaces the weight-norm fold (remove_weight_norm,
+ * scripts/hifigan/models.py:105-109,167-174: w = g * v / ||v||, norm over all dims but 0)
+ * and the eval-mode BatchNorm fold of PostNet / VFE (Layers.py:129-137), and writes the
+ * [K][Co][Ci] compute layout.
+ *   mode VO_PACK_CONV : src (Co, Ci, K) -> dst [K][Co][Ci]
+ *   mode VO_PACK_CONVT: src (Ci, Co, 2s) (ConvTranspose1d) -> dst [2][s*Co][Ci],
+ *                       dst[kk][r*Co + co][ci] = src[ci][co][r + s*(1-kk)]
+ * g (nullable): weight-norm gains, one per src dim-0 slice; row_scale (nullable): per-Co
+ * multiplier (BatchNorm gamma / sqrt(var + eps)). */
+enum vo_pack_mode { VO_PACK_CONV = 0, VO_PACK_CONVT = 1 };
+int vo_pack_weight(const float* src, const float* g, const float* row_scale, int mode, int Co,
+                   int Ci, int K, int stride, void* dst, int dst_dtype, void* stream);
+
+/* ------------------------------------------------------------------ layer norm
+ * y[r, :] = LayerNorm(x[r, :] + res[r, :]) * gamma + beta, then zeroed where row r is padding
+ * (t >= lens[b], r = b*T + t; lens may be NULL).  eps 1e-5.
+ * Replaces: MultiHeadAttention/PositionwiseFeedForward post-LN + residual
+ * (scripts/transformer/SubLayers.py:55,91) and FFTBlock.masked_fill (Layers.py:25,28);
+ * VariancePredictor LN (modules.py:197-206) with res = NULL, lens = NULL. */
+int vo_layernorm(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
+                 const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
+                 int y_dtype, void* stream);
+
+/* ------------------------------------------------------------------ attention
+ * Scaled dot-product attention with key padding, H heads of d_k = D/H, over the fused
+ * qkv activations (B, L, 3D) (columns [q | k | v], head h at h*d_k) -> out (B, L, D)
+ * (head-concat columns h*d_k + d).  Keys t >= lens[b] are masked (-inf before softmax).
+ * Replaces: MultiHeadAttention split/permute + ScaledDotProductAttention
+ * (scripts/transformer/SubLayers.py:39-53, scripts/transformer/Modules.py:14-25).  The
+ * probabilities are never materialised (the reference returns them but no caller uses
+ * them: Models.py:119-124, 190-195). */
+int vo_attention(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
+                 float scale, void* out, void* stream);
+
+/* ------------------------------------------------------------------ length regulator
+ * out[b, t, :] = x[b, j, :] for cs[j-1] <= t < cs[j] (cs = inclusive cumsum of
+ * max(trunc(d[b, j]), 0)), zero for t >= mel_len[b]; mel_len[b] = cs[T_src-1]; rows past
+ * max_len are cropped.  index (nullable) receives j (or -1).
+ * Replaces: LengthRegulator.LR/expand (scripts/model/modules.py:132-159) + pad
+ * (scripts/utils/tools.py:669-687): no per-token device->host sync. */
+int vo_length_regulate(const void* x, int x_dtype, const float* dur, int B, int T_src, int D,
+                       int max_len, void* out, int out_dtype, int64_t* mel_len, int32_t* index,
+                       void* stream);
+/* mel_len only (int64 and int32 copies), so the host can size the output. */
+int vo_lr_lengths(const float* dur, int B, int T_src, int64_t* mel_len, int32_t* mel_len32,
+                  void* stream);
+
+/* ------------------------------------------------------------------ variance heads
+ * Linear(D -> 1) + masked_fill(pad, 0) over h (B*T, D)  (VariancePredictor.linear_layer,
+ * scripts/model/modules.py:207-213), then per head:
+ *  VO_HEAD_DURATION: pred -> log_d; if d_round != NULL: d_round = clamp(round(exp(log_d)-1)
+ *                    * d_control, 0) (modules.py:110-113, round half to even)
+ *  VO_HEAD_ENERGY:   pred -> e_pred; idx = bucketize(target or ((pred*std+mean)*control -
+ *                    mean)/std, bins) (right=False); x[b, t, :] += table[idx] (modules.py:
+ *                    53-64,101-104); e_pred receives the transformed prediction when no
+ *                    target is given, as the reference returns it. */
+enum vo_head_kind { VO_HEAD_DURATION = 0, VO_HEAD_ENERGY = 1 };
+typedef struct vo_head_desc {
+  int kind;
+  const void* h; int h_dtype;     /* (B*T, D) after the second LayerNorm     */
+  const float* w; float b;        /* Linear(D, 1) weight [D] and bias         */
+  const int32_t* lens;            /* src lengths [B] (pad mask), nullable     */
+  int B, T, D;
+  float* pred;                    /* [B*T] log_d or energy prediction         */
+  float* d_round; float d_control;/* duration head                            */
+  const float* target;            /* energy target [B*T] or NULL              */
+  const float* bins; int n_bins;  /* bucket boundaries (n_bins)               */
+  float e_mean, e_std, e_control;
+  const float* table;             /* embedding (n_bins + 1, D) fp32           */
+  void* x; int x_dtype;           /* (B*T, D) hidden state, += table[idx]     */
+  int32_t* idx_out;               /* optional bucket indices                  */
+} vo_head_desc;
+int vo_variance_head(const vo_head_desc* d, void* stream);
+
+/* ------------------------------------------------------------------ encoder glue
+ * Visual feature extractor front: for every 24 x W_s slice (b, i) of images (B, 1, 24, W),
+ * 3 x [Conv2d 3x3 pad 1 (1 -> 1 ch) -> BatchNorm2d(eval, folded scale/shift) -> ReLU],
+ * flattened h*W_s + w into out (B*n, 24*W_s) (then the bridge Linear runs as vo_conv1d K=1).
+ * Replaces: VisualFeatureExtractor.forward slicing loop + embedder
+ * (scripts/model/visual_feature_extractor.py:60-80).  conv: [n_layers][10] = 9 weights +
+ * bias; bn: [n_layers][2] = scale, shift. */
+int vo_vfe_stencil(const float* images, int B, int H, int W, int slice_w, int n_slices,
+                   const float* conv, const float* bn, int n_layers, void* out, int out_dtype,
+                   void* stream);
+/* x[b, t, :] += pe[t, :] (pe nullable) + cls[idx, :] (cls nullable) with idx = cls_idx[b]
+ * (idx_per_token = 0) or cls_idx[b*T + t] (idx_per_token = 1).
+ * Replaces: position_enc add (Models.py:107-116, 184-186), audiotype_emb add (vtts.py:84-85)
+ * and the src_word_emb lookup of the use_image=False branch (Models.py:114). */
+int vo_add_pos_class(void* x, int x_dtype, const float* pe, const float* cls,
+                     const int64_t* cls_idx, int idx_per_token, int B, int T, int D, void* stream);
+/* mask[b, t] = t >= lens[b] (True = padding) and/or lens32[b] = (int32) lens[b];
+ * lens_dtype: 0 = fp32, 2 = int64, 3 = int32.  Replaces get_mask_from_lengths
+ * (scripts/utils/tools.py:164-171). */
+int vo_mask_from_lengths(const void* lens, int lens_dtype, int B, int L, bool* mask,
+                         int32_t* lens32, void* stream);
+
+/* ------------------------------------------------------------------ vocoder glue
+ * conv_post: y[b, t] = tanh(bias + sum_{k<7, c} w[k][c] * lrelu(x[b, t+k-3, c], 0.01))
+ * over channels-last x (B, T, C) -> (B, T) fp32.  Replaces Generator.forward tail
+ * (scripts/hifigan/models.py:161-163).  w packed [K][C] fp32. */
+int vo_conv_post(const void* x, int x_dtype, const float* w, float bias, int B, int T, int C,
+                 int K, float slope, float* y, void* stream);
+/* (B, C, T) -> (B, T, ldy) with channels C..ldy-1 zero-filled; fp32 in, dtype out. */
+int vo_transpose_bct(const float* x, int B, int C, int T, void* y, int y_dtype, int ldy,
+                     void* stream);
+
+/* ------------------------------------------------------------------ mel / STFT front-end
+ * log-mel (B, n_mels, F) and energy (B, F), F = 1 + N / hop, of wav (B, N) fp32 with
+ * torchaudio Spectrogram(n_fft, win=n_fft, hop, power=1, center=True, reflect) +
+ * MelScale(fb) + log(clamp_min(., 1e-5)) semantics (scripts/preprocessor/preprocessor.py:
+ * 22-36,323-337).  window: (n_fft) fp32; fb: (n_fft/2+1, n_mels) fp32. */
+int vo_stft_mel(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
+                int hop, int n_mels, float log_floor, float* mel, float* energy, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VONOMA_H_ */

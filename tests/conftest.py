@@ -20,3 +20,10 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def pytest_runtest_setup(item):
+    if item.get_closest_marker("gpu") is not None:
+        import torch
+        if not torch.cuda.is_available():
+            pytest.skip("needs a GPU")

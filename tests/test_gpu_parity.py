@@ -1,0 +1,295 @@
+"""GPU parity: the HIP path vs the golden vectors (reference outputs) and vs the CPU oracle.
+
+Tolerances (relative L2 unless stated):
+  * fp32 mode (exact-f32 MFMA; only summation order differs from oneDNN):  2e-5 per
+    module, 1e-4 for whole-model outputs;
+  * bf16 kernels (bf16 operands, fp32 accumulation):  2e-2 (measured reference-vs-
+    reference bf16 drift is 3.4e-3 for the Generator, 4.5e-3 for vTTS);
+  * integer / index results (LengthRegulator frames + mel_len, bucket indices, masks,
+    d_rounded):  bit-exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import configs, golden, hifigan_arrays, hifigan_h, rel_l2, stats, vtts_arrays
+from weights import load_into
+
+pytestmark = pytest.mark.gpu
+
+F32_MOD, F32_MODEL, BF16 = 2e-5, 1e-4, 2e-2
+
+
+def cuda(a):
+    return torch.from_numpy(np.array(a)).cuda()
+
+
+@pytest.fixture(scope="module")
+def vtts(device):
+    from visual_onoma_to_wave_amd.model import vTTS
+    m = vTTS(*configs())
+    load_into(m, vtts_arrays())
+    return m.to(device).eval()
+
+
+@pytest.fixture(scope="module")
+def gen(device):
+    from visual_onoma_to_wave_amd import hifigan
+    g = hifigan.Generator(hifigan.AttrDict(hifigan_h()))
+    load_into(g, hifigan_arrays())
+    g.eval()
+    g.remove_weight_norm()
+    return g.to(device)
+
+
+def _prec(m, mode):
+    m.set_precision(mode)
+    return torch.float32 if mode == "fp32" else torch.bfloat16
+
+
+# ------------------------------------------------------------------------------ acoustic modules
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, BF16)])
+def test_vfe(vtts, dt, tol):
+    g = golden("vfe")
+    vfe = vtts.encoder.VisualFeatureExtractor
+    vfe.set_compute_dtype(dt)
+    with torch.no_grad():
+        out = vfe(cuda(g["images"]))
+    assert rel_l2(out.float().cpu(), g["out"]) < tol
+
+
+@pytest.mark.parametrize("name,which", [("fft_enc", "encoder"), ("fft_dec", "decoder")])
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, BF16)])
+def test_fft_block(vtts, name, which, dt, tol):
+    from visual_onoma_to_wave_amd.utils.tools import get_mask_from_lengths
+    g = golden(name)
+    layer = getattr(vtts, which).layer_stack[0]
+    layer.set_compute_dtype(dt)
+    L = g["x"].shape[1]
+    mask = get_mask_from_lengths(cuda(g["lens"]), L)
+    with torch.no_grad():
+        out, _ = layer(cuda(g["x"]), mask=mask)
+    assert rel_l2(out.float().cpu(), g["out"]) < tol
+
+
+def test_variance_predictors(vtts):
+    from visual_onoma_to_wave_amd.utils.tools import get_mask_from_lengths
+    g = golden("var_pred")
+    va = vtts.variance_adaptor
+    va.set_compute_dtype(torch.float32)
+    mask = get_mask_from_lengths(cuda(g["lens"]), 12)
+    with torch.no_grad():
+        ld = va.duration_predictor(cuda(g["x"]), mask)
+        en = va.energy_predictor(cuda(g["x"]), mask)
+    assert rel_l2(ld.cpu(), g["log_d"]) < F32_MOD
+    assert rel_l2(en.cpu(), g["energy"]) < F32_MOD
+    assert (ld.cpu().numpy()[1, 5:] == 0).all()
+
+
+def test_energy_bucketize_embed_exact(vtts):
+    from visual_onoma_to_wave_amd import ops
+    g = golden("bucketize")
+    va = vtts.variance_adaptor
+    vals = cuda(g["values"]).reshape(1, -1)
+    n = vals.shape[1]
+    h = torch.zeros((1, n, 256), device="cuda")
+    x = torch.zeros((1, n, 256), device="cuda")
+    _, idx = ops.energy_head(h, torch.zeros(256, device="cuda"), 0.0, None, x,
+                             va.energy_bins.detach().float().contiguous(),
+                             va.energy_embedding.weight.detach().float().contiguous(), target=vals,
+                             want_index=True)
+    np.testing.assert_array_equal(idx.cpu().numpy()[0], g["index"])
+    np.testing.assert_array_equal(x.cpu().numpy()[0], g["emb"])
+
+
+@pytest.mark.parametrize("tag,max_len", [("none", None), ("given", 16), ("crop", 6)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_length_regulator_exact(tag, max_len, dt):
+    from visual_onoma_to_wave_amd.model.modules import LengthRegulator
+    g = golden("length_regulator")
+    x = cuda(g["x"]).to(dt)
+    out, mel_len = LengthRegulator()(x, cuda(g["d"]), max_len)
+    np.testing.assert_array_equal(mel_len.cpu().numpy(), g["mel_len_" + tag])
+    ref = torch.from_numpy(g["out_" + tag]).to(dt).float().numpy()  # bf16: same rounding as x
+    np.testing.assert_array_equal(out.float().cpu().numpy(), ref)
+
+
+def test_length_regulator_indices_vs_oracle_large():
+    """C2-sized LR (B=32, T_src=12, D=256, 512 frames) + ragged/zero/fractional durations:
+    frame -> token indices bit-exact against the oracle."""
+    from oracle.acoustic import length_regulate
+    from visual_onoma_to_wave_amd import ops
+    rng = np.random.default_rng(5)
+    d = rng.integers(0, 90, size=(32, 12)).astype(np.float32) + rng.choice([0, 0.5, 0.99], size=(32, 12))
+    d[3] = 0
+    d[7, ::2] = -1.0
+    x = rng.normal(size=(32, 12, 256)).astype(np.float32)
+    ref_out, ref_len, ref_idx = length_regulate(torch.from_numpy(x), d, 512)
+    out, mel_len, idx = ops.length_regulate(cuda(x), cuda(d), 512, want_index=True)
+    np.testing.assert_array_equal(mel_len.cpu().numpy(), ref_len.numpy())
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref_out.numpy())
+
+
+def test_mask_exact():
+    from visual_onoma_to_wave_amd.utils.tools import get_mask_from_lengths
+    g = golden("mask")
+    np.testing.assert_array_equal(get_mask_from_lengths(cuda(g["lens"])).cpu().numpy(), g["mask_none"])
+    np.testing.assert_array_equal(get_mask_from_lengths(cuda(g["lens"]), 9).cpu().numpy(), g["mask_9"])
+    np.testing.assert_array_equal(get_mask_from_lengths(cuda(g["lens"]).float(), 9).cpu().numpy(), g["mask_9"])
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, BF16)])
+def test_postnet(vtts, dt, tol):
+    g = golden("postnet")
+    vtts.postnet.set_compute_dtype(dt)
+    with torch.no_grad():
+        out = vtts.postnet(cuda(g["x"]))
+    assert rel_l2(out.cpu(), g["out"]) < tol
+
+
+# ------------------------------------------------------------------------------ whole acoustic model
+
+NAMES = ["mel", "postnet_mel", "e_pred", "k_pred", "log_d_pred", "d_rounded",
+         "src_masks", "mel_masks", "src_lens_out", "mel_lens_out"]
+
+
+def _run_vtts(m, g, teacher):
+    kw = {}
+    if teacher:
+        args = (cuda(g["in_audiotypes"]), cuda(g["in_texts"]), cuda(g["in_src_lens"]), int(g["in_max_src_len"]),
+                cuda(g["in_mels"]), cuda(g["in_mel_lens"]), int(g["in_max_mel_len"]), cuda(g["in_e_targets"]),
+                None, cuda(g["in_d_targets"]), cuda(g["in_images"]), None, True)
+    else:
+        args = (cuda(g["in_audiotypes"]), cuda(g["in_texts"]), cuda(g["in_src_lens"]), int(g["in_max_src_len"]),
+                None, None, None, None, None, None, cuda(g["in_images"]), None, True)
+        kw = dict(e_control=float(g["e_control"]), d_control=float(g["d_control"]))
+    with torch.no_grad():
+        return m(*args, **kw)
+
+
+def _check(out, g, tol):
+    for n, o in zip(NAMES, out):
+        if o is None:
+            assert n not in g, n
+            continue
+        o = o.cpu()
+        if o.dtype in (torch.bool, torch.int64) or n == "d_rounded":
+            np.testing.assert_array_equal(o.numpy(), g[n], err_msg=n)
+        else:
+            assert rel_l2(o, g[n]) < tol, (n, rel_l2(o, g[n]))
+
+
+@pytest.mark.parametrize("mode,tol", [("fp32", F32_MODEL), ("mixed", BF16), ("bf16", 5e-2)])
+def test_vtts_teacher_forced(vtts, mode, tol):
+    _prec(vtts, mode)
+    g = golden("vtts_tf")
+    _check(_run_vtts(vtts, g, True), g, tol)
+
+
+@pytest.mark.parametrize("tag", ["inf", "inf_ctrl"])
+@pytest.mark.parametrize("mode", ["fp32", "mixed"])
+def test_vtts_inference(vtts, tag, mode):
+    """Predicted energy bins and durations: d_rounded / mel_len / masks exact (the
+    encoder and variance adaptor run fp32 in both modes)."""
+    _prec(vtts, mode)
+    g = golden("vtts_" + tag)
+    b = vtts.variance_adaptor.duration_predictor.linear_layer.bias
+    with torch.no_grad():
+        b += float(g["dur_bias_shift"])
+    try:
+        _check(_run_vtts(vtts, g, False), g, F32_MODEL if mode == "fp32" else BF16)
+    finally:
+        with torch.no_grad():
+            b -= float(g["dur_bias_shift"])
+
+
+# ------------------------------------------------------------------------------ vocoder
+
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, BF16)])
+def test_resblocks(gen, stage, dt, tol):
+    g = golden(f"resblock_s{stage}")
+    for j, k in enumerate((3, 7, 11)):
+        rb = gen.resblocks[3 * stage + j]
+        rb.set_compute_dtype(dt)
+        with torch.no_grad():
+            out = rb(cuda(g["x"]))
+        assert rel_l2(out.cpu(), g[f"k{k}"]) < tol, (stage, k)
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, BF16)])
+def test_upsamplers(gen, dt, tol):
+    from visual_onoma_to_wave_amd import ops
+    g = golden("ups")
+    h = hifigan_h()
+    gen.set_compute_dtype(dt)
+    p = gen._packed(torch.device("cuda"), gen._build)
+    for i, (u, k) in enumerate(zip(h["upsample_rates"], h["upsample_kernel_sizes"])):
+        w, b, cout, uu, pad = p["ups"][i]
+        x = ops.transpose_bct(cuda(g[f"x{i}"]), dt)
+        y = ops.conv1d(x, w, b, Co=u * cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=0.1,
+                       transposed=dict(stride=u, pad=pad, cout=cout), out_dtype=torch.float32,
+                       compute_dtype=dt)
+        ref = g[f"y{i}"]
+        assert y.shape == (1, ref.shape[2], ref.shape[1])
+        assert rel_l2(y.cpu().numpy().transpose(0, 2, 1), ref) < tol, i
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MODEL), (torch.bfloat16, BF16)])
+def test_generator(gen, dt, tol):
+    g = golden("generator")
+    gen.set_compute_dtype(dt)
+    with torch.no_grad():
+        wav = gen(cuda(g["mel"]))
+    assert wav.shape == g["wav"].shape
+    assert rel_l2(wav.cpu(), g["wav"]) < tol
+
+
+# ------------------------------------------------------------------------------ kernels vs oracle
+
+@pytest.mark.parametrize("B,T,Ci,Co,K,dil,act", [
+    (2, 300, 256, 256, 3, 1, 0), (3, 257, 128, 128, 7, 3, 2), (2, 1000, 64, 64, 11, 5, 2),
+    (1, 777, 32, 32, 11, 5, 2), (4, 100, 256, 1024, 9, 1, 1), (2, 64, 1024, 256, 1, 1, 0),
+    (2, 50, 80, 512, 7, 1, 0), (2, 33, 512, 80, 5, 1, 0), (1, 384, 2448, 256, 1, 1, 1)])
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])
+def test_conv1d_vs_torch_fp32(B, T, Ci, Co, K, dil, act, dt, tol):
+    """The implicit-GEMM conv against the plain PyTorch fp32 op (CPU) on the same data."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    x = torch.randn(B, T, Ci, generator=g)
+    w = torch.randn(Co, Ci, K, generator=g) / (Ci * K) ** 0.5
+    b = torch.randn(Co, generator=g) * 0.1
+    res = torch.randn(B, T, Co, generator=g)
+    pad = dil * (K - 1) // 2
+    xin = F.leaky_relu(x, 0.1) if act == 2 else x
+    ref = F.conv1d(xin.transpose(1, 2), w, b, padding=pad, dilation=dil).transpose(1, 2)
+    if act == 1:
+        ref = F.relu(ref)
+    ref = (ref + res) * 0.5
+    wp = ops.pack_conv_weight(w.cuda(), dt)
+    out = ops.conv1d(x.cuda().to(dt) if dt == torch.bfloat16 else x.cuda(), wp, b.cuda(), Co=Co, K=K, dil=dil,
+                     pad=pad, pre_act=ops.ACT_LRELU if act == 2 else 0, pre_slope=0.1,
+                     post_act=ops.ACT_RELU if act == 1 else 0, res1=res.cuda(), out_scale=0.5,
+                     out_dtype=torch.float32, compute_dtype=dt)
+    assert rel_l2(out.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("B,L,lens", [(4, 512, [512, 300, 1, 77]), (2, 1000, [1000, 999]), (3, 12, [12, 7, 5])])
+@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])
+def test_attention_vs_oracle(B, L, lens, dt, tol):
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(L)
+    qkv = torch.randn(B, L, 768, generator=g)
+    lens_t = torch.tensor(lens, dtype=torch.int32)
+    q, k, v = qkv.split(256, dim=-1)
+    ref = torch.zeros(B, L, 256)
+    for h in range(2):
+        s = q[..., h * 128:(h + 1) * 128] @ k[..., h * 128:(h + 1) * 128].transpose(1, 2) / 128 ** 0.5
+        s = s.masked_fill(torch.arange(L)[None, None, :] >= lens_t[:, None, None], -float("inf"))
+        ref[..., h * 128:(h + 1) * 128] = torch.softmax(s, -1) @ v[..., h * 128:(h + 1) * 128]
+    out = ops.attention(qkv.cuda().to(dt), lens_t.cuda(), 2)
+    assert rel_l2(out.float().cpu(), ref) < tol

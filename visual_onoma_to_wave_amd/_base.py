@@ -1,0 +1,57 @@
+"""Shared machinery of the HIP-backed nn.Modules.
+
+Each module keeps its parameters in the reference's checkpoint layout (same attribute
+names, shapes and state-dict keys) and, on first use on a device, packs them once into
+the layout its kernels read (``[K][Co][Ci]``, BatchNorm / weight-norm folded, fused
+QKV ...).  The pack is cached per (device, compute dtype) and rebuilt only when a
+parameter's version counter moves (load_state_dict, optimizer step).
+
+Precision ("compute dtype") is a per-module attribute:
+  * torch.float32  -- exact-f32 MFMA everywhere (the parity mode);
+  * torch.bfloat16 -- bf16 MFMA with fp32 accumulation, bf16 activations in HBM.
+``vTTS.set_precision("mixed")`` (the default) keeps the encoder and variance adaptor in
+fp32 -- their outputs feed the discontinuous bucketize / round steps (SURVEY.md section 7,
+hard part 1) -- and runs the decoder, PostNet and vocoder in bf16.
+"""
+
+import torch
+import torch.nn as nn
+
+
+class HipModule(nn.Module):
+    compute_dtype = torch.bfloat16
+
+    def _params_version(self):
+        return tuple(p._version for p in self.parameters()) + tuple(
+            b._version for b in self.buffers())
+
+    def _packed(self, device, builder, dtype=None):
+        dtype = dtype or self.compute_dtype
+        key = (str(device), dtype, self._params_version())
+        cache = self.__dict__.setdefault("_pack_cache", {})
+        hit = cache.get("key")
+        if hit != key:
+            cache.clear()
+            cache["key"] = key
+            with torch.no_grad():
+                cache["val"] = builder(device, dtype)
+        return cache["val"]
+
+    def set_compute_dtype(self, dtype):
+        for m in self.modules():
+            if isinstance(m, HipModule):
+                m.compute_dtype = dtype
+        return self
+
+    def _check_inference(self):
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                f"{type(self).__name__}: the HIP path implements inference (eval / no_grad); "
+                "training goes through visual_onoma_to_wave_amd.train")
+
+
+def fold_bn(bn):
+    """Eval-mode BatchNorm as (scale, shift): y = x * scale + shift."""
+    scale = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+    shift = bn.bias.detach().float() - bn.running_mean.detach().float() * scale
+    return scale, shift

@@ -1,0 +1,112 @@
+"""ctypes binding of lib/libvonoma.so (the C ABI declared in include/vonoma.h).
+
+The product path has NO fallback: if the library is missing or cannot be loaded,
+every op raises.  Build it with ``make -C visual_onoma_to_wave_amd -j8`` (or
+``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvonoma.so")
+
+VO_F32, VO_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
+PACK_CONV, PACK_CONVT = 0, 1
+HEAD_DURATION, HEAD_ENERGY = 0, 1
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_int64 = ctypes.c_int64
+
+
+class Conv1dDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("x_dtype", c_int), ("x_bstride", c_int64), ("ldx", c_int),
+        ("w", c_void_p), ("bias", c_void_p),
+        ("y", c_void_p), ("y_dtype", c_int), ("y_bstride", c_int64), ("ldy", c_int),
+        ("res1", c_void_p), ("res2", c_void_p),
+        ("B", c_int), ("T_in", c_int), ("T_out", c_int),
+        ("Ci", c_int), ("Co", c_int),
+        ("K", c_int), ("dil", c_int), ("pad", c_int),
+        ("pre_act", c_int), ("pre_slope", c_float),
+        ("post_act", c_int), ("post_slope", c_float),
+        ("out_scale", c_float),
+        ("compute_dtype", c_int),
+        ("transposed", c_int), ("up_stride", c_int), ("up_pad", c_int), ("up_cout", c_int),
+        ("up_tout", c_int),
+    ]
+
+
+class HeadDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int),
+        ("h", c_void_p), ("h_dtype", c_int),
+        ("w", c_void_p), ("b", c_float),
+        ("lens", c_void_p),
+        ("B", c_int), ("T", c_int), ("D", c_int),
+        ("pred", c_void_p),
+        ("d_round", c_void_p), ("d_control", c_float),
+        ("target", c_void_p),
+        ("bins", c_void_p), ("n_bins", c_int),
+        ("e_mean", c_float), ("e_std", c_float), ("e_control", c_float),
+        ("table", c_void_p),
+        ("x", c_void_p), ("x_dtype", c_int),
+        ("idx_out", c_void_p),
+    ]
+
+
+_SIGNATURES = {
+    "vo_last_error": (ctypes.c_char_p, []),
+    "vo_version": (c_int, []),
+    "vo_num_symbols": (c_int, []),
+    "vo_symbol_name": (ctypes.c_char_p, [c_int]),
+    "vo_conv1d": (c_int, [ctypes.POINTER(Conv1dDesc), c_void_p]),
+    "vo_pack_weight": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                               c_void_p, c_int, c_void_p]),
+    "vo_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                             c_int, c_int, c_float, c_void_p, c_int, c_void_p]),
+    "vo_attention": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                             c_void_p, c_void_p]),
+    "vo_length_regulate": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                   c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_lr_lengths": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_variance_head": (c_int, [ctypes.POINTER(HeadDesc), c_void_p]),
+    "vo_vfe_stencil": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               c_int, c_void_p, c_int, c_void_p]),
+    "vo_add_pos_class": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                 c_int, c_void_p]),
+    "vo_mask_from_lengths": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_conv_post": (c_int, [c_void_p, c_int, c_void_p, c_float, c_int, c_int, c_int, c_int, c_float,
+                             c_void_p, c_void_p]),
+    "vo_transpose_bct": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "vo_stft_mel": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float,
+                            c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libvonoma.so once; raise (no fallback) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"visual_onoma_to_wave_amd: HIP library not built ({LIB_PATH} missing); run "
+                "`make -C visual_onoma_to_wave_amd -j8` -- there is no CPU fallback")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().vo_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")

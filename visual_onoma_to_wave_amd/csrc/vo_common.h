@@ -1,0 +1,153 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of the synthesis path.
+// Wave = 64 lanes; MFMA 16x16x32 bf16 (or 8 x 16x16x4 f32 in the fp32 parity mode).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "../../include/vonoma.h"
+
+typedef unsigned short bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace vo {
+
+// ---------------------------------------------------------------- scalar conversion
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float x) {
+  __hip_bfloat16 b = __float2bfloat16(x);  // round-to-nearest-even, NaN stays NaN
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+// ---------------------------------------------------------------- 8-element vectors
+// Load 8 consecutive elements (16 B for bf16, 32 B for f32) as floats.
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)from_f32<bf16_t>(v[2 * i]) | ((uint32_t)from_f32<bf16_t>(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void store4(bf16_t* p, const float (&v)[4]) {
+  uint32_t a = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
+  uint32_t b = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
+}
+__device__ __forceinline__ void store4(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void load4(const bf16_t* p, float (&v)[4]) {
+  uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void load4(const float* p, float (&v)[4]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+
+// ---------------------------------------------------------------- MFMA fragments
+// A fragment holds A[row = lane&15][k = 8*(lane>>4) + j], B holds B[k = 8*(lane>>4)+j][col = lane&15]
+// (j = 0..7).  For bf16 that is exactly one v_mfma_f32_16x16x32_bf16.  For f32 the same
+// 32-deep k-slice is split into 8 v_mfma_f32_16x16x4_f32 whose k index (lane>>4) maps to
+// k = 8*(lane>>4) + j -- any consistent k permutation of A and B gives the same sum.
+template <typename TC> struct Frag;
+template <> struct Frag<bf16_t> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (__bf16)0.0f;
+  }
+};
+template <> struct Frag<float> {
+  float v[8];
+  __device__ __forceinline__ void load(const float* p) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+};
+
+__device__ __forceinline__ f32x4 mfma(const Frag<bf16_t>& a, const Frag<bf16_t>& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
+  return c;
+}
+
+// ---------------------------------------------------------------- activations
+__device__ __forceinline__ float act(int kind, float x, float slope) {
+  switch (kind) {
+    case VO_ACT_RELU: return x > 0.f ? x : 0.f;
+    case VO_ACT_LRELU: return x > 0.f ? x : x * slope;
+    case VO_ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+// ---------------------------------------------------------------- wave reductions (64 lanes)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace vo
+
+// error plumbing shared by the launchers (vo_runtime.cpp)
+extern "C" void vo_set_error(const char* fmt, ...);
+
+#define VO_CHECK_ARG(cond, ...)                \
+  do {                                         \
+    if (!(cond)) {                             \
+      vo_set_error(__VA_ARGS__);               \
+      return VO_ERR_INVALID;                   \
+    }                                          \
+  } while (0)
+
+#define VO_RETURN_LAUNCH()                                       \
+  do {                                                           \
+    hipError_t e_ = hipGetLastError();                           \
+    if (e_ != hipSuccess) {                                      \
+      vo_set_error("launch failed: %s", hipGetErrorString(e_));  \
+      return (int)e_;                                            \
+    }                                                            \
+    return VO_OK;                                                \
+  } while (0)

@@ -1,0 +1,31 @@
+// Runtime plumbing of libvonoma.so: last-error string and the exported-symbol table
+// the loader test checks against include/vonoma.h.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "../../include/vonoma.h"
+
+static thread_local char g_err[512] = "";
+
+extern "C" void vo_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char* vo_last_error(void) { return g_err; }
+
+extern "C" int vo_version(void) { return 1; }
+
+static const char* const kSymbols[] = {
+    "vo_last_error",     "vo_version",       "vo_num_symbols", "vo_symbol_name",   "vo_conv1d",
+    "vo_pack_weight",    "vo_layernorm",     "vo_attention",   "vo_length_regulate", "vo_lr_lengths",
+    "vo_variance_head",  "vo_vfe_stencil",   "vo_add_pos_class", "vo_conv_post",   "vo_transpose_bct",
+    "vo_stft_mel",       "vo_mask_from_lengths",
+};
+
+extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }
+extern "C" const char* vo_symbol_name(int i) {
+  return (i >= 0 && i < vo_num_symbols()) ? kSymbols[i] : nullptr;
+}

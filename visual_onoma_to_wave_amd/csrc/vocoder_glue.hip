@@ -1,0 +1,149 @@
+// HiFi-GAN tail and layout/weight preparation kernels.
+//
+// conv_post_kernel: lrelu(0.01) -> Conv1d(C -> 1, k7, pad 3) -> tanh over channels-last
+//   activations (scripts/hifigan/models.py:161-163).  HBM-bound: C*2 bytes in, 4 out per
+//   sample; a workgroup stages 256 + K - 1 rows in LDS and every lane reduces K*C products.
+// transpose_bct_kernel: (B, C, T) fp32 mel -> channels-last (B, T, ldy), zero channel pad.
+// pack_weight_kernel: weight-norm fold (models.py:105-109,167-174), BatchNorm fold and the
+//   [K][Co][Ci] / polyphase ConvTranspose1d layouts the conv1d kernel reads.
+
+#include "vo_common.h"
+
+namespace vo {
+
+constexpr int CP_ROWS = 256;
+
+template <typename TX>
+__global__ void __launch_bounds__(256) conv_post_kernel(const TX* __restrict__ x, const float* __restrict__ w,
+                                                        float bias, int T, int C, int K, float slope,
+                                                        float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float cp_lds[];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * CP_ROWS;
+  const int pad = (K - 1) / 2;
+  const int rows = CP_ROWS + K - 1;
+  const int P = C + 1;  // odd pitch: lanes reading the same channel of consecutive rows spread banks
+  const TX* xb = x + (int64_t)b * T * C;
+  const int vpr = C / 4;
+  for (int v = threadIdx.x; v < rows * vpr; v += 256) {
+    const int r = v / vpr, c = (v - r * vpr) * 4;
+    const int t = t0 - pad + r;
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t >= 0 && t < T) {
+      load4(xb + (int64_t)t * C + c, q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = q[e] > 0.f ? q[e] : q[e] * slope;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cp_lds[r * P + c + e] = q[e];
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T) return;
+  float acc = bias;
+  for (int k = 0; k < K; ++k) {
+    const float* row = cp_lds + (threadIdx.x + k) * P;
+    const float* wk = w + k * C;
+    for (int c = 0; c < C; ++c) acc += wk[c] * row[c];
+  }
+  y[(int64_t)b * T + t] = tanhf(acc);
+}
+
+template <typename TY>
+__global__ void transpose_bct_kernel(const float* __restrict__ x, int C, int T, TY* __restrict__ y, int ldy) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, t = t0 + tx;
+    tile[k][tx] = (c < C && t < T) ? x[((int64_t)b * C + c) * T + t] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int t = t0 + k, c = c0 + tx;
+    if (t < T && c < ldy) y[((int64_t)b * T + t) * ldy + c] = from_f32<TY>(tile[tx][k]);
+  }
+}
+
+// one workgroup per dim-0 slice of src (Co for conv, Ci for transposed conv)
+template <typename TD>
+__global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ src, const float* __restrict__ g,
+                                                          const float* __restrict__ row_scale, int mode, int Co,
+                                                          int Ci, int K, int stride, TD* __restrict__ dst) {
+  __shared__ float red[4];
+  const int s0 = blockIdx.x;
+  const int n = (mode == VO_PACK_CONV) ? Ci * K : Co * K;  // elements per slice
+  const float* sp = src + (int64_t)s0 * n;
+  float mul = 1.f;
+  if (g) {
+    float ss = 0.f;
+    for (int e = threadIdx.x; e < n; e += 256) ss += sp[e] * sp[e];
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    mul = g[s0] / norm;
+  }
+  for (int e = threadIdx.x; e < n; e += 256) {
+    if (mode == VO_PACK_CONV) {
+      // src (Co, Ci, K): s0 = co, e = ci*K + k  -> dst[k][co][ci]
+      const int ci = e / K, k = e - ci * K;
+      const float rs = row_scale ? row_scale[s0] : 1.f;
+      dst[((int64_t)k * Co + s0) * Ci + ci] = from_f32<TD>(sp[e] * mul * rs);
+    } else {
+      // src (Ci, Co, 2s): s0 = ci, e = co*K + kt; tap kt = r + s*(1-kk) -> dst[kk][r*Co + co][ci]
+      const int co = e / K, kt = e - co * K;
+      const int r = kt % stride, kk = 1 - kt / stride;
+      const float rs = row_scale ? row_scale[co] : 1.f;
+      dst[((int64_t)kk * stride * Co + (int64_t)r * Co + co) * Ci + s0] = from_f32<TD>(sp[e] * mul * rs);
+    }
+  }
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int vo_conv_post(const void* x, int x_dtype, const float* w, float bias, int B, int T, int C, int K,
+                            float slope, float* y, void* stream) {
+  VO_CHECK_ARG(x && w && y, "conv_post: null pointer");
+  VO_CHECK_ARG(C % 4 == 0 && K % 2 == 1 && C <= 512 && K <= 31, "conv_post: C=%d K=%d unsupported", C, K);
+  VO_CHECK_ARG(B > 0 && T > 0, "conv_post: empty");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)((T + CP_ROWS - 1) / CP_ROWS), (unsigned)B);
+  const size_t lds = (size_t)(CP_ROWS + K - 1) * (C + 1) * sizeof(float);
+  if (x_dtype == VO_BF16)
+    hipLaunchKernelGGL(conv_post_kernel<bf16_t>, grid, dim3(256), lds, st, (const bf16_t*)x, w, bias, T, C, K, slope, y);
+  else
+    hipLaunchKernelGGL(conv_post_kernel<float>, grid, dim3(256), lds, st, (const float*)x, w, bias, T, C, K, slope, y);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_transpose_bct(const float* x, int B, int C, int T, void* y, int y_dtype, int ldy, void* stream) {
+  VO_CHECK_ARG(x && y && ldy >= C, "transpose_bct: bad arguments");
+  if (B == 0 || T == 0) return VO_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)((T + 31) / 32), (unsigned)((ldy + 31) / 32), (unsigned)B);
+  if (y_dtype == VO_BF16)
+    hipLaunchKernelGGL(transpose_bct_kernel<bf16_t>, grid, dim3(256), 0, st, x, C, T, (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(transpose_bct_kernel<float>, grid, dim3(256), 0, st, x, C, T, (float*)y, ldy);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_pack_weight(const float* src, const float* g, const float* row_scale, int mode, int Co, int Ci,
+                              int K, int stride, void* dst, int dst_dtype, void* stream) {
+  VO_CHECK_ARG(src && dst, "pack_weight: null pointer");
+  VO_CHECK_ARG(mode == VO_PACK_CONV || (mode == VO_PACK_CONVT && stride >= 1 && K == 2 * stride),
+               "pack_weight: bad mode/stride (K must be 2*stride for ConvTranspose1d)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)(mode == VO_PACK_CONV ? Co : Ci));
+  if (dst_dtype == VO_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, grid, dim3(256), 0, st, src, g, row_scale, mode, Co, Ci, K, stride,
+                       (bf16_t*)dst);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, grid, dim3(256), 0, st, src, g, row_scale, mode, Co, Ci, K, stride,
+                       (float*)dst);
+  VO_RETURN_LAUNCH();
+}

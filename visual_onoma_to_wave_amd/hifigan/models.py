@@ -1,0 +1,165 @@
+"""HiFi-GAN V1 generator on HIP kernels (reference: scripts/hifigan/models.py:20-174).
+
+Parameters are registered exactly as the reference registers them (weight-normed
+Conv1d / ConvTranspose1d: ``weight_g`` / ``weight_v`` + ``bias``) so the "universal"
+checkpoint's 234 keys load unchanged; ``remove_weight_norm()`` folds them like the
+reference.  The forward never calls the torch modules: each conv is one channels-last
+implicit-GEMM MFMA launch (``vo_conv1d``) with the leaky-ReLU applied while staging
+its input, the ResBlock residual / MRF sum / 1/num_kernels scale in its epilogue, and
+each ConvTranspose1d upsampler in its polyphase form.
+"""
+
+import warnings
+
+import torch
+import torch.nn as nn
+from torch.nn import Conv1d, ConvTranspose1d
+
+from .. import ops
+from .._base import HipModule
+
+LRELU_SLOPE = 0.1
+
+with warnings.catch_warnings():
+    warnings.simplefilter("ignore")
+    from torch.nn.utils import remove_weight_norm, weight_norm
+
+
+def init_weights(m, mean=0.0, std=0.01):
+    if "Conv" in m.__class__.__name__:
+        m.weight.data.normal_(mean, std)
+
+
+def get_padding(kernel_size, dilation=1):
+    return int((kernel_size * dilation - dilation) / 2)
+
+
+def _wn(conv):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return weight_norm(conv)
+
+
+def _weight_and_gain(m):
+    """(v, g) when weight-normed, else (weight, None)."""
+    if hasattr(m, "weight_v"):
+        return m.weight_v, m.weight_g
+    return m.weight, None
+
+
+def _pack(m, device, dtype, transposed_stride=None):
+    v, g = _weight_and_gain(m)
+    w = ops.pack_conv_weight(v.to(device), dtype, g=None if g is None else g.to(device),
+                             transposed_stride=transposed_stride)
+    return w, m.bias.detach().float().to(device).contiguous()
+
+
+class ResBlock(HipModule):
+    """ResBlock1: for d in dilations: x = c2(lrelu(c1_d(lrelu(x)))) + x."""
+
+    def __init__(self, h, channels, kernel_size=3, dilation=(1, 3, 5)):
+        super().__init__()
+        self.h, self.channels, self.kernel_size, self.dilation = h, channels, kernel_size, tuple(dilation)
+        self.convs1 = nn.ModuleList(
+            _wn(Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
+            for d in self.dilation)
+        self.convs1.apply(init_weights)
+        self.convs2 = nn.ModuleList(
+            _wn(Conv1d(channels, channels, kernel_size, 1, dilation=1, padding=get_padding(kernel_size, 1)))
+            for _ in self.dilation)
+        self.convs2.apply(init_weights)
+
+    def _build(self, device, dtype):
+        return [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
+
+    def run(self, x, out=None, out_scale=1.0, accumulate=None):
+        """x (B, T, C) channels-last -> ResBlock(x) * out_scale (+ accumulate), written to out."""
+        packs = self._packed(x.device, self._build)
+        k, C = self.kernel_size, self.channels
+        cur = x
+        for n, (d, ((w1, b1), (w2, b2))) in enumerate(zip(self.dilation, packs)):
+            t = ops.conv1d(cur, w1, b1, Co=C, K=k, dil=d, pad=get_padding(k, d), pre_act=ops.ACT_LRELU,
+                           pre_slope=LRELU_SLOPE, post_act=ops.ACT_LRELU, post_slope=LRELU_SLOPE,
+                           compute_dtype=self.compute_dtype, out_dtype=x.dtype)
+            last = n == len(self.dilation) - 1
+            cur = ops.conv1d(t, w2, b2, Co=C, K=k, pad=get_padding(k, 1), res1=cur,
+                             out=out if last else None, out_scale=out_scale if last else 1.0,
+                             res2=accumulate if last else None, compute_dtype=self.compute_dtype,
+                             out_dtype=x.dtype)
+        return cur
+
+    def forward(self, x):
+        self._check_inference()
+        xc = ops.transpose_bct(x, self.compute_dtype)
+        y = self.run(xc)
+        return ops.transpose_bct(y.float(), torch.float32)
+
+    def remove_weight_norm(self):
+        for m in list(self.convs1) + list(self.convs2):
+            remove_weight_norm(m)
+
+
+class Generator(HipModule):
+    def __init__(self, h):
+        super().__init__()
+        self.h = h
+        self.num_kernels = len(h.resblock_kernel_sizes)
+        self.num_upsamples = len(h.upsample_rates)
+        c0 = h.upsample_initial_channel
+        self.conv_pre = _wn(Conv1d(80, c0, 7, 1, padding=3))
+        self.ups = nn.ModuleList(
+            _wn(ConvTranspose1d(c0 // 2 ** i, c0 // 2 ** (i + 1), k, u, padding=(k - u) // 2))
+            for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)))
+        self.resblocks = nn.ModuleList(
+            ResBlock(h, c0 // 2 ** (i + 1), k, d)
+            for i in range(len(self.ups))
+            for k, d in zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes))
+        self.conv_post = _wn(Conv1d(c0 // 2 ** len(self.ups), 1, 7, 1, padding=3))
+        self.ups.apply(init_weights)
+        self.conv_post.apply(init_weights)
+
+    def _build(self, device, dtype):
+        ups = []
+        for m, u, k in zip(self.ups, self.h.upsample_rates, self.h.upsample_kernel_sizes):
+            if k != 2 * u:
+                raise NotImplementedError("polyphase ConvTranspose1d needs kernel = 2 * stride")
+            ups.append(_pack(m, device, dtype, transposed_stride=u) + (m.out_channels, u, (k - u) // 2))
+        v, g = _weight_and_gain(self.conv_post)
+        wpost = ops.pack_conv_weight(v.to(device), torch.float32, g=None if g is None else g.to(device))
+        return dict(pre=_pack(self.conv_pre, device, dtype), ups=ups,
+                    post=(wpost.reshape(wpost.shape[0], -1).contiguous(),
+                          float(self.conv_post.bias.detach().float().cpu())))
+
+    def run(self, mel_cl):
+        """mel_cl (B, T, 80) channels-last (fp32 or compute dtype) -> wav (B, 256*T) fp32."""
+        p = self._packed(mel_cl.device, self._build)
+        dt = self.compute_dtype
+        w, b = p["pre"]
+        x = ops.conv1d(mel_cl, w, b, Co=w.shape[1], K=7, pad=3, out_dtype=dt, compute_dtype=dt)
+        for i in range(self.num_upsamples):
+            w, b, cout, u, pad = p["ups"][i]
+            x = ops.conv1d(x, w, b, Co=u * cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=LRELU_SLOPE,
+                           transposed=dict(stride=u, pad=pad, cout=cout), out_dtype=dt, compute_dtype=dt)
+            xs = torch.empty_like(x)
+            for j in range(self.num_kernels):
+                rb = self.resblocks[i * self.num_kernels + j]
+                rb.compute_dtype = dt
+                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None)
+            x = xs
+        wk, bp = p["post"]
+        return ops.conv_post(x, wk, bp, slope=0.01)
+
+    def forward(self, x):
+        """x (B, 80, T) mel -> (B, 1, 256 * T) waveform (reference: models.py:149-165)."""
+        self._check_inference()
+        mel_cl = ops.transpose_bct(x, torch.float32)
+        return self.run(mel_cl).unsqueeze(1)
+
+    def remove_weight_norm(self):
+        print("Removing weight norm...")
+        for m in self.ups:
+            remove_weight_norm(m)
+        for rb in self.resblocks:
+            rb.remove_weight_norm()
+        remove_weight_norm(self.conv_pre)
+        remove_weight_norm(self.conv_post)

@@ -1,0 +1,48 @@
+"""Adam with the Noam warm-up / step-anneal schedule (reference: scripts/model/optimizer.py:5-51).
+
+lr(step) = init_lr * min(step^-0.5, warmup^-1.5 * step) * anneal_rate^#{anneal steps < step},
+evaluated after the step counter is incremented; Adam(betas, eps, weight_decay) from the
+train config.  ``fused=True`` runs Adam as one multi-tensor kernel per step on the GPU.
+"""
+
+import numpy as np
+import torch
+
+
+class ScheduledOptim:
+    def __init__(self, model, train_config, model_config, current_step):
+        o = train_config["optimizer"]
+        params = [p for p in model.parameters() if p.requires_grad]
+        kw = dict(betas=o["betas"], eps=o["eps"], weight_decay=o["weight_decay"])
+        if params and params[0].is_cuda:
+            kw["fused"] = True
+        self._optimizer = torch.optim.Adam(params, **kw)
+        self.n_warmup_steps = o["warm_up_step"]
+        self.anneal_steps = o["anneal_steps"]
+        self.anneal_rate = o["anneal_rate"]
+        self.current_step = current_step
+        self.init_lr = o["init_lr"]
+
+    def step_and_update_lr(self):
+        self._update_learning_rate()
+        self._optimizer.step()
+
+    def zero_grad(self):
+        self._optimizer.zero_grad()
+
+    def load_state_dict(self, path):
+        self._optimizer.load_state_dict(path)
+
+    def _get_lr_scale(self):
+        s = self.current_step
+        lr = min(np.power(s, -0.5), np.power(self.n_warmup_steps, -1.5) * s)
+        for a in self.anneal_steps:
+            if s > a:
+                lr = lr * self.anneal_rate
+        return lr
+
+    def _update_learning_rate(self):
+        self.current_step += 1
+        lr = self.init_lr * self._get_lr_scale()
+        for group in self._optimizer.param_groups:
+            group["lr"] = lr

@@ -1,0 +1,297 @@
+"""Torch-tensor front end of the C ABI: shape checks, output allocation, stream plumbing.
+
+Every function here launches a hand-written HIP kernel from ``lib/libvonoma.so`` on
+the current torch stream of the tensors' device.  Tensors must be CUDA (ROCm)
+tensors; there is no CPU path -- a CPU tensor raises.
+"""
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, HEAD_DURATION, HEAD_ENERGY,  # noqa: F401
+                   PACK_CONV, PACK_CONVT, VO_BF16, VO_F32)
+
+_DT = {torch.float32: VO_F32, torch.bfloat16: VO_BF16}
+
+
+def vo_dtype(t):
+    try:
+        return _DT[t if isinstance(t, torch.dtype) else t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t}") from None
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    if not t.is_cuda:
+        raise RuntimeError("visual_onoma_to_wave_amd ops run on the GPU only (got a CPU tensor); "
+                           "there is no CPU fallback")
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _contig(t, name):
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+# ----------------------------------------------------------------------------- conv1d
+
+def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_dtype=None,
+           pre_act=ACT_NONE, pre_slope=0.0, post_act=ACT_NONE, post_slope=0.0, res1=None,
+           res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None):
+    """Channels-last conv: x (B, T_in, Ci) -> y (B, T_out, Co).
+
+    ``w_packed``: [K][Co][Ci] in ``compute_dtype`` (see pack_conv_weight).
+    ``transposed``: None or dict(stride=s, pad=p, cout=C_out) for the polyphase
+    ConvTranspose1d; then Co = s*C_out, K = 2, pad = 1 and y is (B, s*T_in, C_out).
+    """
+    if x.dim() == 2:
+        x = x.unsqueeze(0)
+    B, T_in, ldx = x.shape
+    if x.stride(2) != 1 or x.stride(1) != ldx:
+        raise ValueError("conv1d: x must be row-contiguous (B, T, C)")
+    Ci = w_packed.shape[2]
+    if w_packed.shape[0] != K or w_packed.shape[1] != Co:
+        raise ValueError(f"conv1d: packed weight {tuple(w_packed.shape)} != [{K}][{Co}][Ci]")
+    if w_packed.dtype != compute_dtype:
+        raise ValueError("conv1d: packed weight dtype must equal the compute dtype")
+    out_dtype = out_dtype or x.dtype
+    if transposed is not None:
+        s, p, cout = transposed["stride"], transposed["pad"], transposed["cout"]
+        T_rows = T_in + 1
+        up_tout = transposed.get("tout", T_in * s + s - 2 * p)
+        shape = (B, up_tout, cout)
+        ldy = cout
+    else:
+        T_rows = T_out if T_out is not None else T_in + 2 * pad - dil * (K - 1)
+        shape = (B, T_rows, Co)
+        ldy = Co
+    if out is None:
+        out = torch.empty(shape, dtype=out_dtype, device=x.device)
+    if out.dim() == 2:
+        out = out.unsqueeze(0)
+    _contig(out, "out")
+    if res1 is not None and (res1.shape != out.shape or res1.dtype != out.dtype):
+        raise ValueError("conv1d: res1 must match the output")
+    if res2 is not None and (res2.shape != out.shape or res2.dtype != out.dtype):
+        raise ValueError("conv1d: res2 must match the output")
+    d = _lib.Conv1dDesc()
+    d.x = x.data_ptr(); d.x_dtype = vo_dtype(x); d.x_bstride = x.stride(0); d.ldx = ldx
+    d.w = w_packed.data_ptr(); d.bias = bias.data_ptr() if bias is not None else None
+    d.y = out.data_ptr(); d.y_dtype = vo_dtype(out); d.y_bstride = out.stride(0); d.ldy = ldy
+    d.res1 = res1.data_ptr() if res1 is not None else None
+    d.res2 = res2.data_ptr() if res2 is not None else None
+    d.B, d.T_in, d.T_out, d.Ci, d.Co = B, T_in, T_rows, Ci, Co
+    d.K, d.dil, d.pad = K, dil, pad
+    d.pre_act, d.pre_slope, d.post_act, d.post_slope = pre_act, pre_slope, post_act, post_slope
+    d.out_scale = out_scale
+    d.compute_dtype = vo_dtype(compute_dtype)
+    if transposed is not None:
+        d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
+    _lib.check(_lib.lib().vo_conv1d(ctypes.byref(d), _stream(x)), "vo_conv1d")
+    return out
+
+
+def pack_conv_weight(w, dtype, g=None, row_scale=None, transposed_stride=None):
+    """(Co, Ci, K) Conv1d weight (or (Ci, Co, 2s) ConvTranspose1d weight) -> packed.
+
+    g: weight-norm gains (one per dim-0 slice), row_scale: per-output-channel multiplier.
+    Returns [K][Co][Ci] (conv) or [2][s*Co][Ci] (transposed) in ``dtype``.
+    """
+    w = w.detach().float().contiguous()
+    if transposed_stride is None:
+        Co, Ci, K = w.shape
+        out = torch.empty((K, Co, Ci), dtype=dtype, device=w.device)
+        mode, stride = PACK_CONV, 1
+    else:
+        Ci, Co, K = w.shape
+        s = transposed_stride
+        out = torch.empty((2, s * Co, Ci), dtype=dtype, device=w.device)
+        mode, stride = PACK_CONVT, s
+    g = None if g is None else g.detach().float().reshape(-1).contiguous()
+    rs = None if row_scale is None else row_scale.detach().float().reshape(-1).contiguous()
+    _lib.check(_lib.lib().vo_pack_weight(_ptr(w), _ptr(g), _ptr(rs), mode, Co, Ci, K, stride,
+                                         _ptr(out), vo_dtype(dtype), _stream(w)), "vo_pack_weight")
+    return out
+
+
+# ----------------------------------------------------------------------------- layer norm
+
+def layernorm(x, gamma, beta, res=None, lens=None, out=None, out_dtype=None, eps=1e-5):
+    """y = LN(x + res) * gamma + beta, rows t >= lens[b] zeroed.  x: (B, T, D)."""
+    if x.dim() == 2:
+        x = x.unsqueeze(0)
+    B, T, D = x.shape
+    _contig(x, "x")
+    if res is not None:
+        _contig(res, "res")
+        if res.shape != x.shape:
+            raise ValueError("layernorm: res shape mismatch")
+    out = out if out is not None else torch.empty(x.shape, dtype=out_dtype or x.dtype, device=x.device)
+    _lib.check(_lib.lib().vo_layernorm(
+        _ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res) if res is not None else vo_dtype(x),
+        _ptr(gamma), _ptr(beta), _ptr(lens), B, T, D, eps, _ptr(out), vo_dtype(out), _stream(x)),
+        "vo_layernorm")
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+
+def attention(qkv, lens, n_head, out=None):
+    """qkv (B, L, 3D) -> (B, L, D); keys t >= lens[b] masked."""
+    _contig(qkv, "qkv")
+    B, L, D3 = qkv.shape
+    D = D3 // 3
+    dk = D // n_head
+    out = out if out is not None else torch.empty((B, L, D), dtype=qkv.dtype, device=qkv.device)
+    scale = 1.0 / float(dk) ** 0.5
+    _lib.check(_lib.lib().vo_attention(_ptr(qkv), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
+                                       scale, _ptr(out), _stream(qkv)), "vo_attention")
+    return out
+
+
+# ----------------------------------------------------------------------------- length regulator
+
+def lr_lengths(dur):
+    """(B, T) float durations -> (mel_len int64 (B,), mel_len int32 (B,))."""
+    dur = _contig(dur.float(), "dur")
+    B, T = dur.shape
+    m64 = torch.empty(B, dtype=torch.int64, device=dur.device)
+    m32 = torch.empty(B, dtype=torch.int32, device=dur.device)
+    _lib.check(_lib.lib().vo_lr_lengths(_ptr(dur), B, T, _ptr(m64), _ptr(m32), _stream(dur)),
+               "vo_lr_lengths")
+    return m64, m32
+
+
+def length_regulate(x, dur, max_len, out_dtype=None, want_index=False):
+    """x (B, T_src, D), dur (B, T_src) float -> (out (B, max_len, D), mel_len int64, index)."""
+    _contig(x, "x")
+    dur = _contig(dur.float(), "dur")
+    B, T, D = x.shape
+    out = torch.empty((B, max_len, D), dtype=out_dtype or x.dtype, device=x.device)
+    mel_len = torch.empty(B, dtype=torch.int64, device=x.device)
+    index = torch.empty((B, max_len), dtype=torch.int32, device=x.device) if want_index else None
+    _lib.check(_lib.lib().vo_length_regulate(_ptr(x), vo_dtype(x), _ptr(dur), B, T, D, max_len,
+                                             _ptr(out), vo_dtype(out), _ptr(mel_len), _ptr(index),
+                                             _stream(x)), "vo_length_regulate")
+    return out, mel_len, index
+
+
+# ----------------------------------------------------------------------------- variance heads
+
+def duration_head(h, w, b, lens, d_control=1.0, want_round=True):
+    B, T, D = h.shape
+    pred = torch.empty((B, T), dtype=torch.float32, device=h.device)
+    dr = torch.empty((B, T), dtype=torch.float32, device=h.device) if want_round else None
+    d = _lib.HeadDesc()
+    d.kind = HEAD_DURATION
+    d.h, d.h_dtype = h.data_ptr(), vo_dtype(h)
+    d.w, d.b = w.data_ptr(), float(b)
+    d.lens = lens.data_ptr() if lens is not None else None
+    d.B, d.T, d.D = B, T, D
+    d.pred = pred.data_ptr()
+    d.d_round = dr.data_ptr() if dr is not None else None
+    d.d_control = float(d_control)
+    d.x_dtype = vo_dtype(h)
+    _lib.check(_lib.lib().vo_variance_head(ctypes.byref(d), _stream(h)), "vo_variance_head")
+    return pred, dr
+
+
+def energy_head(h, w, b, lens, x, bins, table, target=None, mean=0.0, std=1.0, control=1.0,
+                want_index=False):
+    """Energy prediction + bucketize + x += table[idx] (in place).  Returns (pred, idx)."""
+    B, T, D = h.shape
+    _contig(x, "x")
+    pred = torch.empty((B, T), dtype=torch.float32, device=h.device)
+    idx = torch.empty((B, T), dtype=torch.int32, device=h.device) if want_index else None
+    tgt = _contig(target.float(), "target") if target is not None else None
+    d = _lib.HeadDesc()
+    d.kind = HEAD_ENERGY
+    d.h, d.h_dtype = h.data_ptr(), vo_dtype(h)
+    d.w, d.b = w.data_ptr(), float(b)
+    d.lens = lens.data_ptr() if lens is not None else None
+    d.B, d.T, d.D = B, T, D
+    d.pred = pred.data_ptr()
+    d.target = tgt.data_ptr() if tgt is not None else None
+    d.bins, d.n_bins = bins.data_ptr(), bins.numel()
+    d.e_mean, d.e_std, d.e_control = float(mean), float(std), float(control)
+    d.table = table.data_ptr()
+    d.x, d.x_dtype = x.data_ptr(), vo_dtype(x)
+    d.idx_out = idx.data_ptr() if idx is not None else None
+    _lib.check(_lib.lib().vo_variance_head(ctypes.byref(d), _stream(h)), "vo_variance_head")
+    return pred, idx
+
+
+# ----------------------------------------------------------------------------- encoder glue
+
+def vfe_stencil(images, conv_params, bn_params, slice_w, out_dtype):
+    """images (B, 1, H, W) fp32 -> (B*n, H*slice_w) flattened stencil output."""
+    images = _contig(images.float(), "images")
+    B, C, H, W = images.shape
+    if C != 1:
+        raise ValueError("vfe_stencil: gray-scale (1 channel) images only")
+    n = W // slice_w
+    out = torch.empty((B * n, H * slice_w), dtype=out_dtype, device=images.device)
+    _lib.check(_lib.lib().vo_vfe_stencil(_ptr(images), B, H, W, slice_w, n, _ptr(conv_params),
+                                         _ptr(bn_params), conv_params.shape[0], _ptr(out),
+                                         vo_dtype(out), _stream(images)), "vo_vfe_stencil")
+    return out, n
+
+
+def add_pos_class(x, pe=None, cls=None, cls_idx=None, per_token=False):
+    """x (B, T, D) += pe[t] + cls[cls_idx[b]] (or cls[cls_idx[b, t]] when per_token), in place."""
+    B, T, D = x.shape
+    _contig(x, "x")
+    if cls_idx is not None:
+        cls_idx = _contig(cls_idx.long(), "cls_idx")
+    _lib.check(_lib.lib().vo_add_pos_class(_ptr(x), vo_dtype(x), _ptr(pe), _ptr(cls), _ptr(cls_idx),
+                                           1 if per_token else 0, B, T, D, _stream(x)),
+               "vo_add_pos_class")
+    return x
+
+
+_LENS_DT = {torch.float32: 0, torch.int64: 2, torch.int32: 3}
+
+
+def mask_from_lengths(lens, max_len, want_mask=True):
+    """-> (mask (B, max_len) bool, True = padding; lens int32 (B,))."""
+    lens = _contig(lens, "lens")
+    if lens.dtype not in _LENS_DT:
+        lens = lens.long()
+    B = lens.shape[0]
+    mask = torch.empty((B, max_len), dtype=torch.bool, device=lens.device) if want_mask else None
+    l32 = torch.empty(B, dtype=torch.int32, device=lens.device)
+    _lib.check(_lib.lib().vo_mask_from_lengths(_ptr(lens), _LENS_DT[lens.dtype], B, max_len,
+                                               _ptr(mask), _ptr(l32), _stream(lens)),
+               "vo_mask_from_lengths")
+    return mask, l32
+
+
+# ----------------------------------------------------------------------------- vocoder glue
+
+def conv_post(x, w_kc, bias, slope=0.01):
+    """x (B, T, C) -> tanh(conv(lrelu(x))) (B, T) fp32; w_kc (K, C) fp32."""
+    _contig(x, "x")
+    B, T, C = x.shape
+    K = w_kc.shape[0]
+    y = torch.empty((B, T), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().vo_conv_post(_ptr(x), vo_dtype(x), _ptr(w_kc), float(bias), B, T, C, K,
+                                       float(slope), _ptr(y), _stream(x)), "vo_conv_post")
+    return y
+
+
+def transpose_bct(x, out_dtype, ldy=None):
+    """(B, C, T) fp32 -> (B, T, ldy) channels-last with zero channel padding."""
+    x = _contig(x.float(), "x")
+    B, C, T = x.shape
+    ldy = ldy or C
+    y = torch.empty((B, T, ldy), dtype=out_dtype, device=x.device)
+    _lib.check(_lib.lib().vo_transpose_bct(_ptr(x), B, C, T, _ptr(y), vo_dtype(y), ldy, _stream(x)),
+               "vo_transpose_bct")
+    return y
