@@ -80,6 +80,8 @@ typedef struct vo_conv1d_desc {
   float out_scale;
   int compute_dtype;  /* VO_BF16 or VO_F32 */
   int transposed, up_stride, up_pad, up_cout, up_tout; /* polyphase ConvTranspose1d */
+  int variant;        /* 0 = generic; 1..4 = HiFi-GAN MRF stage 0..3 (bf16 I/O): a kernel
+                         instantiation of its own, so profiles attribute the stages   */
 } vo_conv1d_desc;
 int vo_conv1d(const vo_conv1d_desc* d, void* stream);
 

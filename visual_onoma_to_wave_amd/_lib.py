@@ -37,6 +37,7 @@ class Conv1dDesc(ctypes.Structure):
         ("compute_dtype", c_int),
         ("transposed", c_int), ("up_stride", c_int), ("up_pad", c_int), ("up_cout", c_int),
         ("up_tout", c_int),
+        ("variant", c_int),
     ]
 
 

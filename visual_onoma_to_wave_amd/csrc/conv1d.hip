@@ -72,7 +72,9 @@ template <> struct Raw8<float> {
 __device__ __forceinline__ void lds_store8(bf16_t* p, const float (&v)[8]) { store8(p, v); }
 __device__ __forceinline__ void lds_store8(float* p, const float (&v)[8]) { store8(p, v); }
 
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT>
+// ROLE only names the instantiation (0 = generic, 1..4 = HiFi-GAN MRF stage 0..3), so a
+// profiler attributes the vocoder's stages to distinct kernels; the code is identical.
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int ROLE>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -272,7 +274,7 @@ conv1d_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------ host dispatch
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT>
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int ROLE = 0>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -295,7 +297,7 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
     return VO_ERR_INVALID;
   }
   dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)((d->Co + BCO - 1) / BCO));
-  hipLaunchKernelGGL((conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT>), grid, dim3(WCO * WT * 64),
+  hipLaunchKernelGGL((conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, ROLE>), grid, dim3(WCO * WT * 64),
                      lds, st, a);
   VO_RETURN_LAUNCH();
 }
@@ -303,9 +305,6 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
 template <typename TIN, typename TC, typename TOUT>
 static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   const int64_t rows = (int64_t)d->B * d->T_out;
-  if (d->Co % 16 != 0 && d->Co > 32) {
-    // ragged channel counts (e.g. 80 mel bins) use the 64-wide tile with masking
-  }
   if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4>(d, st);   // 32 x 256
   if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4>(d, st);  // 64 x 256
   if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2>(d, st);  // 64 x 64
@@ -328,6 +327,9 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
                d->Co, d->ldy);
   VO_CHECK_ARG(d->dil >= 1 && (d->K - 1) * d->dil <= HALO_MAX,
                "conv1d: (K-1)*dil = %d exceeds the supported halo %d", (d->K - 1) * d->dil, HALO_MAX);
+  VO_CHECK_ARG(d->variant == 0 || (d->variant == 1 && d->Co >= 128) || (d->variant == 2 && d->Co >= 128) ||
+                   (d->variant == 3 && d->Co <= 64 && d->Co % 16 == 0) || (d->variant == 4 && d->Co <= 32),
+               "conv1d: variant %d does not fit Co=%d", d->variant, d->Co);
   if (d->transposed) {
     VO_CHECK_ARG(d->up_stride >= 1 && d->up_cout > 0 && d->Co == d->up_stride * d->up_cout &&
                      d->up_cout % 16 == 0 && d->K == 2 && d->pad == 1,
@@ -342,7 +344,15 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
     return launch_types<float, float, float>(d, st);
   }
   VO_CHECK_ARG(d->compute_dtype == VO_BF16, "conv1d: bad compute dtype");
-  if (xi == VO_BF16 && yo == VO_BF16) return launch_types<bf16_t, bf16_t, bf16_t>(d, st);
+  if (xi == VO_BF16 && yo == VO_BF16) {
+    switch (d->variant) {  // HiFi-GAN MRF stages: own instantiations (same tiles as generic)
+      case 1: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 1>(d, st);
+      case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2>(d, st);
+      case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 3>(d, st);
+      case 4: return launch_cfg<bf16_t, bf16_t, bf16_t, 2, 4, 1, 4, 4>(d, st);
+      default: return launch_types<bf16_t, bf16_t, bf16_t>(d, st);
+    }
+  }
   if (xi == VO_F32 && yo == VO_BF16) return launch_types<float, bf16_t, bf16_t>(d, st);
   if (xi == VO_BF16 && yo == VO_F32) return launch_types<bf16_t, bf16_t, float>(d, st);
   if (xi == VO_F32 && yo == VO_F32) return launch_types<float, bf16_t, float>(d, st);

@@ -72,20 +72,23 @@ class ResBlock(HipModule):
     def _build(self, device, dtype):
         return [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
 
-    def run(self, x, out=None, out_scale=1.0, accumulate=None):
-        """x (B, T, C) channels-last -> ResBlock(x) * out_scale (+ accumulate), written to out."""
+    def run(self, x, out=None, out_scale=1.0, accumulate=None, stage=None):
+        """x (B, T, C) channels-last -> ResBlock(x) * out_scale (+ accumulate), written to out.
+        ``stage`` (0..3) selects the MRF stage's own kernel instantiation and timer tag."""
+        var = 0 if stage is None else stage + 1
+        tag = None if stage is None else f"mrf_s{stage}"
         packs = self._packed(x.device, self._build)
         k, C = self.kernel_size, self.channels
         cur = x
         for n, (d, ((w1, b1), (w2, b2))) in enumerate(zip(self.dilation, packs)):
             t = ops.conv1d(cur, w1, b1, Co=C, K=k, dil=d, pad=get_padding(k, d), pre_act=ops.ACT_LRELU,
                            pre_slope=LRELU_SLOPE, post_act=ops.ACT_LRELU, post_slope=LRELU_SLOPE,
-                           compute_dtype=self.compute_dtype, out_dtype=x.dtype)
+                           compute_dtype=self.compute_dtype, out_dtype=x.dtype, variant=var, tag=tag)
             last = n == len(self.dilation) - 1
             cur = ops.conv1d(t, w2, b2, Co=C, K=k, pad=get_padding(k, 1), res1=cur,
                              out=out if last else None, out_scale=out_scale if last else 1.0,
                              res2=accumulate if last else None, compute_dtype=self.compute_dtype,
-                             out_dtype=x.dtype)
+                             out_dtype=x.dtype, variant=var, tag=tag)
         return cur
 
     def forward(self, x):
@@ -144,7 +147,8 @@ class Generator(HipModule):
             for j in range(self.num_kernels):
                 rb = self.resblocks[i * self.num_kernels + j]
                 rb.compute_dtype = dt
-                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None)
+                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
+                       stage=i if self.num_upsamples == 4 else None)
             x = xs
         wk, bp = p["post"]
         return ops.conv_post(x, wk, bp, slope=0.01)

@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, profiling
 from ._lib import (ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, HEAD_DURATION, HEAD_ENERGY,  # noqa: F401
                    PACK_CONV, PACK_CONVT, VO_BF16, VO_F32)
 
@@ -44,7 +44,8 @@ def _contig(t, name):
 
 def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_dtype=None,
            pre_act=ACT_NONE, pre_slope=0.0, post_act=ACT_NONE, post_slope=0.0, res1=None,
-           res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None):
+           res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None, variant=0,
+           tag=None):
     """Channels-last conv: x (B, T_in, Ci) -> y (B, T_out, Co).
 
     ``w_packed``: [K][Co][Ci] in ``compute_dtype`` (see pack_conv_weight).
@@ -94,7 +95,18 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     d.compute_dtype = vo_dtype(compute_dtype)
     if transposed is not None:
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
+    d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
+    timer = profiling.active()
+    ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
     _lib.check(_lib.lib().vo_conv1d(ctypes.byref(d), _stream(x)), "vo_conv1d")
+    if ev is not None:
+        esz = x.element_size()
+        flops = 2.0 * B * T_rows * Co * Ci * K
+        nbytes = (B * T_in * Ci * esz + out.numel() * out.element_size() +
+                  (res1.numel() * res1.element_size() if res1 is not None else 0) +
+                  (res2.numel() * res2.element_size() if res2 is not None else 0) +
+                  w_packed.numel() * w_packed.element_size())
+        timer.stop(tag, ev, flops, nbytes)
     return out
 
 
