@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the MRF conv kernels from two rocprofv3 --pmc passes.
+
+FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one TCC
+pass).  Per MI355X_MICROARCH.md section HBM: both are KB; on gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced streaming read, so it is doubled.  Result:
+{"mrf_s<i>": {"hbm_bytes_per_launch", "fetch_bytes", "write_bytes", "launches"}}.
+
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        m = re.search(r"conv1d_kernel<.*,\s*(\d+)>", r["Kernel_Name"])
+        if not m or m.group(1) == "0":
+            continue
+        acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main(fetch_csv, write_csv, out):
+    f = load(fetch_csv, "FETCH_SIZE")
+    w = load(write_csv, "WRITE_SIZE")
+    res = {}
+    for tag in sorted(set(f) | set(w)):
+        fb = 2.0 * 1024 * sum(f[tag]) / max(1, len(f[tag]))
+        wb = 1024 * sum(w[tag]) / max(1, len(w[tag]))
+        res[tag] = {"hbm_bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
+                    "launches": len(f[tag]),
+                    "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB -> bytes"}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
