@@ -44,6 +44,8 @@ int vo_version(void);
 /* number of entry points and their names (used by the loader test) */
 int vo_num_symbols(void);
 const char* vo_symbol_name(int i);
+/* tuning knobs for experiments ("conv_persistent": 0/1); returns VO_OK or VO_ERR_INVALID */
+int vo_tune(const char* key, int value);
 
 /* ------------------------------------------------------------------ conv1d (implicit GEMM)
  * y[b, t, co] = post( sum_{k, ci} W[k][co][ci] * pre(x[b, t*1 + k*dil - pad, ci]) + bias[co] )

@@ -24,6 +24,11 @@
 // modules.py:216-259), ResBlock (scripts/hifigan/models.py:96-103), Generator conv_pre /
 // ups (models.py:149-160).
 
+#include <string.h>
+
+#include <algorithm>
+#include <type_traits>
+
 #include "vo_common.h"
 
 namespace vo {
@@ -39,7 +44,7 @@ struct ConvArgs {
   int T_in, T_out, Ci, Co, K, dil, pad;
   int pre_act; float pre_slope; int post_act; float post_slope; float out_scale;
   int transposed, up_stride, up_pad, up_cout, up_tout;
-  int tiles_per_b;
+  int tiles_per_b, co_tiles, B;
 };
 
 template <typename T> struct Raw8;  // 8 elements of T held in registers
@@ -68,157 +73,41 @@ template <> struct Raw8<float> {
   }
 };
 
-// write 8 floats to LDS as TC
-__device__ __forceinline__ void lds_store8(bf16_t* p, const float (&v)[8]) { store8(p, v); }
-__device__ __forceinline__ void lds_store8(float* p, const float (&v)[8]) { store8(p, v); }
-
-// ROLE only names the instantiation (0 = generic, 1..4 = HiFi-GAN MRF stage 0..3), so a
-// profiler attributes the vocoder's stages to distinct kernels; the code is identical.
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int ROLE>
-__global__ void __launch_bounds__(WCO * WT * 64)
-conv1d_kernel(ConvArgs a) {
-  constexpr int NT = WCO * WT * 64;
-  constexpr int BCO = 16 * NI * WCO;
-  constexpr int BT = 16 * NJ * WT;
-  constexpr int RP = KC + 8;                  // LDS row pitch (elements)
-  constexpr int VPR = KC / 8;                 // 8-element vectors per row
-  constexpr int MAXV = ((BT + HALO_MAX) * VPR + NT - 1) / NT;
-  constexpr int WV = (BCO * VPR + NT - 1) / NT;
-
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  TC* smem = reinterpret_cast<TC*>(smem_raw);
-
-  const int halo = (a.K - 1) * a.dil;
-  const int win_rows = BT + halo;
-  TC* win_buf[2] = {smem, smem + win_rows * RP};
-  TC* w_buf[2] = {smem + 2 * win_rows * RP, smem + 2 * win_rows * RP + BCO * RP};
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wave_co0 = (wave % WCO) * 16 * NI;
-  const int wave_t0 = (wave / WCO) * 16 * NJ;
-
-  const int b = blockIdx.x / a.tiles_per_b;
-  const int t0 = (blockIdx.x % a.tiles_per_b) * BT;
-  const int co_blk = blockIdx.y * BCO;
-
-  const TIN* __restrict__ X = reinterpret_cast<const TIN*>(a.x) + (int64_t)b * a.xbs;
-  const TC* __restrict__ Wp = reinterpret_cast<const TC*>(a.w);
-  const int in_row0 = t0 - a.pad;
-  const int n_chunks = (a.Ci + KC - 1) / KC;
-  const int n_steps = n_chunks * a.K;
-
-  Raw8<TIN> win_r[MAXV];
-  Raw8<TC> w_r[WV];
-
-  auto load_window = [&](int c) {
-    const int c0 = c * KC;
-#pragma unroll
-    for (int s = 0; s < MAXV; ++s) {
-      const int v = tid + s * NT;
-      const int r = v / VPR, q = v % VPR;
-      const int t_in = in_row0 + r;
-      const int ci = c0 + q * 8;
-      if (r < win_rows && t_in >= 0 && t_in < a.T_in && ci < a.Ci)
-        win_r[s].load(X + (int64_t)t_in * a.ldx + ci);
-      else
-        win_r[s].zero();
-    }
-  };
-  auto store_window = [&](int buf) {
-#pragma unroll
-    for (int s = 0; s < MAXV; ++s) {
-      const int v = tid + s * NT;
-      const int r = v / VPR, q = v % VPR;
-      if (r < win_rows) {
-        float f[8];
-        win_r[s].to_f32(f);
-        if (a.pre_act != VO_ACT_NONE) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = act(a.pre_act, f[e], a.pre_slope);
-        }
-        lds_store8(win_buf[buf] + r * RP + q * 8, f);
-      }
-    }
-  };
-  auto load_w = [&](int c, int k) {
-    const int c0 = c * KC;
-#pragma unroll
-    for (int s = 0; s < WV; ++s) {
-      const int v = tid + s * NT;
-      const int r = v / VPR, q = v % VPR;
-      const int co = co_blk + r;
-      const int ci = c0 + q * 8;
-      if (r < BCO && co < a.Co && ci < a.Ci)
-        w_r[s].load(Wp + ((int64_t)k * a.Co + co) * a.Ci + ci);
-      else
-        w_r[s].zero();
-    }
-  };
-  auto store_w = [&](int buf) {
-#pragma unroll
-    for (int s = 0; s < WV; ++s) {
-      const int v = tid + s * NT;
-      const int r = v / VPR, q = v % VPR;
-      if (r < BCO) {
-        float f[8];
-        w_r[s].to_f32(f);
-        lds_store8(w_buf[buf] + r * RP + q * 8, f);
-      }
-    }
-  };
-
-  f32x4 acc[NI][NJ];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue
-  load_window(0);
-  load_w(0, 0);
-  store_window(0);
-  store_w(0);
-  __syncthreads();
-
-  const int lr = lane & 15;
-  const int lk = (lane >> 4) * 8;
-  // A row (weights) for co-tile i:  NI*4*(lr>>2) + 4*i + (lr&3)
-  const int a_row_base = wave_co0 + NI * 4 * (lr >> 2) + (lr & 3);
-
-  for (int s = 0; s < n_steps; ++s) {
-    const int c = s / a.K;
-    const int k = s - c * a.K;
-    const bool has_next = (s + 1) < n_steps;
-    const int cn = (s + 1) / a.K;
-    const int kn = (s + 1) - cn * a.K;
-    if (has_next) {
-      load_w(cn, kn);
-      if (kn == 0) load_window(cn);
-    }
-
-    const TC* wb = w_buf[s & 1];
-    const TC* xb = win_buf[c & 1];
-    Frag<TC> af[NI], bfr[NJ];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) af[i].load(wb + (a_row_base + 4 * i) * RP + lk);
-    const int brow = wave_t0 + lr + k * a.dil;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bfr[j].load(xb + (brow + 16 * j) * RP + lk);
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
-
-    if (has_next) {
-      store_w((s + 1) & 1);
-      if (kn == 0) store_window(cn & 1);
-    }
-    __syncthreads();
+// ---------------------------------------------------------------- LDS tile layout
+// bf16: 32 elements (64 B) per row; 16-byte chunk q of row r lives at chunk
+//   q ^ ((r >> (SH - 1)) & 2).  With SH = 2 the B-fragment reads (16 consecutive rows from
+//   ANY starting row -- taps shift the window by k*dil -- x 4 chunks) are free of
+//   ds_read_b128 bank conflicts; with SH = log2(4*NI) so are the A-fragment reads of the
+//   weight rows NI*4*(m>>2) + 4*i + (m&3) (checked exhaustively against the gfx950 lane
+//   groups; the first version's unswizzled 80-byte pitch was 2-way (B) / 4-way (A)).
+//   Adding 16*j rows never changes the swizzle bit, so one offset serves all NJ tiles.
+// f32 (parity mode): 40-float padded rows, no swizzle.
+template <typename TC> struct Lds;
+template <> struct Lds<bf16_t> {
+  static constexpr int PITCH = 32;
+  template <int SH> __device__ static __forceinline__ int off(int r, int q) {
+    return r * 32 + 8 * (q ^ ((r >> (SH - 1)) & 2));
   }
+};
+template <> struct Lds<float> {
+  static constexpr int PITCH = 40;
+  template <int SH> __device__ static __forceinline__ int off(int r, int q) { return r * 40 + 8 * q; }
+};
 
-  // epilogue: lane holds channels [co0, co0 + 4*NI) of position pos
+__device__ __forceinline__ void lds_put(bf16_t* p, const Raw8<bf16_t>& v) { *reinterpret_cast<uint4*>(p) = v.u; }
+__device__ __forceinline__ void lds_put(float* p, const Raw8<float>& v) {
+  *reinterpret_cast<float4*>(p) = v.a;
+  *reinterpret_cast<float4*>(p + 4) = v.b;
+}
+
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+
+// epilogue: lane (g = lane>>4, lr = lane&15) holds channels [n0, n0 + 4*NI) of position
+// pos for each of its NJ position tiles
+template <typename TOUT, int NI, int NJ>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0, int co_blk,
+                                              int wave_co0, int wave_t0, int lane) {
+  const int lr = lane & 15;
   const int g = lane >> 4;
   const int n0 = co_blk + wave_co0 + NI * 4 * g;
   if (n0 >= a.Co) return;
@@ -250,7 +139,15 @@ conv1d_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[4 * i + r] = act(a.post_act, acc[i][j][r] + bias[4 * i + r], a.post_slope);
+      for (int r = 0; r < 4; ++r) v[4 * i + r] = acc[i][j][r] + bias[4 * i + r];
+    if (a.post_act == VO_ACT_TANH) {
+#pragma unroll
+      for (int e = 0; e < 4 * NI; ++e) v[e] = tanhf(v[e]);
+    } else {
+      const float ps = a.post_act == VO_ACT_RELU ? 0.f : (a.post_act == VO_ACT_LRELU ? a.post_slope : 1.f);
+#pragma unroll
+      for (int e = 0; e < 4 * NI; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * ps;
+    }
 #pragma unroll
     for (int h = 0; h < NI; ++h) {
       float q[4] = {v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
@@ -273,11 +170,196 @@ conv1d_kernel(ConvArgs a) {
   }
 }
 
+// ROLE only names the instantiation (0 = generic, 1..4 = HiFi-GAN MRF stage 0..3), so a
+// profiler attributes the vocoder's stages to distinct kernels; the code is identical.
+// TPS = taps per pipeline step: the weight tiles of TPS taps are staged together so one
+// barrier covers TPS x NI x NJ MFMAs per wave.  NICE = (Ci % 32 == 0 && Co % BCO == 0):
+// no channel bounds checks in the staging loops.
+// Instruction budget: every staging / fragment address is precomputed once per thread;
+// the loop body is LDS reads + MFMAs + a few global loads / LDS stores per step (the
+// first version spent ~15 VALU+SALU instructions per MFMA on address math).
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE>
+__global__ void __launch_bounds__(WCO * WT * 64)
+conv1d_kernel(ConvArgs a) {
+  constexpr int NT = WCO * WT * 64;
+  constexpr int BCO = 16 * NI * WCO;
+  constexpr int BT = 16 * NJ * WT;
+  constexpr int P = Lds<TC>::PITCH;
+  constexpr int VPR = KC / 8;                 // 8-element vectors per row (4)
+  constexpr int MAXV = ((BT + HALO_MAX) * VPR + NT - 1) / NT;
+  constexpr int WV = (TPS * BCO * VPR + NT - 1) / NT;
+  constexpr int SHW = ilog2(4 * NI);
+
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TC* smem = reinterpret_cast<TC*>(smem_raw);
+
+  const int win_rows = BT + (a.K - 1) * a.dil;
+  TC* const win0 = smem;
+  TC* const wt0 = smem + 2 * win_rows * P;
+  const int win_stride = win_rows * P;      // elements between the two window buffers
+  constexpr int WSTRIDE = TPS * BCO * P;    // elements between the two weight buffers
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_co0 = (wave % WCO) * 16 * NI;
+  const int wave_t0 = (wave / WCO) * 16 * NJ;
+
+  const int b = blockIdx.x / a.tiles_per_b;
+  const int t0 = (blockIdx.x - b * a.tiles_per_b) * BT;
+  const int co_blk = blockIdx.y * BCO;
+
+  const TIN* __restrict__ X = reinterpret_cast<const TIN*>(a.x) + (int64_t)b * a.xbs;
+  const TC* __restrict__ Wp = reinterpret_cast<const TC*>(a.w);
+  const int n_chunks = (a.Ci + KC - 1) / KC;
+  const int tsteps = (a.K + TPS - 1) / TPS;
+  const int n_steps = n_chunks * tsteps;
+  const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE;
+  // prologue activation as one select: none -> slope 1, relu -> 0, lrelu -> slope
+  const float pre_s = a.pre_act == VO_ACT_RELU ? 0.f : (a.pre_act == VO_ACT_LRELU ? a.pre_slope : 1.f);
+  const int64_t tap_stride = (int64_t)a.Co * a.Ci;
+
+  // ---- per-thread staging geometry, computed once
+  int xg[MAXV], xl[MAXV], xr[MAXV], xc[MAXV];
+#pragma unroll
+  for (int s = 0; s < MAXV; ++s) {
+    const int v = tid + s * NT;
+    const int r = v / VPR, q = v % VPR;
+    xr[s] = r < win_rows ? t0 - a.pad + r : -0x40000000;  // input row (invalid rows never load)
+    xc[s] = q * 8;
+    xg[s] = xr[s] * a.ldx + q * 8;
+    xl[s] = r < win_rows ? Lds<TC>::template off<2>(r, q) : -1;
+  }
+  int wg[WV], wl[WV], wk[WV];
+  bool wok[WV];
+#pragma unroll
+  for (int s = 0; s < WV; ++s) {
+    const int v = tid + s * NT;
+    const int r = v / VPR, q = v % VPR;   // r = tap_in_step * BCO + co_local
+    const int t = r / BCO, col = r - t * BCO;
+    wk[s] = t;
+    wok[s] = r < TPS * BCO && (NICE || co_blk + col < a.Co);
+    wg[s] = (co_blk + col) * a.Ci + q * 8;
+    wl[s] = t * BCO * P + Lds<TC>::template off<SHW>(col, q);
+  }
+
+  Raw8<TIN> win_r[MAXV];
+  Raw8<TC> w_r[WV];
+
+  auto load_window = [&](int c) {
+    const int c0 = c * KC;
+#pragma unroll
+    for (int s = 0; s < MAXV; ++s) {
+      const bool ok = xr[s] >= 0 && xr[s] < a.T_in && (NICE || c0 + xc[s] < a.Ci);
+      if (ok)
+        win_r[s].load(X + xg[s] + c0);
+      else
+        win_r[s].zero();
+    }
+  };
+  auto store_window = [&](int buf) {
+    TC* base = win0 + buf * win_stride;
+#pragma unroll
+    for (int s = 0; s < MAXV; ++s) {
+      if (xl[s] < 0) continue;
+      if constexpr (std::is_same<TIN, TC>::value) {
+        if (raw_window) {
+          lds_put(base + xl[s], win_r[s]);
+          continue;
+        }
+      }
+      float f[8];
+      win_r[s].to_f32(f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * pre_s;
+      store8(base + xl[s], f);
+    }
+  };
+  auto load_w = [&](int c, int k0) {
+    const int c0 = c * KC;
+#pragma unroll
+    for (int s = 0; s < WV; ++s) {
+      const int k = min(k0 + wk[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
+      if (wok[s] && (NICE || c0 + ((tid + s * NT) % VPR) * 8 < a.Ci))
+        w_r[s].load(Wp + k * tap_stride + wg[s] + c0);
+      else
+        w_r[s].zero();
+    }
+  };
+  auto store_w = [&](int buf) {
+    TC* base = wt0 + buf * WSTRIDE;
+#pragma unroll
+    for (int s = 0; s < WV; ++s)
+      if ((tid + s * NT) / VPR < TPS * BCO) lds_put(base + wl[s], w_r[s]);
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (elements)
+  const int lr = lane & 15;
+  const int lq = lane >> 4;
+  int a_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    a_off[i] = Lds<TC>::template off<SHW>(wave_co0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq);
+  const int brow0 = wave_t0 + lr;
+
+  // prologue
+  load_window(0);
+  load_w(0, 0);
+  store_window(0);
+  store_w(0);
+  __syncthreads();
+
+  int c = 0, tg = 0;
+  for (int s = 0; s < n_steps; ++s) {
+    int cn = c, tgn = tg + 1;
+    if (tgn == tsteps) { tgn = 0; ++cn; }
+    const bool has_next = cn < n_chunks;
+    const bool next_win = (tg == 0) && (c + 1 < n_chunks);
+    if (has_next) load_w(cn, tgn * TPS);
+    if (next_win) load_window(c + 1);   // a whole chunk of MFMAs ahead of its use
+
+    const TC* xb = win0 + (c & 1) * win_stride;
+    const TC* wb = wt0 + (s & 1) * WSTRIDE;
+    const int k0 = tg * TPS;
+#pragma unroll
+    for (int t = 0; t < TPS; ++t) {
+      if (k0 + t < a.K) {
+        Frag<TC> af[NI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) af[i].load(wb + t * BCO * P + a_off[i]);
+        const int br = brow0 + (k0 + t) * a.dil;
+        const int boff = Lds<TC>::template off<2>(br, lq);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + 16 * j * P);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+      }
+    }
+
+    if (has_next) store_w((s + 1) & 1);
+    if (tgn == 0 && has_next) store_window(cn & 1);
+    __syncthreads();
+    c = cn;
+    tg = tgn;
+  }
+  conv_epilogue<TOUT, NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
+}
+
 // ------------------------------------------------------------------ host dispatch
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int ROLE = 0>
+static int g_conv_persistent = 0;  // reserved tuning slot (experiments)
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
+  constexpr int TPS = sizeof(TC) == 2 ? TPS_BF16 : 1;
   ConvArgs a;
   a.x = d->x; a.xbs = d->x_bstride; a.ldx = d->ldx;
   a.w = d->w; a.bias = d->bias;
@@ -290,30 +372,41 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   a.transposed = d->transposed; a.up_stride = d->up_stride; a.up_pad = d->up_pad;
   a.up_cout = d->up_cout; a.up_tout = d->up_tout;
   a.tiles_per_b = (d->T_out + BT - 1) / BT;
+  a.co_tiles = (d->Co + BCO - 1) / BCO;
+  a.B = d->B;
   const int win_rows = BT + (d->K - 1) * d->dil;
-  const size_t lds = (size_t)(2 * win_rows + 2 * BCO) * (KC + 8) * sizeof(TC);
+  const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO) * Lds<TC>::PITCH * sizeof(TC);
   if (lds > 160 * 1024) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)((d->Co + BCO - 1) / BCO));
-  hipLaunchKernelGGL((conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, ROLE>), grid, dim3(WCO * WT * 64),
-                     lds, st, a);
+  const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE>
+                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE>;
+  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles);
+  hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
   VO_RETURN_LAUNCH();
 }
 
 template <typename TIN, typename TC, typename TOUT>
 static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   const int64_t rows = (int64_t)d->B * d->T_out;
-  if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4>(d, st);   // 32 x 256
-  if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4>(d, st);  // 64 x 256
-  if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2>(d, st);  // 64 x 64
-  return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2>(d, st);                    // 128 x 128
+  if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4, 4>(d, st);   // 32 x 256
+  if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
+  if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2, 2>(d, st);  // 64 x 64
+  return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }
 
 }  // namespace vo
 
 using namespace vo;
+
+extern "C" int vo_tune(const char* key, int value) {
+  if (!key) return VO_ERR_INVALID;
+  if (!strcmp(key, "conv_tps_override")) { g_conv_persistent = value; return VO_OK; }
+  vo_set_error("vo_tune: unknown key %s", key);
+  return VO_ERR_INVALID;
+}
 
 extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d != nullptr, "conv1d: null descriptor");
@@ -346,10 +439,10 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d->compute_dtype == VO_BF16, "conv1d: bad compute dtype");
   if (xi == VO_BF16 && yo == VO_BF16) {
     switch (d->variant) {  // HiFi-GAN MRF stages: own instantiations (same tiles as generic)
-      case 1: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 1>(d, st);
-      case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2>(d, st);
-      case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 3>(d, st);
-      case 4: return launch_cfg<bf16_t, bf16_t, bf16_t, 2, 4, 1, 4, 4>(d, st);
+      case 1: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
+      case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);
+      case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 4, 3>(d, st);
+      case 4: return launch_cfg<bf16_t, bf16_t, bf16_t, 2, 4, 1, 4, 4, 4>(d, st);
       default: return launch_types<bf16_t, bf16_t, bf16_t>(d, st);
     }
   }
