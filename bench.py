@@ -48,7 +48,60 @@ def parse():
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--mode", default="infer", choices=["infer", "train"],
+                    help="infer: end-to-end synthesis (headline); train: C4 training step (DDP)")
     return ap.parse_args()
+
+
+def bench_train(a, dev, rank, world, dist):
+    """C4: scripts/04_train.py step (teacher-forced forward, FastSpeech2Loss, backward with the
+    bucketed RCCL all-reduce, clip 1.0, Adam + schedule) on B utterances per GPU."""
+    from helpers import configs, vtts_arrays
+    from weights import load_into
+    from visual_onoma_to_wave_amd import synth
+    from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
+    from visual_onoma_to_wave_amd.train import GradBucketer, train_step, unused_on_path
+    pc, mc, tc = configs()
+    m = vTTS(pc, mc, tc)
+    load_into(m, vtts_arrays())
+    m = m.to(dev).train().set_precision(a.precision)
+    opt = ScheduledOptim(m, tc, mc, 0)
+    bk = None
+    if dist:
+        skip = unused_on_path(m)
+        bk = GradBucketer([p for p in m.parameters() if id(p) not in skip])
+        bk.broadcast_parameters(m)
+    b = synth.acoustic_batch(1234 + rank, a.batch, a.src_len, a.mel_len)
+    t = {k: (torch.from_numpy(v).to(dev) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+    batch = (None, t["audiotypes"], t["texts"], t["src_lens"], t["max_src_len"], t["mels"], t["mel_lens"],
+             t["max_mel_len"], t["e_targets"], None, t["d_targets"], t["images"], None)
+    loss_fn = FastSpeech2Loss()
+    for _ in range(a.warmup):
+        train_step(m, opt, loss_fn, batch, bucketer=bk)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        losses = train_step(m, opt, loss_fn, batch, bucketer=bk)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    frames = a.batch * a.mel_len * a.steps * world
+    if rank == 0:
+        print(json.dumps({
+            "metric": "C4 training mel-frames/sec (FastSpeech2 + variance loss, DDP)", "value": round(frames / elapsed, 1),
+            "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
+            "final_loss": round(float(losses[0]), 5),
+            "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
+                       "seq_len": a.mel_len, "src_len": a.src_len, "parallelism": f"dp{world} (RCCL bucketed all-reduce)"}}))
 
 
 def build_models(device, precision):
@@ -120,6 +173,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+
+    if a.mode == "train":
+        bench_train(a, dev, rank, world, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     model, gen = build_models(dev, a.precision)
     args = make_batch(1234 + rank, a.batch, a.src_len, a.mel_len, dev)

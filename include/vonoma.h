@@ -94,9 +94,12 @@ int vo_conv1d(const vo_conv1d_desc* d, void* stream);
  *   mode VO_PACK_CONV : src (Co, Ci, K) -> dst [K][Co][Ci]
  *   mode VO_PACK_CONVT: src (Ci, Co, 2s) (ConvTranspose1d) -> dst [2][s*Co][Ci],
  *                       dst[kk][r*Co + co][ci] = src[ci][co][r + s*(1-kk)]
+ *   mode VO_PACK_DGRAD: src (Co, Ci, K) -> dst [K][Ci][Co], dst[K-1-k][ci][co] = src[co][ci][k]
+ *                       (the input-gradient of a conv is the conv of dY with these weights,
+ *                       padding (K-1)*dil - pad)
  * g (nullable): weight-norm gains, one per src dim-0 slice; row_scale (nullable): per-Co
  * multiplier (BatchNorm gamma / sqrt(var + eps)). */
-enum vo_pack_mode { VO_PACK_CONV = 0, VO_PACK_CONVT = 1 };
+enum vo_pack_mode { VO_PACK_CONV = 0, VO_PACK_CONVT = 1, VO_PACK_DGRAD = 2 };
 int vo_pack_weight(const float* src, const float* g, const float* row_scale, int mode, int Co,
                    int Ci, int K, int stride, void* dst, int dst_dtype, void* stream);
 

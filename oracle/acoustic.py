@@ -90,14 +90,18 @@ def linear(x, sd, p):
     return F.linear(x, sd[p + ".weight"], sd[p + ".bias"])
 
 
-def batch_norm_eval(x, sd, p, eps=1e-5):
+def batch_norm_eval(x, sd, p, eps=1e-5, training=False):
+    """BatchNorm; training=True normalises with batch statistics (train-mode forward) without
+    touching the running stats of ``sd``."""
+    if training:
+        return F.batch_norm(x, None, None, sd[p + ".weight"], sd[p + ".bias"], True, 0.0, eps)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
                         sd[p + ".weight"], sd[p + ".bias"], False, 0.0, eps)
 
 
 # ----------------------------------------------------------------------------- modules
 
-def vfe(sd, images, p="encoder.VisualFeatureExtractor", slice_w=102, stride=1, n_conv=3):
+def vfe(sd, images, p="encoder.VisualFeatureExtractor", slice_w=102, stride=1, n_conv=3, training=False):
     """VisualFeatureExtractor.forward, scripts/model/visual_feature_extractor.py:60-83.
 
     Slices i*W .. i*W + W*stride of the image width, for i < (width - (stride//2)*W*2)/W,
@@ -112,7 +116,7 @@ def vfe(sd, images, p="encoder.VisualFeatureExtractor", slice_w=102, stride=1, n
     for i in range(n_conv):
         x = F.conv2d(x, sd[f"{p}.embedder.{3 * i}.weight"], sd[f"{p}.embedder.{3 * i}.bias"],
                      padding=1)
-        x = batch_norm_eval(x, sd, f"{p}.embedder.{3 * i + 1}")
+        x = batch_norm_eval(x, sd, f"{p}.embedder.{3 * i + 1}", training=training)
         x = F.relu(x)
     x = x.reshape(B * n, -1)
     x = F.relu(linear(x, sd, f"{p}.bridge.0"))
@@ -153,10 +157,10 @@ def fft_block(sd, p, x, pad_mask):
     return y.masked_fill(pad_mask[..., None], 0), attn
 
 
-def encoder(sd, images, src_mask, n_layers=4):
+def encoder(sd, images, src_mask, n_layers=4, training=False):
     """Encoder.forward (use_image branch), scripts/transformer/Models.py:99-126."""
     B, T = src_mask.shape
-    x = vfe(sd, images) + sd["encoder.position_enc"][:, :T, :]
+    x = vfe(sd, images, training=training) + sd["encoder.position_enc"][:, :T, :]
     for i in range(n_layers):
         x, _ = fft_block(sd, f"encoder.layer_stack.{i}", x, src_mask)
     return x
@@ -216,13 +220,14 @@ def variance_adaptor(sd, x, src_mask, mel_mask, max_len, e_target, d_target,
     return x, e_pred, log_d, d_rounded, mel_len, mel_mask, idx, index
 
 
-def postnet(sd, x, n=5, k=5):
-    """PostNet.forward, scripts/transformer/Layers.py:129-137 (eval: dropout off)."""
+def postnet(sd, x, n=5, k=5, training=False):
+    """PostNet.forward, scripts/transformer/Layers.py:129-137 (dropout off; BatchNorm with batch
+    statistics when training)."""
     y = x.transpose(1, 2)
     for i in range(n):
         p = f"postnet.convolutions.{i}"
         y = F.conv1d(y, sd[p + ".0.conv.weight"], sd[p + ".0.conv.bias"], padding=(k - 1) // 2)
-        y = batch_norm_eval(y, sd, p + ".1")
+        y = batch_norm_eval(y, sd, p + ".1", training=training)
         if i < n - 1:
             y = torch.tanh(y)
     return y.transpose(1, 2)
@@ -231,19 +236,19 @@ def postnet(sd, x, n=5, k=5):
 def vtts_forward(sd, audiotypes, texts, src_lens, max_src_len, mels=None, mel_lens=None,
                  max_mel_len=None, e_targets=None, k_targets=None, d_targets=None,
                  images=None, event_image_features=None, use_image=True, e_control=1.0,
-                 d_control=1.0, energy_stats=None):
+                 d_control=1.0, energy_stats=None, training=False):
     """vTTS.forward, scripts/model/vtts.py:47-119 -> the reference's 10-tuple."""
     assert use_image, "only the visual-text input path is on the hot path"
     src_masks = mask_from_lengths(src_lens, max_src_len)
     mel_masks = mask_from_lengths(mel_lens, max_mel_len) if mels is not None else None
-    x = encoder(sd, images, src_masks)
+    x = encoder(sd, images, src_masks, training=training)
     x = x + sd["audiotype_emb.weight"][audiotypes][:, None, :]
     x, e_pred, log_d, d_rounded, mel_lens_o, mel_masks, _, _ = variance_adaptor(
         sd, x, src_masks, mel_masks, max_mel_len, e_targets, d_targets, e_control, d_control,
         energy_stats)
-    x, mel_masks = decoder(sd, x, mel_masks)
+    x, mel_masks = decoder(sd, x, mel_masks, training=training)
     mel = linear(x, sd, "mel_linear")
-    post = postnet(sd, mel) + mel
+    post = postnet(sd, mel, training=training) + mel
     return (mel, post, e_pred, None, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_lens_o)
 
 

@@ -60,3 +60,39 @@ def get_spec(wav, n_fft=1024, hop=256, win=1024, n_mels=80, sr=22050, fmin=0.0, 
     logmel = torch.log(torch.clamp_min(mel, 1.0e-5) * 1.0)
     energy = torch.linalg.vector_norm(mag, dim=-2)
     return logmel, energy
+
+
+def _hz_to_mel_slaney(f):
+    f = np.asarray(f, np.float64)
+    f_sp, min_log_hz, logstep = 200.0 / 3, 1000.0, np.log(6.4) / 27.0
+    return np.where(f >= min_log_hz, min_log_hz / f_sp + np.log(np.maximum(f, 1e-30) / min_log_hz) / logstep,
+                    f / f_sp)
+
+
+def _mel_to_hz_slaney(m):
+    m = np.asarray(m, np.float64)
+    f_sp, min_log_hz, logstep = 200.0 / 3, 1000.0, np.log(6.4) / 27.0
+    mm = min_log_hz / f_sp
+    return np.where(m >= mm, min_log_hz * np.exp(logstep * (m - mm)), f_sp * m)
+
+
+def librosa_mel(sr, n_fft, n_mels, fmin, fmax):
+    """librosa.filters.mel(sr, n_fft, n_mels, fmin, fmax) (htk=False, norm="slaney"), the basis
+    of TacotronSTFT (scripts/audio/stft.py:145-149) -> (n_mels, 1 + n_fft // 2)."""
+    fft = np.linspace(0, sr / 2.0, 1 + n_fft // 2)
+    mel_f = _mel_to_hz_slaney(np.linspace(_hz_to_mel_slaney(fmin), _hz_to_mel_slaney(fmax), n_mels + 2))
+    fdiff = np.diff(mel_f)
+    ramps = np.subtract.outer(mel_f, fft)
+    lower = -ramps[:-2] / fdiff[:-1, None]
+    upper = ramps[2:] / fdiff[1:, None]
+    w = np.maximum(0, np.minimum(lower, upper)) * (2.0 / (mel_f[2:] - mel_f[:-2]))[:, None]
+    return w.astype(np.float32)
+
+
+def tacotron_mel(wav, n_fft=1024, hop=256, n_mels=80, sr=22050, fmin=0.0, fmax=8000.0):
+    """TacotronSTFT.mel_spectrogram (scripts/audio/stft.py:159-178): |STFT| (reflect pad n_fft/2,
+    hann) -> librosa mel basis -> log(clamp(., 1e-5)); energy = ||X||_2 over frequency."""
+    mag = magnitude(torch.as_tensor(wav, dtype=torch.float32), n_fft, hop, n_fft)
+    basis = torch.from_numpy(librosa_mel(sr, n_fft, n_mels, fmin, fmax))
+    mel = torch.matmul(basis, mag)
+    return torch.log(torch.clamp(mel, min=1e-5)), torch.linalg.vector_norm(mag, dim=-2)

@@ -44,10 +44,13 @@ class HipModule(nn.Module):
         return self
 
     def _check_inference(self):
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+        if self._training_path():
             raise NotImplementedError(
-                f"{type(self).__name__}: the HIP path implements inference (eval / no_grad); "
-                "training goes through visual_onoma_to_wave_amd.train")
+                f"{type(self).__name__}.forward: training runs through vTTS.forward (train_run path)")
+
+    def _training_path(self):
+        """True when autograd must record the op graph (train mode with grad enabled)."""
+        return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
 
 def fold_bn(bn):

@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
                                                           int Ci, int K, int stride, TD* __restrict__ dst) {
   __shared__ float red[4];
   const int s0 = blockIdx.x;
-  const int n = (mode == VO_PACK_CONV) ? Ci * K : Co * K;  // elements per slice
+  const int n = (mode == VO_PACK_CONVT) ? Co * K : Ci * K;  // elements per slice
   const float* sp = src + (int64_t)s0 * n;
   float mul = 1.f;
   if (g) {
@@ -91,6 +91,12 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
       const int ci = e / K, k = e - ci * K;
       const float rs = row_scale ? row_scale[s0] : 1.f;
       dst[((int64_t)k * Co + s0) * Ci + ci] = from_f32<TD>(sp[e] * mul * rs);
+    } else if (mode == VO_PACK_DGRAD) {
+      // src (Co, Ci, K): the input-gradient conv uses taps reversed and C_in/C_out swapped:
+      // dst[K-1-k][ci][co] = src[co][ci][k]
+      const int ci = e / K, k = e - ci * K;
+      const float rs = row_scale ? row_scale[s0] : 1.f;
+      dst[((int64_t)(K - 1 - k) * Ci + ci) * Co + s0] = from_f32<TD>(sp[e] * mul * rs);
     } else {
       // src (Ci, Co, 2s): s0 = ci, e = co*K + kt; tap kt = r + s*(1-kk) -> dst[kk][r*Co + co][ci]
       const int co = e / K, kt = e - co * K;
@@ -135,10 +141,10 @@ extern "C" int vo_transpose_bct(const float* x, int B, int C, int T, void* y, in
 extern "C" int vo_pack_weight(const float* src, const float* g, const float* row_scale, int mode, int Co, int Ci,
                               int K, int stride, void* dst, int dst_dtype, void* stream) {
   VO_CHECK_ARG(src && dst, "pack_weight: null pointer");
-  VO_CHECK_ARG(mode == VO_PACK_CONV || (mode == VO_PACK_CONVT && stride >= 1 && K == 2 * stride),
+  VO_CHECK_ARG(mode == VO_PACK_CONV || mode == VO_PACK_DGRAD || (mode == VO_PACK_CONVT && stride >= 1 && K == 2 * stride),
                "pack_weight: bad mode/stride (K must be 2*stride for ConvTranspose1d)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((unsigned)(mode == VO_PACK_CONV ? Co : Ci));
+  dim3 grid((unsigned)(mode == VO_PACK_CONVT ? Ci : Co));
   if (dst_dtype == VO_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, grid, dim3(256), 0, st, src, g, row_scale, mode, Co, Ci, K, stride,
                        (bf16_t*)dst);

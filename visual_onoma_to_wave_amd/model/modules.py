@@ -19,6 +19,9 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+import torch.nn.functional as F
+
+from .. import autograd as AG
 from .. import ops
 from .._base import HipModule
 from ..transformer.SubLayers import lens_from_mask
@@ -78,6 +81,16 @@ class VariancePredictor(HipModule):
         h = ops.conv1d(h, p["w2"], p["b2"], Co=self.filter_size, K=k, pad=1, post_act=ops.ACT_RELU,
                        compute_dtype=self.compute_dtype, out_dtype=self.compute_dtype)
         return ops.layernorm(h, p["g2"], p["be2"]), p
+
+    def train_run(self, x, mask):
+        c, cd, k = self.conv_layer, self.compute_dtype, self.kernel
+        h = AG.conv1d(x, c.conv1d_1.conv.weight, c.conv1d_1.conv.bias, K=k, pad=(k - 1) // 2, relu=True,
+                      compute_dtype=cd)
+        h = F.dropout(AG.layernorm(h, None, c.layer_norm_1.weight, c.layer_norm_1.bias), self.dropout, True)
+        h = AG.conv1d(h, c.conv1d_2.conv.weight, c.conv1d_2.conv.bias, K=k, pad=1, relu=True, compute_dtype=cd)
+        h = F.dropout(AG.layernorm(h, None, c.layer_norm_2.weight, c.layer_norm_2.bias), self.dropout, True)
+        out = F.linear(h.float(), self.linear_layer.weight, self.linear_layer.bias).squeeze(-1)
+        return out.masked_fill(mask, 0.0) if mask is not None else out
 
     def forward(self, encoder_output, mask):
         self._check_inference()
@@ -162,6 +175,24 @@ class VarianceAdaptor(HipModule):
             mel_mask, mel_lens32 = ops.mask_from_lengths(mel_len, out.shape[1])
         d_rounded = d_target if d_target is not None else d_round
         return out, e_pred, k_pred, log_d, d_rounded, mel_len, mel_mask, mel_lens32
+
+    def train_run(self, x, src_mask, src_lens, mel_mask, max_len, e_target, k_target, d_target, out_dtype):
+        """Teacher-forced training forward (scripts/model/modules.py:79-108)."""
+        if d_target is None:
+            raise ValueError("training needs duration targets (teacher forcing), as in the reference")
+        log_d = self.duration_predictor.train_run(x, src_mask)
+        e_pred = k_pred = None
+        if self.is_energy:
+            e_pred = self.energy_predictor.train_run(x, src_mask)
+            x = x + self.energy_embedding(torch.bucketize(e_target, self.energy_bins)).to(x.dtype)
+        if self.is_kurtosis:
+            k_pred = self.kurtosis_predictor.train_run(x, src_mask)
+            x = x + self.kurt_embedding(torch.bucketize(k_target, self.kurt_bins)).to(x.dtype)
+        if max_len is None:
+            mel_len, _ = ops.lr_lengths(d_target)
+            max_len = int(mel_len.cpu().max())
+        out, mel_len = AG.length_regulate(x, d_target, max_len, out_dtype=out_dtype)
+        return out, e_pred, k_pred, log_d, d_target, mel_len, mel_mask
 
     def forward(self, x, src_mask, mel_mask=None, max_len=None, energy_target=None, kurtosis_target=None,
                 duration_target=None, e_control=1.0, d_control=1.0):

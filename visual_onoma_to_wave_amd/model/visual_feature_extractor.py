@@ -70,6 +70,19 @@ class VisualFeatureExtractor(HipModule):
                        compute_dtype=self.compute_dtype)
         return y.view(B, n, self.embed_dim)
 
+    def train_run(self, images, out_dtype):
+        """Training forward (BatchNorm2d uses batch statistics, so the eval-folded stencil kernel
+        does not apply): slices as a strided view, embedder via PyTorch-ROCm, bridge on HIP."""
+        from .. import autograd as AG
+        B, C, H, W = images.shape
+        n = int((W - (self.stride // 2) * self.slice_width * 2) / self.slice_width)
+        sl = images[..., : n * self.slice_width].reshape(B, C, H, n, self.slice_width)
+        x = sl.permute(0, 3, 1, 2, 4).reshape(B * n, C, H, self.slice_width)
+        x = self.embedder(x)
+        y = AG.linear(x.reshape(1, B * n, -1).to(out_dtype), self.bridge[0].weight, self.bridge[0].bias,
+                      relu=True, compute_dtype=out_dtype)
+        return y.view(B, n, self.embed_dim)
+
     def forward(self, images):
         self._check_inference()
         return self.run(images)

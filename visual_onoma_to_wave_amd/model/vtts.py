@@ -57,7 +57,9 @@ class vTTS(HipModule):
     def forward(self, audiotypes, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
                 e_targets=None, k_targets=None, d_targets=None, images=None, event_image_features=None,
                 use_image=True, e_control=1.0, d_control=1.0):
-        self._check_inference()
+        if self._training_path():
+            return self._train_forward(audiotypes, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len,
+                                       e_targets, k_targets, d_targets, images, use_image)
         src_masks, src_l32 = ops.mask_from_lengths(src_lens, max_src_len)
         mel_masks = mel_l32 = None
         if mels is not None:
@@ -79,4 +81,25 @@ class vTTS(HipModule):
         mel = ops.conv1d(x, p["wmel"], p["bmel"], Co=self.mel_linear.out_features, K=1,
                          out_dtype=torch.float32, compute_dtype=self.compute_dtype)
         post = self.postnet.run(mel, residual=mel, out_dtype=torch.float32)
+        return (mel, post, e_pred, k_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
+
+    def _train_forward(self, audiotypes, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len, e_targets,
+                       k_targets, d_targets, images, use_image):
+        """Training step forward (dropout and BatchNorm batch statistics active; autograd records
+        HIP-forward ops, see visual_onoma_to_wave_amd.autograd)."""
+        from .. import autograd as AG
+        src_masks, src_l32 = ops.mask_from_lengths(src_lens, max_src_len)
+        if mels is None:
+            raise ValueError("training needs mels / mel_lens / max_mel_len (teacher forcing)")
+        mel_masks, mel_l32 = ops.mask_from_lengths(mel_lens, max_mel_len)
+        x = self.encoder.train_run(texts, src_l32, images=images, use_image=use_image)
+        if self.audiotype_emb is not None:
+            x = x + self.audiotype_emb(audiotypes).to(x.dtype)[:, None, :]
+        x, e_pred, k_pred, log_d, d_rounded, mel_len, mel_masks = self.variance_adaptor.train_run(
+            x, src_masks, src_l32, mel_masks, max_mel_len, e_targets, k_targets, d_targets,
+            out_dtype=self.decoder.compute_dtype)
+        x, mel_masks = self.decoder.train_run(x, mel_masks, mel_l32)
+        mel = AG.linear(x, self.mel_linear.weight, self.mel_linear.bias, compute_dtype=self.compute_dtype,
+                        out_dtype=torch.float32)
+        post = self.postnet.train_run(mel) + mel
         return (mel, post, e_pred, k_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)

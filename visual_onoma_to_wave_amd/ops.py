@@ -110,6 +110,16 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     return out
 
 
+def pack_dgrad_weight(w, dtype):
+    """(Co, Ci, K) -> [K][Ci][Co] taps reversed: dX = conv1d(dY, this, Co=Ci, pad=(K-1)*dil - pad)."""
+    w = w.detach().float().contiguous()
+    Co, Ci, K = w.shape
+    out = torch.empty((K, Ci, Co), dtype=dtype, device=w.device)
+    _lib.check(_lib.lib().vo_pack_weight(_ptr(w), None, None, 2, Co, Ci, K, 1, _ptr(out), vo_dtype(dtype),
+                                         _stream(w)), "vo_pack_weight")
+    return out
+
+
 def pack_conv_weight(w, dtype, g=None, row_scale=None, transposed_stride=None):
     """(Co, Ci, K) Conv1d weight (or (Ci, Co, 2s) ConvTranspose1d weight) -> packed.
 
@@ -307,3 +317,18 @@ def transpose_bct(x, out_dtype, ldy=None):
     _lib.check(_lib.lib().vo_transpose_bct(_ptr(x), B, C, T, _ptr(y), vo_dtype(y), ldy, _stream(x)),
                "vo_transpose_bct")
     return y
+
+
+# ----------------------------------------------------------------------------- mel / STFT
+
+def stft_mel(wav, window, fb, n_fft=1024, hop=256, n_mels=80, log_floor=1e-5):
+    """wav (B, N) fp32 -> (log-mel (B, n_mels, 1 + N // hop), energy (B, 1 + N // hop))."""
+    _contig(wav, "wav")
+    B, N = wav.shape
+    F = 1 + N // hop
+    mel = torch.empty((B, n_mels, F), dtype=torch.float32, device=wav.device)
+    energy = torch.empty((B, F), dtype=torch.float32, device=wav.device)
+    _lib.check(_lib.lib().vo_stft_mel(_ptr(wav), B, N, _ptr(window), _ptr(fb), n_fft, hop, n_mels,
+                                      float(log_floor), _ptr(mel), _ptr(energy), _stream(wav)),
+               "vo_stft_mel")
+    return mel, energy

@@ -10,6 +10,9 @@ PostNet  <- scripts/transformer/Layers.py:67-137 (5 x Conv1d k5 + BatchNorm1d(ev
 import torch
 import torch.nn as nn
 
+import torch.nn.functional as F
+
+from .. import autograd as AG
 from .. import ops
 from .._base import HipModule, fold_bn
 from .SubLayers import MultiHeadAttention, PositionwiseFeedForward, lens_from_mask
@@ -24,6 +27,21 @@ class FFTBlock(HipModule):
     def run(self, x, lens):
         y = self.slf_attn.run(x, lens, mask_rows=True)
         return self.pos_ffn.run(y, lens)
+
+    def train_run(self, x, lens):
+        """Training forward (autograd; dropout active), scripts/transformer/Layers.py:21-30."""
+        mha, ffn, cd = self.slf_attn, self.pos_ffn, self.compute_dtype
+        wqkv = torch.cat([mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight], 0)
+        bqkv = torch.cat([mha.w_qs.bias, mha.w_ks.bias, mha.w_vs.bias], 0)
+        qkv = AG.linear(x, wqkv, bqkv, compute_dtype=cd)
+        att = AG.attention(qkv, lens, mha.n_head)
+        y = F.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p, True)
+        x1 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
+        k1, k2 = ffn.kernel_size
+        h = AG.conv1d(x1, ffn.w_1.weight, ffn.w_1.bias, K=k1, pad=(k1 - 1) // 2, relu=True, compute_dtype=cd)
+        y2 = AG.conv1d(h, ffn.w_2.weight, ffn.w_2.bias, K=k2, pad=(k2 - 1) // 2, compute_dtype=cd)
+        y2 = F.dropout(y2, ffn.dropout.p, True)
+        return AG.layernorm(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens)
 
     def forward(self, enc_input, mask=None, slf_attn_mask=None):
         self._check_inference()
@@ -53,6 +71,7 @@ class PostNet(HipModule):
         chans = ([n_mel_channels] + [postnet_embedding_dim] * (postnet_n_convolutions - 1) +
                  [n_mel_channels])
         self.kernel_size = postnet_kernel_size
+        self.dropout_p = 0.5  # F.dropout(..., 0.5, training), scripts/transformer/Layers.py:129-131
         self.convolutions = nn.ModuleList(
             nn.Sequential(
                 ConvNorm(cin, cout, kernel_size=postnet_kernel_size,
@@ -83,6 +102,23 @@ class PostNet(HipModule):
                            res1=residual if last else None,
                            out_dtype=out_dtype if last else self.compute_dtype,
                            compute_dtype=self.compute_dtype)
+        return h
+
+    def train_run(self, x):
+        """Training forward: conv (HIP) -> BatchNorm1d with batch statistics -> tanh -> dropout(0.5)."""
+        h = x
+        k = self.kernel_size
+        n = len(self.convolutions)
+        for i, seq in enumerate(self.convolutions):
+            conv, bn = seq[0].conv, seq[1]
+            last = i == n - 1
+            h = AG.conv1d(h, conv.weight, conv.bias, K=k, pad=(k - 1) // 2, compute_dtype=self.compute_dtype,
+                          out_dtype=torch.float32 if last else self.compute_dtype)
+            hb = F.batch_norm(h.transpose(1, 2), bn.running_mean, bn.running_var, bn.weight, bn.bias, True,
+                              bn.momentum, bn.eps)
+            if not last:
+                hb = torch.tanh(hb)
+            h = F.dropout(hb, self.dropout_p, True).transpose(1, 2).contiguous()
         return h
 
     def forward(self, x):

@@ -86,6 +86,18 @@ class Encoder(HipModule):
             x = layer.run(x, lens)
         return x
 
+    def train_run(self, src_seq, lens, images=None, use_image=True):
+        B, T = src_seq.shape
+        pe = self.position_enc[0, :T].to(self.compute_dtype)
+        if use_image:
+            x = self.VisualFeatureExtractor.train_run(images, self.compute_dtype)
+        else:
+            x = self.src_word_emb(src_seq).to(self.compute_dtype)
+        x = (x + pe[None]).contiguous()
+        for layer in self.layer_stack:
+            x = layer.train_run(x, lens)
+        return x
+
     def forward(self, src_seq, mask, return_attns=False, images=None, use_image=True):
         self._check_inference()
         return self.run(src_seq, lens_from_mask(mask), images, use_image)
@@ -116,6 +128,15 @@ class Decoder(HipModule):
         ops.add_pos_class(x, pe=pe)
         for layer in self.layer_stack:
             x = layer.run(x, lens)
+        return x, mask
+
+    def train_run(self, x, mask, lens):
+        B, T, D = x.shape
+        T = min(T, self.max_seq_len)
+        x = (x[:, :T] + self.position_enc[0, :T].to(x.dtype)[None]).contiguous()
+        mask = mask[:, :T]
+        for layer in self.layer_stack:
+            x = layer.train_run(x, lens)
         return x, mask
 
     def forward(self, enc_seq, mask, return_attns=False):
