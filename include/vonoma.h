@@ -44,7 +44,8 @@ int vo_version(void);
 /* number of entry points and their names (used by the loader test) */
 int vo_num_symbols(void);
 const char* vo_symbol_name(int i);
-/* tuning knobs for experiments ("conv_persistent": 0/1); returns VO_OK or VO_ERR_INVALID */
+/* kernel-variant knobs for A/B experiments ("pair_cfg", "conv_cfg"; default 0 = shipped
+ * configuration); returns VO_OK or VO_ERR_INVALID for an unknown key */
 int vo_tune(const char* key, int value);
 
 /* ------------------------------------------------------------------ conv1d (implicit GEMM)
@@ -192,6 +193,17 @@ int vo_mask_from_lengths(const void* lens, int lens_dtype, int B, int L, bool* m
  * (scripts/hifigan/models.py:161-163).  w packed [K][C] fp32. */
 int vo_conv_post(const void* x, int x_dtype, const float* w, float bias, int B, int T, int C,
                  int K, float slope, float* y, void* stream);
+/* Fused ResBlock1 pair for C = 32 / 64 (bf16, channels-last (B, T, C)):
+ *   y = (x + c2(lrelu(c1_dil(lrelu(x, slope)), slope))) * out_scale (+ acc)
+ * c1 / c2: K taps, packed [K][C][C] bf16 (vo_pack_weight VO_PACK_CONV), biases fp32;
+ * c1 dilation dil, c2 dilation 1, both "same" padding.  The c1 output stays in LDS.
+ * acc may alias y (MRF accumulate); y must not alias x.
+ * Replaces one (c1, c2) iteration of ResBlock.forward (scripts/hifigan/models.py:96-103)
+ * plus the MRF sum / 1/num_kernels of Generator.forward (models.py:155-160). */
+int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void* w2,
+                     const float* b2, void* y, const void* acc, int B, int T, int C, int K,
+                     int dil, float slope, float out_scale, void* stream);
+
 /* (B, C, T) -> (B, T, ldy) with channels C..ldy-1 zero-filled; fp32 in, dtype out. */
 int vo_transpose_bct(const float* x, int B, int C, int T, void* y, int y_dtype, int ldy,
                      void* stream);

@@ -293,3 +293,26 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
         ref[..., h * 128:(h + 1) * 128] = torch.softmax(s, -1) @ v[..., h * 128:(h + 1) * 128]
     out = ops.attention(qkv.cuda().to(dt), lens_t.cuda(), 2)
     assert rel_l2(out.float().cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
+                                     (32, 246 * 3, 11, 5), (64, 4096, 3, 5)])
+def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d):
+    """vo_resblock_pair (c1 -> lrelu -> c2 + residual, MRF accumulate) at tile edges vs torch fp32."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(C * T + k)
+    B = 2
+    x = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+    w1 = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+    w2 = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+    b1, b2 = torch.randn(C, generator=g) * 0.1, torch.randn(C, generator=g) * 0.1
+    acc = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+    xf = x.float().transpose(1, 2)
+    t = F.leaky_relu(F.conv1d(F.leaky_relu(xf, 0.1), w1, b1, padding=d * (k - 1) // 2, dilation=d), 0.1)
+    ref = ((F.conv1d(t, w2, b2, padding=(k - 1) // 2) + xf) / 3.0).transpose(1, 2) + acc.float()
+    p1 = ops.pack_conv_weight(w1.cuda(), torch.bfloat16)
+    p2 = ops.pack_conv_weight(w2.cuda(), torch.bfloat16)
+    out = acc.cuda().clone()
+    ops.resblock_pair(x.cuda(), p1, b1.cuda(), p2, b2.cuda(), k, d, 0.1, out=out, out_scale=1.0 / 3, acc=out)
+    assert rel_l2(out.float().cpu(), ref) < 1e-2

@@ -354,7 +354,6 @@ conv1d_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------ host dispatch
-static int g_conv_persistent = 0;  // reserved tuning slot (experiments)
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
@@ -400,13 +399,6 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
 }  // namespace vo
 
 using namespace vo;
-
-extern "C" int vo_tune(const char* key, int value) {
-  if (!key) return VO_ERR_INVALID;
-  if (!strcmp(key, "conv_tps_override")) { g_conv_persistent = value; return VO_OK; }
-  vo_set_error("vo_tune: unknown key %s", key);
-  return VO_ERR_INVALID;
-}
 
 extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d != nullptr, "conv1d: null descriptor");

@@ -133,6 +133,7 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // error plumbing shared by the launchers (vo_runtime.cpp)
 extern "C" void vo_set_error(const char* fmt, ...);
+extern "C" int vo_tune_get(const char* key);
 
 #define VO_CHECK_ARG(cond, ...)                \
   do {                                         \

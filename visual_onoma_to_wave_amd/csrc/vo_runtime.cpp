@@ -2,6 +2,7 @@
 // the loader test checks against include/vonoma.h.
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../include/vonoma.h"
 
@@ -18,11 +19,31 @@ extern "C" const char* vo_last_error(void) { return g_err; }
 
 extern "C" int vo_version(void) { return 1; }
 
+// experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0
+static const char* const kKnobs[] = {"pair_cfg", "conv_cfg"};
+static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {0, 0};
+
+extern "C" int vo_tune(const char* key, int value) {
+  for (size_t i = 0; key && i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
+    if (!strcmp(key, kKnobs[i])) {
+      g_knobs[i] = value;
+      return VO_OK;
+    }
+  vo_set_error("vo_tune: unknown key %s", key ? key : "(null)");
+  return VO_ERR_INVALID;
+}
+
+extern "C" int vo_tune_get(const char* key) {
+  for (size_t i = 0; i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
+    if (!strcmp(key, kKnobs[i])) return g_knobs[i];
+  return 0;
+}
+
 static const char* const kSymbols[] = {
     "vo_last_error",     "vo_version",       "vo_num_symbols", "vo_symbol_name",   "vo_conv1d",
     "vo_pack_weight",    "vo_layernorm",     "vo_attention",   "vo_length_regulate", "vo_lr_lengths",
     "vo_variance_head",  "vo_vfe_stencil",   "vo_add_pos_class", "vo_conv_post",   "vo_transpose_bct",
-    "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune",
+    "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

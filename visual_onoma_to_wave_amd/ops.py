@@ -319,6 +319,29 @@ def transpose_bct(x, out_dtype, ldy=None):
     return y
 
 
+# ----------------------------------------------------------------------------- fused ResBlock pair
+
+def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None):
+    """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64}."""
+    _contig(x, "x")
+    B, T, C = x.shape
+    if x.dtype != torch.bfloat16 or w1.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16:
+        raise TypeError("resblock_pair: bf16 activations and packed bf16 weights")
+    out = out if out is not None else torch.empty_like(x)
+    if acc is not None and (acc.shape != x.shape or acc.dtype != x.dtype):
+        raise ValueError("resblock_pair: acc must match x")
+    timer = profiling.active()
+    ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
+    _lib.check(_lib.lib().vo_resblock_pair(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(out), _ptr(acc),
+                                           B, T, C, K, dil, float(slope), float(out_scale), _stream(x)),
+               "vo_resblock_pair")
+    if ev is not None:
+        flops = 2.0 * 2.0 * B * T * C * C * K
+        nbytes = 2.0 * x.numel() * 2 + (x.numel() * 2 if acc is not None else 0) + 2 * w1.numel() * 2
+        timer.stop(tag, ev, flops, nbytes)
+    return out
+
+
 # ----------------------------------------------------------------------------- mel / STFT
 
 def stft_mel(wav, window, fb, n_fft=1024, hop=256, n_mels=80, log_floor=1e-5):
