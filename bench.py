@@ -225,11 +225,12 @@ def main():
                 traffic = json.load(f).get(tag, {}).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": f"conv1d_kernel<..., ROLE={int(tag[-1]) + 1}> (HiFi-GAN MRF stage {tag[-1]})",
+                "kernel": f"{' + '.join(d['kernels'])} (HiFi-GAN MRF stage {tag[-1]})",
                 "launches": d["launches"], "avg_launch_ms": round(d["avg_ms"], 4),
                 "flops_per_launch": d["flops_per_launch"],
                 "algorithmic_bytes_per_launch": d["bytes_per_launch"],
-                "all_stages": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
+                "all_stages": {k: {"kernel": " + ".join(v["kernels"]), "avg_ms": round(v["avg_ms"], 4),
+                                   "launches": v["launches"],
                                    "tflops": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12, 1),
                                    "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1)}
                                for k, v in sorted(ks.items())}}

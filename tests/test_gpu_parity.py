@@ -295,12 +295,17 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
     assert rel_l2(out.float().cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
-                                     (32, 246 * 3, 11, 5), (64, 4096, 3, 5)])
-def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d):
-    """vo_resblock_pair (c1 -> lrelu -> c2 + residual, MRF accumulate) at tile edges vs torch fp32."""
+                                     (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
+                                     # several tiles per persistent workgroup (pipelined window/weights)
+                                     (32, 131072, 11, 5), (32, 65536, 3, 1), (64, 65536, 7, 3),
+                                     (64, 65536, 3, 1), (64, 40000, 11, 5)])
+def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, cfg):
+    """vo_resblock_pair (c1 -> lrelu -> c2 + residual, MRF accumulate) at tile edges vs torch fp32,
+    for every kernel configuration the pair_cfg knob selects (0 = shipped)."""
     import torch.nn.functional as F
-    from visual_onoma_to_wave_amd import ops
+    from visual_onoma_to_wave_amd import _lib, ops
     g = torch.Generator().manual_seed(C * T + k)
     B = 2
     x = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
@@ -314,5 +319,10 @@ def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d):
     p1 = ops.pack_conv_weight(w1.cuda(), torch.bfloat16)
     p2 = ops.pack_conv_weight(w2.cuda(), torch.bfloat16)
     out = acc.cuda().clone()
-    ops.resblock_pair(x.cuda(), p1, b1.cuda(), p2, b2.cuda(), k, d, 0.1, out=out, out_scale=1.0 / 3, acc=out)
+    _lib.lib().vo_tune(b"pair_cfg", cfg)
+    try:
+        ops.resblock_pair(x.cuda(), p1, b1.cuda(), p2, b2.cuda(), k, d, 0.1, out=out, out_scale=1.0 / 3, acc=out)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().vo_tune(b"pair_cfg", 0)
     assert rel_l2(out.float().cpu(), ref) < 1e-2

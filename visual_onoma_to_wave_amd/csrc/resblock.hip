@@ -3,132 +3,179 @@
 // (scripts/hifigan/models.py:96-103, one (c1, c2) iteration; the Generator's MRF sum and
 // 1/num_kernels scale, models.py:155-160, ride in the epilogue).
 //
-// One workgroup = R1 = 256 consecutive c1-output rows = BT = R1 - (K-1) output positions:
-//   phase 1: T1 = lrelu(c1(window) + b1) for positions [t0 - h2, t0 - h2 + R1) straight into
-//            LDS (rows outside [0, T) forced to 0 = c2's zero padding); the input window
-//            (R1 + (K-1)*dil rows, lrelu applied once while staging) is loaded ONCE for all
-//            channel chunks and taps;
-//   phase 2: y = c2(T1) + b2 + x (residual re-read from global, L2-hot), scaled/accumulated.
-// The intermediate never touches HBM: per position the pair reads x ~1.2x (halo) + once for
-// the residual and writes y once (bf16), against 5 activation passes for two separate
-// conv launches.  Both GEMMs run on v_mfma_f32_16x16x32_bf16 with the conflict-free
-// XOR-swizzled 64-byte LDS rows of conv1d.hip; weights stream through a double buffer,
-// TPS taps per barrier.
+// Persistent kernel: one workgroup per CU walks a contiguous run of time tiles.  A tile is
+// R1 = NW*16*NJ c1-output rows = BT = R1 - (K-1) output positions:
+//   P1: T1 = lrelu(c1(window) + b1) for positions [t0 - h2, t0 - h2 + R1) straight into LDS
+//       (rows outside [0, T) forced to 0 = c2's zero padding); the lrelu'd input window
+//       (R1 + (K-1)*dil rows, all channel planes) is staged once per tile;
+//   P2: y = (c2(T1) + b2 + x) * out_scale (+ acc).
+// Software pipeline (the C = 32 / 64 pair is HBM-bound, so loads must not wait behind the
+// MFMAs): the NEXT tile's window is fetched into registers before this tile's P1 and written
+// to LDS (lrelu applied) during P2; this tile's residual / MRF-accumulator rows are fetched
+// in epilogue layout before P1 and consumed after P2.  Weights: RES = both convs resident in
+// LDS for the whole kernel (no barrier inside a phase); otherwise TG-tap groups stream
+// through a double buffer (one barrier per group), continuing across phases and tiles.
+// Per position the pair moves x once (+ halo, L2-hot) in, x once more as the residual
+// (L2-hot) and y once out: ~2 HBM activation passes against 5 for two conv launches.
+// LDS rows are 64 B (32 bf16 of one channel plane) with the conflict-free XOR swizzle of
+// conv1d.hip.
+
+#include <algorithm>
 
 #include "vo_common.h"
 
 namespace vo {
 
-// c1 rows per workgroup = R1 (template): 4 waves x 16*NJ positions
-
 struct PairArgs {
   const bf16_t* x; const bf16_t* w1; const float* b1; const bf16_t* w2; const float* b2;
   bf16_t* y; const bf16_t* acc;
-  int T, K, dil, tiles_per_b;
+  int T, K, dil, tiles_per_b, ntiles;
   float slope, out_scale;
 };
 
 __device__ __forceinline__ int rb_off(int r, int q, int sh) { return r * 32 + 8 * (q ^ ((r >> (sh - 1)) & 2)); }
 
-template <int C, int TPS, int RB_R1>
-__global__ void __launch_bounds__(256) resblock_pair_kernel(PairArgs a) {
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)from_f32<bf16_t>(lo) | ((uint32_t)from_f32<bf16_t>(hi) << 16);
+}
+
+// leaky ReLU of 8 packed bf16 (0 <= slope <= 1: lrelu(v) = max(v, slope * v))
+__device__ __forceinline__ uint4 lrelu8(uint4 u, float s) {
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+    w[i] = pack_bf16x2(fmaxf(lo, lo * s), fmaxf(hi, hi * s));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void unpack8(uint4 u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <int C, int NW, int NJ, bool RES, int TG>
+__global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
+  constexpr int NT = NW * 64;
   constexpr int NC = C / 32;              // 32-channel planes
-  constexpr int NI = C / 16;              // co tiles per wave (all channels in one wave)
-  constexpr int NJ = RB_R1 / 64;          // 16*NJ positions per wave
-  constexpr int SHW = NI == 4 ? 4 : 3;    // log2(4 * NI)
-  constexpr int WVEC = TPS * C * 4;       // 8-element weight vectors per step (TPS taps x C co x 32 ci)
-  constexpr int WV = (WVEC + 255) / 256;
+  constexpr int NI = C / 16;              // co tiles per wave (every wave owns all channels)
+  constexpr int R1 = NW * 16 * NJ;        // c1 rows per tile
+  constexpr int SHW = NI == 4 ? 4 : 3;    // log2(4 * NI): weight-row swizzle
+  constexpr int VPR = NC * 4;             // 16-byte vectors per activation row
+  constexpr int MAXW = ((R1 + 64) * VPR + NT - 1) / NT;  // window vectors per thread, halo <= 64
+  constexpr int TAPV = C * VPR;           // 16-byte vectors per weight tap (C co x C ci)
+  constexpr int TAPE = NC * C * 32;       // LDS elements per weight tap
+  constexpr int GV = (TG * TAPV + NT - 1) / NT;  // streamed weight vectors per thread per group
+  constexpr int T1R = R1 + 16;            // P2 reads up to row R1 + K - 2 (feeds discarded rows only)
+  constexpr int NH = NI / 2;              // 8-channel vectors per lane in epilogue layout
+
+  const int K = a.K, dil = a.dil, T = a.T;
+  const int h1 = dil * (K - 1) / 2, h2 = (K - 1) / 2;
+  const int win_rows = R1 + 2 * h1;
+  const int BT = R1 - 2 * h2;
+  const float slope = a.slope;
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
-  const int K = a.K, dil = a.dil;
-  const int h1 = dil * (K - 1) / 2, h2 = (K - 1) / 2;
-  const int win_rows = RB_R1 + 2 * h1;
-  const int t1_rows = RB_R1 + 16;          // phase-2 reads up to row 255 + K - 1 (garbage rows feed discarded outputs)
-  bf16_t* win = smem;                                   // [NC][win_rows][32]
-  bf16_t* t1 = win + NC * win_rows * 32;                // [NC][t1_rows][32]
-  bf16_t* wbuf = t1 + NC * t1_rows * 32;                // [2][TPS][C][32]
-  constexpr int WSTRIDE = TPS * C * 32;
+  bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);  // [NC][win_rows][32]
+  bf16_t* t1 = win + NC * win_rows * 32;               // [NC][T1R][32]
+  bf16_t* wls = t1 + NC * T1R * 32;                    // RES: [2][K] taps; else [2 bufs][TG] taps
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
-  const int BT = RB_R1 - 2 * h2;
-  const int b = blockIdx.x / a.tiles_per_b;
-  const int t0 = (blockIdx.x - b * a.tiles_per_b) * BT;
-  const bf16_t* X = a.x + (int64_t)b * a.T * C;
-  const float slope = a.slope;
+  const int n0 = NI * 4 * lq;  // epilogue: this lane's 4*NI contiguous output channels
 
-  // ---- stage the lrelu'd input window, all planes (positions t0 - h2 - h1 + r).  Every
-  // load is issued before the first one is consumed (compile-time-bounded register array):
-  // a runtime-trip-count load->store loop serialises one HBM round trip per iteration.
-  {
-    constexpr int MAXW = (NC * (RB_R1 + 128) * 4 + 255) / 256;
-    const int row0 = t0 - h2 - h1;
-    const int nvec = NC * win_rows * 4;
-    uint4 buf[MAXW];
-#pragma unroll
-    for (int i = 0; i < MAXW; ++i) {
-      const int v = tid + i * 256;
-      const int pl = v / (win_rows * 4);
-      const int rem = v - pl * win_rows * 4;
-      const int t = row0 + (rem >> 2);
-      buf[i] = make_uint4(0, 0, 0, 0);
-      if (v < nvec && t >= 0 && t < a.T)
-        buf[i] = *reinterpret_cast<const uint4*>(X + (int64_t)t * C + pl * 32 + (rem & 3) * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < MAXW; ++i) {
-      const int v = tid + i * 256;
-      if (v >= nvec) break;
-      const int pl = v / (win_rows * 4);
-      const int rem = v - pl * win_rows * 4;
-      const int r = rem >> 2, q = rem & 3;
-      const uint4 u = buf[i];
-      float f[8];
-      uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f[2 * i] = __uint_as_float(w[i] << 16);
-        f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * slope;
-      store8(win + pl * win_rows * 32 + rb_off(r, q, 2), f);
-    }
-  }
+  // contiguous tile run of this workgroup (uniform per workgroup: the early exit is safe)
+  const int G = gridDim.x;
+  int tile = (int)(((int64_t)blockIdx.x * a.ntiles) / G);
+  const int tile_end = (int)(((int64_t)(blockIdx.x + 1) * a.ntiles) / G);
+  if (tile >= tile_end) return;
 
-  // ---- weight streaming: step s covers (phase, plane c, taps k0..k0+TPS-1)
-  const int tsteps = (K + TPS - 1) / TPS;
-  const int S1 = NC * tsteps;
-  const int S = 2 * S1;
-  int wg[WV], wl[WV], wk[WV];
-  bool wv_ok[WV];
+  // ---- weights
+  const int NG = (K + TG - 1) / TG;  // streamed groups per phase
+  int wg_g[GV], wg_l[GV], wg_t[GV];
 #pragma unroll
-  for (int s = 0; s < WV; ++s) {
-    const int v = tid + s * 256;
-    const int r = v >> 2, q = v & 3;  // r = t * C + co
-    const int t = r / C, co = r - t * C;
-    wv_ok[s] = v < WVEC;
-    wk[s] = t;
-    wg[s] = co * C + q * 8;
-    wl[s] = t * C * 32 + rb_off(co, q, SHW);
+  for (int s = 0; s < GV; ++s) {
+    const int v = tid + s * NT;
+    const int t = v / TAPV, vv = v - t * TAPV;
+    const int co = vv / VPR, rem = vv - co * VPR;
+    wg_t[s] = v < TG * TAPV ? t : 0x40000000;
+    wg_g[s] = co * C + rem * 8;
+    wg_l[s] = t * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW);
   }
-  uint4 w_r[WV];
-  auto load_w = [&](int s) {
-    const int ph = s >= S1;
-    const int ss = s - ph * S1;
-    const int c = ss / tsteps, k0 = (ss - c * tsteps) * TPS;
+  uint4 wr[GV];
+  auto load_group = [&](int gi) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
+    const int ph = gi >= NG;
+    const int k0 = (gi - ph * NG) * TG;
     const bf16_t* W = ph ? a.w2 : a.w1;
 #pragma unroll
-    for (int i = 0; i < WV; ++i) {
-      const int k = min(k0 + wk[i], K - 1);
-      if (wv_ok[i]) w_r[i] = *reinterpret_cast<const uint4*>(W + (int64_t)k * C * C + wg[i] + c * 32);
+    for (int s = 0; s < GV; ++s) {
+      const int k = k0 + wg_t[s];
+      wr[s] = k < K ? *reinterpret_cast<const uint4*>(W + (int64_t)k * C * C + wg_g[s]) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_w = [&](int buf) {
+  auto store_group = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < WV; ++i)
-      if (wv_ok[i]) *reinterpret_cast<uint4*>(wbuf + buf * WSTRIDE + wl[i]) = w_r[i];
+    for (int s = 0; s < GV; ++s)
+      if (wg_t[s] < TG) *reinterpret_cast<uint4*>(wls + buf * TG * TAPE + wg_l[s]) = wr[s];
+  };
+
+  if constexpr (RES) {
+    // both convs, all taps, once per kernel: batches of 8 independent loads
+    const int total = 2 * K * TAPV;
+    for (int v0 = 0; v0 < total; v0 += 8 * NT) {
+      uint4 buf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int v = v0 + u * NT + tid;
+        const int ck = v / TAPV, vv = v - ck * TAPV;  // ck = conv * K + tap
+        const bf16_t* W = ck >= K ? a.w2 + (int64_t)(ck - K) * C * C : a.w1 + (int64_t)ck * C * C;
+        buf[u] = v < total ? *reinterpret_cast<const uint4*>(W + vv * 8) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int v = v0 + u * NT + tid;
+        if (v < total) {
+          const int ck = v / TAPV, vv = v - ck * TAPV;
+          const int co = vv / VPR, rem = vv - co * VPR;
+          *reinterpret_cast<uint4*>(wls + ck * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW)) = buf[u];
+        }
+      }
+    }
+  } else {
+    load_group(0);
+    store_group(0);
+  }
+
+  // ---- input window staging geometry (row-major vectors: consecutive lanes, consecutive 16 B)
+  int xr[MAXW], xl[MAXW], xg[MAXW];
+#pragma unroll
+  for (int s = 0; s < MAXW; ++s) {
+    const int v = tid + s * NT;
+    const int r = v / VPR, rem = v - r * VPR;
+    xr[s] = r < win_rows ? r : 0x40000000;
+    xg[s] = r * C + rem * 8;
+    xl[s] = (rem >> 2) * win_rows * 32 + rb_off(r, rem & 3, 2);
+  }
+  uint4 xw[MAXW];
+  auto load_win = [&](int tl) {
+    const int b = tl / a.tiles_per_b;
+    const int R0 = (tl - b * a.tiles_per_b) * BT - h2 - h1;
+    const bf16_t* base = a.x + ((int64_t)b * T + R0) * C;
+#pragma unroll
+    for (int s = 0; s < MAXW; ++s) {
+      const int t = R0 + xr[s];
+      xw[s] = (t >= 0 && t < T) ? *reinterpret_cast<const uint4*>(base + xg[s]) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_win = [&]() {
+#pragma unroll
+    for (int s = 0; s < MAXW; ++s)
+      if (xr[s] < win_rows) *reinterpret_cast<uint4*>(win + xl[s]) = lrelu8(xw[s], slope);
   };
 
   int a_off[NI];
@@ -136,113 +183,154 @@ __global__ void __launch_bounds__(256) resblock_pair_kernel(PairArgs a) {
   for (int i = 0; i < NI; ++i) a_off[i] = rb_off(NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq, SHW);
   const int brow0 = wave * 16 * NJ + lr;
 
-  f32x4 acc[NI][NJ];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  load_w(0);
-  store_w(0);
+  load_win(tile);
+  store_win();
   __syncthreads();
 
-  const int g = lane >> 4;
-  const int n0 = NI * 4 * g;  // this lane's first output channel (4*NI contiguous channels)
-  for (int s = 0; s < S; ++s) {
-    if (s + 1 < S) load_w(s + 1);
-    const int ph = s >= S1;
-    const int ss = s - ph * S1;
-    const int c = ss / tsteps, k0 = (ss - c * tsteps) * TPS;
-    const bf16_t* wb = wbuf + (s & 1) * WSTRIDE;
-    const bf16_t* src = ph ? (t1 + c * t1_rows * 32) : (win + c * win_rows * 32);
-    const int step = ph ? 1 : dil;
+  f32x4 acc[NI][NJ];
+  int gcount = 0;  // streamed groups consumed so far (selects the double buffer)
+
+  // one tap of one plane: NI x NJ MFMAs
+  auto tap = [&](const bf16_t* wt, const bf16_t* src, int row) {
+    Frag<bf16_t> af[NI], bfr[NJ];
 #pragma unroll
-    for (int t = 0; t < TPS; ++t) {
-      if (k0 + t < K) {
-        Frag<bf16_t> af[NI], bfr[NJ];
+    for (int i = 0; i < NI; ++i) af[i].load(wt + a_off[i]);
+    const int boff = rb_off(row, lq, 2);
 #pragma unroll
-        for (int i = 0; i < NI; ++i) af[i].load(wb + t * C * 32 + a_off[i]);
-        const int br = brow0 + (k0 + t) * step;
-        const int boff = rb_off(br, lq, 2);
+    for (int j = 0; j < NJ; ++j) bfr[j].load(src + boff + 16 * j * 32);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bfr[j].load(src + boff + 16 * j * 32);
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+  };
+
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / a.tiles_per_b;
+    const int t0 = (tile - b * a.tiles_per_b) * BT;
+    const bool has_next = tile + 1 < tile_end;
+
+    // residual / accumulator rows of this tile (epilogue layout), consumed after P2
+    uint4 xres[NJ][NH], ares[NJ][NH];
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    for (int j = 0; j < NJ; ++j) {
+      const int r = wave * 16 * NJ + 16 * j + lr;
+      const int pos = t0 + r;
+      const bool ok = r < BT && pos < T;
+      const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        xres[j][h] = ok ? *reinterpret_cast<const uint4*>(a.x + off + 8 * h) : make_uint4(0, 0, 0, 0);
+        ares[j][h] = (ok && a.acc) ? *reinterpret_cast<const uint4*>(a.acc + off + 8 * h) : make_uint4(0, 0, 0, 0);
       }
     }
-    if (s + 1 < S) store_w((s + 1) & 1);
+    if (has_next) load_win(tile + 1);
 
-    if (s == S1 - 1) {
-      // phase-1 epilogue: T1 = lrelu(acc + b1), zero outside [0, T) (c2's zero padding)
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // P1 epilogue: T1 = lrelu(acc + b1), zero outside [0, T) (c2's zero padding); clears acc
+    auto p1_epilogue = [&]() {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int r = wave * 16 * NJ + 16 * j + lr;
         const int pos = t0 - h2 + r;
-        const bool inside = pos >= 0 && pos < a.T;
-        float v[4 * NI];
+        const bool inside = pos >= 0 && pos < T;
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float z = acc[i][j][e] + a.b1[n0 + 4 * i + e];
-            v[4 * i + e] = inside ? (z > 0.f ? z : z * slope) : 0.f;
-          }
-#pragma unroll
-        for (int h = 0; h < NI / 2; ++h) {  // 8-channel chunks
-          const int ch = n0 + 8 * h;
+        for (int h = 0; h < NH; ++h) {
           float f[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = v[8 * h + e];
-          store8(t1 + (ch / 32) * t1_rows * 32 + rb_off(r, (ch & 31) / 8, 2), f);
+          for (int e = 0; e < 8; ++e) {
+            const float z = acc[2 * h + e / 4][j][e & 3] + a.b1[n0 + 8 * h + e];
+            f[e] = inside ? fmaxf(z, z * slope) : 0.f;
+          }
+          const int ch = n0 + 8 * h;
+          store8(t1 + (ch >> 5) * T1R * 32 + rb_off(r, (ch & 31) >> 3, 2), f);
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    }
-    __syncthreads();
-  }
+    };
 
-  // ---- phase-2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
-  bf16_t* Y = a.y + (int64_t)b * a.T * C;
-  const bf16_t* A = a.acc ? a.acc + (int64_t)b * a.T * C : nullptr;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int r = wave * 16 * NJ + 16 * j + lr;
-    const int pos = t0 + r;
-    if (r >= BT || pos >= a.T) continue;
-    const int64_t off = (int64_t)pos * C + n0;
-#pragma unroll
-    for (int h = 0; h < NI; ++h) {
-      float xr[4], q[4];
-      load4(X + off + 4 * h, xr);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) q[e] = (acc[h][j][e] + a.b2[n0 + 4 * h + e] + xr[e]) * a.out_scale;
-      if (A) {
-        float ar[4];
-        load4(A + off + 4 * h, ar);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) q[e] += ar[e];
+    if constexpr (RES) {
+      for (int c = 0; c < NC; ++c)
+        for (int k = 0; k < K; ++k) tap(wls + k * TAPE + c * C * 32, win + c * win_rows * 32, brow0 + k * dil);
+      p1_epilogue();
+      __syncthreads();
+      if (has_next) store_win();
+      const bf16_t* wb = wls + K * TAPE;
+      for (int c = 0; c < NC; ++c)
+        for (int k = 0; k < K; ++k) tap(wb + k * TAPE + c * C * 32, t1 + c * T1R * 32, brow0 + k);
+    } else {
+      for (int gi = 0; gi < 2 * NG; ++gi) {
+        const int ph = gi >= NG;
+        const int g = gi - ph * NG;
+        const bool more = has_next || gi + 1 < 2 * NG;
+        if (more) load_group(gi + 1 == 2 * NG ? 0 : gi + 1);
+        const bf16_t* wb = wls + (gcount & 1) * TG * TAPE;
+        const bf16_t* src = ph ? t1 : win;
+        const int plane = ph ? T1R * 32 : win_rows * 32;
+        const int step = ph ? 1 : dil;
+        for (int t = 0; t < TG; ++t) {
+          const int k = g * TG + t;
+          if (k < K)
+            for (int c = 0; c < NC; ++c) tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + k * step);
+        }
+        if (gi == NG - 1) p1_epilogue();
+        if (gi == NG && has_next) store_win();  // P1 reads of the window ended at the last barrier
+        if (more) store_group((gcount + 1) & 1);
+        __syncthreads();
+        ++gcount;
       }
-      store4(Y + off + 4 * h, q);
     }
+
+    // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int r = wave * 16 * NJ + 16 * j + lr;
+      const int pos = t0 + r;
+      if (r >= BT || pos >= T) continue;
+      const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float xf[8], af8[8], q[8];
+        unpack8(xres[j][h], xf);
+        unpack8(ares[j][h], af8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          q[e] = (acc[2 * h + e / 4][j][e & 3] + a.b2[n0 + 8 * h + e] + xf[e]) * a.out_scale + af8[e];
+        store8(a.y + off + 8 * h, q);
+      }
+    }
+    if constexpr (RES) __syncthreads();
   }
 }
 
-template <int C, int TPS, int RB_R1>
-static int pair_launch(const PairArgs& a0, int B, int T, int K, int dil, hipStream_t st) {
-  PairArgs a = a0;
-  const int h1 = dil * (K - 1) / 2, h2 = (K - 1) / 2;
-  const int BT = RB_R1 - 2 * h2;
-  a.tiles_per_b = (T + BT - 1) / BT;
-  const size_t lds = ((size_t)(C / 32) * (RB_R1 + 2 * h1) * 32 + (size_t)(C / 32) * (RB_R1 + 16) * 32 +
-                      2 * (size_t)TPS * C * 32) * sizeof(bf16_t);
+template <int C, int NW, int NJ, bool RES, int TG>
+static int pair_launch(PairArgs a, int B, hipStream_t st) {
+  constexpr int R1 = NW * 16 * NJ;
+  const int h1 = a.dil * (a.K - 1) / 2, h2 = (a.K - 1) / 2;
+  const int BT = R1 - 2 * h2;
+  a.tiles_per_b = (a.T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  const size_t wtaps = RES ? 2 * (size_t)a.K : 2 * (size_t)TG;
+  const size_t lds = ((size_t)(R1 + 2 * h1) + (R1 + 16) + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t);
   if (lds > 160 * 1024) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  hipLaunchKernelGGL((resblock_pair_kernel<C, TPS, RB_R1>), dim3((unsigned)(a.tiles_per_b * B)), dim3(256), lds, st, a);
+  auto kern = mrf_pair_kernel<C, NW, NJ, RES, TG>;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NW * 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int grid = (int)std::min<int64_t>((int64_t)cus * per_cu, a.ntiles);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
   VO_RETURN_LAUNCH();
 }
 
@@ -255,16 +343,27 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
                                 float out_scale, void* stream) {
   VO_CHECK_ARG(x && w1 && b1 && w2 && b2 && y, "resblock_pair: null pointer");
   VO_CHECK_ARG(C == 32 || C == 64, "resblock_pair: C=%d unsupported (32 or 64)", C);
-  VO_CHECK_ARG(K % 2 == 1 && K >= 1 && dil >= 1 && dil * (K - 1) <= 128 && K <= 15,
-               "resblock_pair: K=%d dil=%d unsupported", K, dil);
+  VO_CHECK_ARG(K % 2 == 1 && K >= 1 && K <= 15 && dil >= 1 && dil * (K - 1) <= 64,
+               "resblock_pair: K=%d dil=%d unsupported (odd K <= 15, (K-1)*dil <= 64)", K, dil);
+  VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "resblock_pair: slope %g outside [0, 1]", slope);
   VO_CHECK_ARG(B > 0 && T > 0, "resblock_pair: empty");
-  VO_CHECK_ARG(y != x, "resblock_pair: y must not alias x (the residual is re-read)");
+  VO_CHECK_ARG(y != x, "resblock_pair: y must not alias x (neighbouring tiles re-read x)");
+  VO_CHECK_ARG(acc == nullptr || acc == y || acc != x, "resblock_pair: acc must not alias x");
   PairArgs a;
   a.x = (const bf16_t*)x; a.w1 = (const bf16_t*)w1; a.b1 = b1; a.w2 = (const bf16_t*)w2; a.b2 = b2;
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
   a.T = T; a.K = K; a.dil = dil; a.slope = slope; a.out_scale = out_scale;
+  a.tiles_per_b = a.ntiles = 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // measured on MI355X, B=32 MRF shapes (tools/ab_pair.py): C=32 K<=7 -> 256-row tiles (3
+  // workgroups/CU), K=11 -> 512-row tiles; C=64 K=3 -> resident weights, K>=7 -> 2-tap groups.
+  // pair_cfg selects the alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
-  if (C == 32) return cfg == 1 ? pair_launch<32, 8, 256>(a, B, T, K, dil, st) : pair_launch<32, 4, 256>(a, B, T, K, dil, st);
-  return cfg == 1 ? pair_launch<64, 4, 128>(a, B, T, K, dil, st) : pair_launch<64, 2, 128>(a, B, T, K, dil, st);
+  if (C == 32) {
+    const bool small = cfg == 0 ? K <= 7 : cfg == 1;
+    return small ? pair_launch<32, 8, 2, true, 1>(a, B, st) : pair_launch<32, 8, 4, true, 1>(a, B, st);
+  }
+  if (K <= 3 && cfg != 2) return pair_launch<64, 8, 2, true, 1>(a, B, st);
+  if (cfg == 1) return pair_launch<64, 8, 2, false, 4>(a, B, st);
+  return pair_launch<64, 8, 3, false, 2>(a, B, st);
 }

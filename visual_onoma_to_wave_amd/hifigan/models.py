@@ -61,9 +61,9 @@ class ResBlock(HipModule):
         super().__init__()
         self.h, self.channels, self.kernel_size, self.dilation = h, channels, kernel_size, tuple(dilation)
         # channel widths that run each (c1, c2) pair as one vo_resblock_pair launch (bf16 only).
-        # Measured on MI355X at B=32: C=32 fused 0.32/0.41/0.49 ms vs 0.44/0.47/0.56 ms for two
-        # conv launches (k=3/7/11); C=64 fused loses (0.56/0.85/1.42 vs 0.54/0.60/0.68 ms).
-        self.fused_pair_channels = (32,)
+        # Measured on MI355X at B=32 (k=3/7/11): C=32 0.18/0.20/0.31 ms vs 0.44/0.47/0.57 ms for
+        # two conv launches; C=64 0.28/0.42/0.53 vs 0.54/0.60/0.67 ms.
+        self.fused_pair_channels = (32, 64)
         self.convs1 = nn.ModuleList(
             _wn(Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
             for d in self.dilation)

@@ -106,7 +106,7 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
                   (res1.numel() * res1.element_size() if res1 is not None else 0) +
                   (res2.numel() * res2.element_size() if res2 is not None else 0) +
                   w_packed.numel() * w_packed.element_size())
-        timer.stop(tag, ev, flops, nbytes)
+        timer.stop(tag, ev, flops, nbytes, kernel=f"conv1d_kernel<..., ROLE={d.variant}>")
     return out
 
 
@@ -338,7 +338,7 @@ def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0,
     if ev is not None:
         flops = 2.0 * 2.0 * B * T * C * C * K
         nbytes = 2.0 * x.numel() * 2 + (x.numel() * 2 if acc is not None else 0) + 2 * w1.numel() * 2
-        timer.stop(tag, ev, flops, nbytes)
+        timer.stop(tag, ev, flops, nbytes, kernel=f"mrf_pair_kernel<C={C}, ...>")
     return out
 
 

@@ -14,7 +14,7 @@ _ACTIVE = None
 class KernelTimer:
     def __init__(self, tags):
         self.tags = set(tags)
-        self.pending = []  # (tag, start_event, end_event, flops, bytes)
+        self.pending = []  # (tag, start_event, end_event, flops, bytes, kernel label)
 
     def __enter__(self):
         global _ACTIVE
@@ -33,17 +33,19 @@ class KernelTimer:
         ev.record()
         return ev
 
-    def stop(self, tag, start_ev, flops, nbytes):
+    def stop(self, tag, start_ev, flops, nbytes, kernel=None):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self.pending.append((tag, start_ev, ev, flops, nbytes))
+        self.pending.append((tag, start_ev, ev, flops, nbytes, kernel))
 
     def summary(self):
-        """{tag: dict(launches, avg_ms, flops_per_launch, bytes_per_launch)} (synchronizes)."""
+        """{tag: dict(launches, avg_ms, flops_per_launch, bytes_per_launch, kernels)} (synchronizes)."""
         torch.cuda.synchronize()
         out = {}
-        for tag, s, e, fl, nb in self.pending:
-            d = out.setdefault(tag, dict(launches=0, total_ms=0.0, flops=0.0, bytes=0.0))
+        for tag, s, e, fl, nb, kern in self.pending:
+            d = out.setdefault(tag, dict(launches=0, total_ms=0.0, flops=0.0, bytes=0.0, kernels=[]))
+            if kern and kern not in d["kernels"]:
+                d["kernels"].append(kern)
             d["launches"] += 1
             d["total_ms"] += s.elapsed_time(e)
             d["flops"] += fl
