@@ -8,9 +8,9 @@ from collections import defaultdict
 d = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "conv1d" not in r["Kernel_Name"]:
+        if "conv1d" not in r["Kernel_Name"] and "pair" not in r["Kernel_Name"]:
             continue
-        k = r["Kernel_Name"].split("<")[1][:60]
+        k = r["Kernel_Name"].split("(")[0][-80:]
         d[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in d.items():
     m = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -24,4 +24,9 @@ for k, cs in d.items():
             if c in m:
                 print(f"   {c:28s} {100 * m[c] / wc:6.1f}% of wave cycles")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
-        print(f"   MFMA busy = {100 * m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] * 1024):.1f}% (per SIMD, 1024 SIMDs)")
+        # GRBM_GUI_ACTIVE sums the 8 XCDs; MFMA busy cycles sum the 1024 SIMDs
+        print(f"   MFMA busy = {100 * m['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / (m['GRBM_GUI_ACTIVE'] / 8):.1f}% of SIMD cycles")
+    if "SQ_INSTS_MFMA" in m:
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+            if c in m:
+                print(f"   {c:28s} {m[c] / m['SQ_INSTS_MFMA']:6.2f} per MFMA")

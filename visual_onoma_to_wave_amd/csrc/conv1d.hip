@@ -198,6 +198,7 @@ conv1d_kernel(ConvArgs a) {
   TC* const wt0 = smem + 2 * win_rows * P;
   const int win_stride = win_rows * P;      // elements between the two window buffers
   constexpr int WSTRIDE = TPS * BCO * P;    // elements between the two weight buffers
+  TC* const dummy = wt0 + 2 * WSTRIDE;      // one row that absorbs the stores of idle staging slots
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -220,17 +221,22 @@ conv1d_kernel(ConvArgs a) {
   const int64_t tap_stride = (int64_t)a.Co * a.Ci;
 
   // ---- per-thread staging geometry, computed once
-  int xg[MAXV], xl[MAXV], xr[MAXV], xc[MAXV];
+  // Every global load below is UNCONDITIONAL (addresses clamped into the tensor) and the
+  // out-of-range vectors are zeroed when they are written to LDS: a load under a divergent
+  // branch gets an immediate s_waitcnt vmcnt(0) from the compiler, which serialised the
+  // prefetch against HBM latency (seen in the ISA of the first version).
+  int xg[MAXV], xl[MAXV], xr[MAXV], xc[MAXV];  // xr: row-in-range flag
 #pragma unroll
   for (int s = 0; s < MAXV; ++s) {
     const int v = tid + s * NT;
     const int r = v / VPR, q = v % VPR;
-    xr[s] = r < win_rows ? t0 - a.pad + r : -0x40000000;  // input row (invalid rows never load)
+    const int row = t0 - a.pad + r;
+    xr[s] = r < win_rows && row >= 0 && row < a.T_in;  // row in range
     xc[s] = q * 8;
-    xg[s] = xr[s] * a.ldx + q * 8;
+    xg[s] = min(max(row, 0), a.T_in - 1) * a.ldx + q * 8;
     xl[s] = r < win_rows ? Lds<TC>::template off<2>(r, q) : -1;
   }
-  int wg[WV], wl[WV], wk[WV];
+  int wg[WV], wl[WV], wk[WV], wq[WV];
   bool wok[WV];
 #pragma unroll
   for (int s = 0; s < WV; ++s) {
@@ -238,33 +244,33 @@ conv1d_kernel(ConvArgs a) {
     const int r = v / VPR, q = v % VPR;   // r = tap_in_step * BCO + co_local
     const int t = r / BCO, col = r - t * BCO;
     wk[s] = t;
+    wq[s] = q * 8;
     wok[s] = r < TPS * BCO && (NICE || co_blk + col < a.Co);
-    wg[s] = (co_blk + col) * a.Ci + q * 8;
+    wg[s] = min(co_blk + col, a.Co - 1) * a.Ci + q * 8;
     wl[s] = t * BCO * P + Lds<TC>::template off<SHW>(col, q);
   }
 
   Raw8<TIN> win_r[MAXV];
   Raw8<TC> w_r[WV];
+  bool win_ok[MAXV], w_ok[WV];
 
   auto load_window = [&](int c) {
     const int c0 = c * KC;
 #pragma unroll
     for (int s = 0; s < MAXV; ++s) {
-      const bool ok = xr[s] >= 0 && xr[s] < a.T_in && (NICE || c0 + xc[s] < a.Ci);
-      if (ok)
-        win_r[s].load(X + xg[s] + c0);
-      else
-        win_r[s].zero();
+      win_ok[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
+      win_r[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
     }
   };
   auto store_window = [&](int buf) {
     TC* base = win0 + buf * win_stride;
 #pragma unroll
-    for (int s = 0; s < MAXV; ++s) {
-      if (xl[s] < 0) continue;
+    for (int s = 0; s < MAXV; ++s) {  // branch-free: idle slots store to the dummy row
+      TC* dst = xl[s] >= 0 ? base + xl[s] : dummy;
+      if (!win_ok[s]) win_r[s].zero();
       if constexpr (std::is_same<TIN, TC>::value) {
         if (raw_window) {
-          lds_put(base + xl[s], win_r[s]);
+          lds_put(dst, win_r[s]);
           continue;
         }
       }
@@ -272,7 +278,7 @@ conv1d_kernel(ConvArgs a) {
       win_r[s].to_f32(f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * pre_s;
-      store8(base + xl[s], f);
+      store8(dst, f);
     }
   };
   auto load_w = [&](int c, int k0) {
@@ -280,17 +286,17 @@ conv1d_kernel(ConvArgs a) {
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
       const int k = min(k0 + wk[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
-      if (wok[s] && (NICE || c0 + ((tid + s * NT) % VPR) * 8 < a.Ci))
-        w_r[s].load(Wp + k * tap_stride + wg[s] + c0);
-      else
-        w_r[s].zero();
+      w_ok[s] = wok[s] && (NICE || c0 + wq[s] < a.Ci);
+      w_r[s].load(Wp + k * tap_stride + wg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - wq[s])));
     }
   };
   auto store_w = [&](int buf) {
     TC* base = wt0 + buf * WSTRIDE;
 #pragma unroll
-    for (int s = 0; s < WV; ++s)
-      if ((tid + s * NT) / VPR < TPS * BCO) lds_put(base + wl[s], w_r[s]);
+    for (int s = 0; s < WV; ++s) {
+      if (!w_ok[s]) w_r[s].zero();
+      lds_put((tid + s * NT) / VPR < TPS * BCO ? base + wl[s] : dummy, w_r[s]);
+    }
   };
 
   f32x4 acc[NI][NJ];
@@ -315,15 +321,11 @@ conv1d_kernel(ConvArgs a) {
   store_w(0);
   __syncthreads();
 
-  int c = 0, tg = 0;
-  for (int s = 0; s < n_steps; ++s) {
-    int cn = c, tgn = tg + 1;
-    if (tgn == tsteps) { tgn = 0; ++cn; }
-    const bool has_next = cn < n_chunks;
-    const bool next_win = (tg == 0) && (c + 1 < n_chunks);
-    if (has_next) load_w(cn, tgn * TPS);
-    if (next_win) load_window(c + 1);   // a whole chunk of MFMAs ahead of its use
-
+  // One pipeline step = TPS taps of one 32-channel chunk c (weights in buffer s & 1).  The
+  // next chunk's window is fetched when a chunk starts and written to LDS in its last step.
+  // Loads are issued on every path (re-fetching the last chunk instead of branching): a
+  // conditional load makes the compiler's wait counts conservative on every path.
+  auto mfma_step = [&](int c, int tg, int s) {
     const TC* xb = win0 + (c & 1) * win_stride;
     const TC* wb = wt0 + (s & 1) * WSTRIDE;
     const int k0 = tg * TPS;
@@ -343,12 +345,26 @@ conv1d_kernel(ConvArgs a) {
           for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
       }
     }
+  };
 
-    if (has_next) store_w((s + 1) & 1);
-    if (tgn == 0 && has_next) store_window(cn & 1);
+  int s = 0;
+  for (int c = 0; c < n_chunks; ++c) {
+    const bool more_chunks = c + 1 < n_chunks;
+    load_window(min(c + 1, n_chunks - 1));   // a whole chunk of MFMAs ahead of its use
+    for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
+      load_w(c, (tg + 1) * TPS);
+      mfma_step(c, tg, s);
+      store_w((s + 1) & 1);
+      __syncthreads();
+    }
+    load_w(min(c + 1, n_chunks - 1), 0);
+    mfma_step(c, tsteps - 1, s);
+    if (more_chunks) {
+      store_w((s + 1) & 1);
+      store_window((c + 1) & 1);
+    }
     __syncthreads();
-    c = cn;
-    tg = tgn;
+    ++s;
   }
   conv_epilogue<TOUT, NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
 }
@@ -374,7 +390,7 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   a.co_tiles = (d->Co + BCO - 1) / BCO;
   a.B = d->B;
   const int win_rows = BT + (d->K - 1) * d->dil;
-  const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO) * Lds<TC>::PITCH * sizeof(TC);
+  const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO + 1) * Lds<TC>::PITCH * sizeof(TC);
   if (lds > 160 * 1024) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;

@@ -26,6 +26,10 @@
 
 namespace vo {
 
+// staging registers use a clang vector type: HIP's uint4 struct is copied with memcpy, which
+// kept the streamed-weight registers in scratch memory
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 struct PairArgs {
   const bf16_t* x; const bf16_t* w1; const float* b1; const bf16_t* w2; const float* b2;
   bf16_t* y; const bf16_t* acc;
@@ -40,17 +44,17 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 }
 
 // leaky ReLU of 8 packed bf16 (0 <= slope <= 1: lrelu(v) = max(v, slope * v))
-__device__ __forceinline__ uint4 lrelu8(uint4 u, float s) {
+__device__ __forceinline__ u32x4 lrelu8(u32x4 u, float s) {
   uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
     w[i] = pack_bf16x2(fmaxf(lo, lo * s), fmaxf(hi, hi * s));
   }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  return u32x4{w[0], w[1], w[2], w[3]};
 }
 
-__device__ __forceinline__ void unpack8(uint4 u, float (&f)[8]) {
+__device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -84,6 +88,8 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
   bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);  // [NC][win_rows][32]
   bf16_t* t1 = win + NC * win_rows * 32;               // [NC][T1R][32]
   bf16_t* wls = t1 + NC * T1R * 32;                    // RES: [2][K] taps; else [2 bufs][TG] taps
+  float* sbias = reinterpret_cast<float*>(wls + (RES ? 2 * K : 2 * TG) * TAPE);  // [b1 | b2]
+  bf16_t* spare = reinterpret_cast<bf16_t*>(sbias + 2 * C);  // 16 B sink for idle staging slots
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
@@ -103,38 +109,39 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     const int v = tid + s * NT;
     const int t = v / TAPV, vv = v - t * TAPV;
     const int co = vv / VPR, rem = vv - co * VPR;
-    wg_t[s] = v < TG * TAPV ? t : 0x40000000;
+    wg_t[s] = v < TG * TAPV ? t : TG;  // TG marks an idle slot (loads tap 0.., never stored)
     wg_g[s] = co * C + rem * 8;
     wg_l[s] = t * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW);
   }
-  uint4 wr[GV];
+  u32x4 wr[GV];
   auto load_group = [&](int gi) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
     const int ph = gi >= NG;
     const int k0 = (gi - ph * NG) * TG;
     const bf16_t* W = ph ? a.w2 : a.w1;
 #pragma unroll
     for (int s = 0; s < GV; ++s) {
-      const int k = k0 + wg_t[s];
-      wr[s] = k < K ? *reinterpret_cast<const uint4*>(W + (int64_t)k * C * C + wg_g[s]) : make_uint4(0, 0, 0, 0);
+      const int k = k0 + (wg_t[s] < TG ? wg_t[s] : 0);
+      wr[s] = *reinterpret_cast<const u32x4*>(W + (int64_t)min(k, K - 1) * C * C + wg_g[s]);  // taps >= K unused
     }
   };
   auto store_group = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < GV; ++s)
-      if (wg_t[s] < TG) *reinterpret_cast<uint4*>(wls + buf * TG * TAPE + wg_l[s]) = wr[s];
+      if (GV * NT == TG * TAPV || wg_t[s] < TG) *reinterpret_cast<u32x4*>(wls + buf * TG * TAPE + wg_l[s]) = wr[s];
   };
 
+  for (int i = tid; i < 2 * C; i += NT) sbias[i] = i < C ? a.b1[i] : a.b2[i - C];
   if constexpr (RES) {
     // both convs, all taps, once per kernel: batches of 8 independent loads
     const int total = 2 * K * TAPV;
     for (int v0 = 0; v0 < total; v0 += 8 * NT) {
-      uint4 buf[8];
+      u32x4 buf[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int v = v0 + u * NT + tid;
         const int ck = v / TAPV, vv = v - ck * TAPV;  // ck = conv * K + tap
         const bf16_t* W = ck >= K ? a.w2 + (int64_t)(ck - K) * C * C : a.w1 + (int64_t)ck * C * C;
-        buf[u] = v < total ? *reinterpret_cast<const uint4*>(W + vv * 8) : make_uint4(0, 0, 0, 0);
+        buf[u] = v < total ? *reinterpret_cast<const u32x4*>(W + vv * 8) : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -142,7 +149,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
         if (v < total) {
           const int ck = v / TAPV, vv = v - ck * TAPV;
           const int co = vv / VPR, rem = vv - co * VPR;
-          *reinterpret_cast<uint4*>(wls + ck * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW)) = buf[u];
+          *reinterpret_cast<u32x4*>(wls + ck * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW)) = buf[u];
         }
       }
     }
@@ -158,24 +165,31 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     const int v = tid + s * NT;
     const int r = v / VPR, rem = v - r * VPR;
     xr[s] = r < win_rows ? r : 0x40000000;
-    xg[s] = r * C + rem * 8;
+    xg[s] = rem * 8;
     xl[s] = (rem >> 2) * win_rows * 32 + rb_off(r, rem & 3, 2);
   }
-  uint4 xw[MAXW];
+  // Global loads are unconditional (clamped rows, zeroed when written to LDS): a load under a
+  // divergent branch gets an immediate vmcnt(0) from the compiler and the prefetch is lost.
+  u32x4 xw[MAXW];
+  bool xw_ok[MAXW];
   auto load_win = [&](int tl) {
     const int b = tl / a.tiles_per_b;
     const int R0 = (tl - b * a.tiles_per_b) * BT - h2 - h1;
-    const bf16_t* base = a.x + ((int64_t)b * T + R0) * C;
+    const bf16_t* base = a.x + (int64_t)b * T * C;
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
       const int t = R0 + xr[s];
-      xw[s] = (t >= 0 && t < T) ? *reinterpret_cast<const uint4*>(base + xg[s]) : make_uint4(0, 0, 0, 0);
+      xw_ok[s] = t >= 0 && t < T;
+      xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg[s]);
     }
   };
   auto store_win = [&]() {
 #pragma unroll
-    for (int s = 0; s < MAXW; ++s)
-      if (xr[s] < win_rows) *reinterpret_cast<uint4*>(win + xl[s]) = lrelu8(xw[s], slope);
+    for (int s = 0; s < MAXW; ++s) {
+      const u32x4 v = lrelu8(xw[s], slope);
+      // idle slots (rows past the window) write the spare row after the bias table
+      *reinterpret_cast<u32x4*>(xr[s] < win_rows ? win + xl[s] : spare) = xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
+    }
   };
 
   int a_off[NI];
@@ -210,20 +224,19 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     const bool has_next = tile + 1 < tile_end;
 
     // residual / accumulator rows of this tile (epilogue layout), consumed after P2
-    uint4 xres[NJ][NH], ares[NJ][NH];
+    u32x4 xres[NJ][NH], ares[NJ][NH];
+    const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int r = wave * 16 * NJ + 16 * j + lr;
-      const int pos = t0 + r;
-      const bool ok = r < BT && pos < T;
+      const int pos = min(t0 + wave * 16 * NJ + 16 * j + lr, T - 1);  // rows past the tile are not stored
       const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        xres[j][h] = ok ? *reinterpret_cast<const uint4*>(a.x + off + 8 * h) : make_uint4(0, 0, 0, 0);
-        ares[j][h] = (ok && a.acc) ? *reinterpret_cast<const uint4*>(a.acc + off + 8 * h) : make_uint4(0, 0, 0, 0);
+        xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+        ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
       }
     }
-    if (has_next) load_win(tile + 1);
+    load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
 
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -242,7 +255,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
           float f[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float z = acc[2 * h + e / 4][j][e & 3] + a.b1[n0 + 8 * h + e];
+            const float z = acc[2 * h + e / 4][j][e & 3] + sbias[n0 + 8 * h + e];
             f[e] = inside ? fmaxf(z, z * slope) : 0.f;
           }
           const int ch = n0 + 8 * h;
@@ -263,26 +276,32 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
       for (int c = 0; c < NC; ++c)
         for (int k = 0; k < K; ++k) tap(wb + k * TAPE + c * C * 32, t1 + c * T1R * 32, brow0 + k);
     } else {
-      for (int gi = 0; gi < 2 * NG; ++gi) {
-        const int ph = gi >= NG;
-        const int g = gi - ph * NG;
+      // peeled per phase so the P1 epilogue / window store sit on straight-line paths
+      auto group = [&](int ph, int g, bool p1_last, bool p2_first) {
+        const int gi = ph * NG + g;
         const bool more = has_next || gi + 1 < 2 * NG;
-        if (more) load_group(gi + 1 == 2 * NG ? 0 : gi + 1);
+        load_group(gi + 1 == 2 * NG ? 0 : gi + 1);  // unconditional; stored only if needed
         const bf16_t* wb = wls + (gcount & 1) * TG * TAPE;
         const bf16_t* src = ph ? t1 : win;
         const int plane = ph ? T1R * 32 : win_rows * 32;
         const int step = ph ? 1 : dil;
+#pragma unroll
         for (int t = 0; t < TG; ++t) {
           const int k = g * TG + t;
           if (k < K)
+#pragma unroll
             for (int c = 0; c < NC; ++c) tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + k * step);
         }
-        if (gi == NG - 1) p1_epilogue();
-        if (gi == NG && has_next) store_win();  // P1 reads of the window ended at the last barrier
+        if (p1_last) p1_epilogue();
+        if (p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
         if (more) store_group((gcount + 1) & 1);
         __syncthreads();
         ++gcount;
-      }
+      };
+      for (int g = 0; g < NG - 1; ++g) group(0, g, false, false);
+      group(0, NG - 1, true, false);
+      group(1, 0, false, true);
+      for (int g = 1; g < NG; ++g) group(1, g, false, false);
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
@@ -299,7 +318,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
         unpack8(ares[j][h], af8);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          q[e] = (acc[2 * h + e / 4][j][e & 3] + a.b2[n0 + 8 * h + e] + xf[e]) * a.out_scale + af8[e];
+          q[e] = (acc[2 * h + e / 4][j][e & 3] + sbias[C + n0 + 8 * h + e] + xf[e]) * a.out_scale + (a.acc ? af8[e] : 0.f);
         store8(a.y + off + 8 * h, q);
       }
     }
@@ -315,7 +334,8 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
   a.tiles_per_b = (a.T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
   const size_t wtaps = RES ? 2 * (size_t)a.K : 2 * (size_t)TG;
-  const size_t lds = ((size_t)(R1 + 2 * h1) + (R1 + 16) + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t);
+  const size_t lds = ((size_t)(R1 + 2 * h1) + (R1 + 16) + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t) +
+                     2 * C * sizeof(float) + 16;
   if (lds > 160 * 1024) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
