@@ -300,7 +300,8 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
                                      # several tiles per persistent workgroup (pipelined window/weights)
                                      (32, 131072, 11, 5), (32, 65536, 3, 1), (64, 65536, 7, 3),
-                                     (64, 65536, 3, 1), (64, 40000, 11, 5)])
+                                     (64, 65536, 3, 1), (64, 40000, 11, 5),
+                                     (128, 300, 3, 1), (128, 1, 7, 3), (128, 32768, 11, 5), (128, 20000, 3, 5)])
 def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, cfg):
     """vo_resblock_pair (c1 -> lrelu -> c2 + residual, MRF accumulate) at tile edges vs torch fp32,
     for every kernel configuration the pair_cfg knob selects (0 = shipped)."""

@@ -24,7 +24,7 @@ def t_ms(fn, n=10):
 
 def main():
     B = 32
-    for C, T in ((64, 65536), (32, 131072)):
+    for C, T in ((128, 32768), (64, 65536), (32, 131072)):
         for k, d in ((3, 1), (7, 3), (11, 5)):
             x = torch.randn(B, T, C, device="cuda").to(torch.bfloat16)
             w1 = ops.pack_conv_weight(torch.randn(C, C, k, device="cuda") / (C * k) ** 0.5, torch.bfloat16)
@@ -32,7 +32,7 @@ def main():
             b = torch.zeros(C, device="cuda")
             y = torch.empty_like(x)
             t = torch.empty_like(x)
-            var = 3 if C == 64 else 4
+            var = {128: 2, 64: 3, 32: 4}[C]
 
             def unfused():
                 ops.conv1d(x, w1, b, Co=C, K=k, dil=d, pad=d * (k - 1) // 2, pre_act=ops.ACT_LRELU, pre_slope=0.1,

@@ -4,7 +4,7 @@
 // 1/num_kernels scale, models.py:155-160, ride in the epilogue).
 //
 // Persistent kernel: one workgroup per CU walks a contiguous run of time tiles.  A tile is
-// R1 = NW*16*NJ c1-output rows = BT = R1 - (K-1) output positions:
+// R1 = WT*16*NJ c1-output rows = BT = R1 - (K-1) output positions:
 //   P1: T1 = lrelu(c1(window) + b1) for positions [t0 - h2, t0 - h2 + R1) straight into LDS
 //       (rows outside [0, T) forced to 0 = c2's zero padding); the lrelu'd input window
 //       (R1 + (K-1)*dil rows, all channel planes) is staged once per tile;
@@ -63,12 +63,14 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
   }
 }
 
-template <int C, int NW, int NJ, bool RES, int TG>
-__global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
+// WC x WT waves: wave (wc, wt) owns channels [wc*C/WC, (wc+1)*C/WC) of rows [wt*16*NJ, ..+16*NJ)
+template <int C, int WC, int WT, int NJ, bool RES, int TG>
+__global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
+  constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
   constexpr int NC = C / 32;              // 32-channel planes
-  constexpr int NI = C / 16;              // co tiles per wave (every wave owns all channels)
-  constexpr int R1 = NW * 16 * NJ;        // c1 rows per tile
+  constexpr int NI = C / (16 * WC);       // co tiles per wave
+  constexpr int R1 = WT * 16 * NJ;        // c1 rows per tile
   constexpr int SHW = NI == 4 ? 4 : 3;    // log2(4 * NI): weight-row swizzle
   constexpr int VPR = NC * 4;             // 16-byte vectors per activation row
   constexpr int MAXW = ((R1 + 64) * VPR + NT - 1) / NT;  // window vectors per thread, halo <= 64
@@ -93,7 +95,9 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
-  const int n0 = NI * 4 * lq;  // epilogue: this lane's 4*NI contiguous output channels
+  const int wc = wave % WC, wt = wave / WC;
+  const int cw0 = wc * (C / WC);    // the wave's first channel
+  const int n0 = cw0 + NI * 4 * lq;  // epilogue: this lane's 4*NI contiguous output channels
 
   // contiguous tile run of this workgroup (uniform per workgroup: the early exit is safe)
   const int G = gridDim.x;
@@ -194,8 +198,8 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
 
   int a_off[NI];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) a_off[i] = rb_off(NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq, SHW);
-  const int brow0 = wave * 16 * NJ + lr;
+  for (int i = 0; i < NI; ++i) a_off[i] = rb_off(cw0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq, SHW);
+  const int brow0 = wt * 16 * NJ + lr;
 
   load_win(tile);
   store_win();
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int pos = min(t0 + wave * 16 * NJ + 16 * j + lr, T - 1);  // rows past the tile are not stored
+      const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);  // rows past the tile are not stored
       const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
@@ -247,7 +251,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     auto p1_epilogue = [&]() {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int r = wave * 16 * NJ + 16 * j + lr;
+        const int r = wt * 16 * NJ + 16 * j + lr;
         const int pos = t0 - h2 + r;
         const bool inside = pos >= 0 && pos < T;
 #pragma unroll
@@ -307,7 +311,7 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int r = wave * 16 * NJ + 16 * j + lr;
+      const int r = wt * 16 * NJ + 16 * j + lr;
       const int pos = t0 + r;
       if (r >= BT || pos >= T) continue;
       const int64_t off = ((int64_t)b * T + pos) * C + n0;
@@ -326,9 +330,10 @@ __global__ void __launch_bounds__(NW * 64) mrf_pair_kernel(PairArgs a) {
   }
 }
 
-template <int C, int NW, int NJ, bool RES, int TG>
+template <int C, int WC, int WT, int NJ, bool RES, int TG>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
-  constexpr int R1 = NW * 16 * NJ;
+  constexpr int NW = WC * WT;
+  constexpr int R1 = WT * 16 * NJ;
   const int h1 = a.dil * (a.K - 1) / 2, h2 = (a.K - 1) / 2;
   const int BT = R1 - 2 * h2;
   a.tiles_per_b = (a.T + BT - 1) / BT;
@@ -340,7 +345,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, NW, NJ, RES, TG>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -362,7 +367,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
                                 void* y, const void* acc, int B, int T, int C, int K, int dil, float slope,
                                 float out_scale, void* stream) {
   VO_CHECK_ARG(x && w1 && b1 && w2 && b2 && y, "resblock_pair: null pointer");
-  VO_CHECK_ARG(C == 32 || C == 64, "resblock_pair: C=%d unsupported (32 or 64)", C);
+  VO_CHECK_ARG(C == 32 || C == 64 || C == 128, "resblock_pair: C=%d unsupported (32, 64 or 128)", C);
   VO_CHECK_ARG(K % 2 == 1 && K >= 1 && K <= 15 && dil >= 1 && dil * (K - 1) <= 64,
                "resblock_pair: K=%d dil=%d unsupported (odd K <= 15, (K-1)*dil <= 64)", K, dil);
   VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "resblock_pair: slope %g outside [0, 1]", slope);
@@ -376,14 +381,19 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   a.tiles_per_b = a.ntiles = 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // measured on MI355X, B=32 MRF shapes (tools/ab_pair.py): C=32 K<=7 -> 256-row tiles (3
-  // workgroups/CU), K=11 -> 512-row tiles; C=64 K=3 -> resident weights, K>=7 -> 2-tap groups.
+  // workgroups/CU), K=11 -> 512-row tiles; C=64 K=3 -> resident weights, K>=7 -> 2-tap groups;
+  // C=128 -> 128-row tiles, one streamed tap per group.
   // pair_cfg selects the alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
   if (C == 32) {
     const bool small = cfg == 0 ? K <= 7 : cfg == 1;
-    return small ? pair_launch<32, 8, 2, true, 1>(a, B, st) : pair_launch<32, 8, 4, true, 1>(a, B, st);
+    return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
   }
-  if (K <= 3 && cfg != 2) return pair_launch<64, 8, 2, true, 1>(a, B, st);
-  if (cfg == 1) return pair_launch<64, 8, 2, false, 4>(a, B, st);
-  return pair_launch<64, 8, 3, false, 2>(a, B, st);
+  if (C == 128) {  // 2 x 4 waves of 64 channels x 32 rows (2 waves/SIMD) beat 2 x 2 waves of 64 x 64
+    if (cfg == 1) return pair_launch<128, 2, 2, 4, false, 1>(a, B, st);
+    return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
+  }
+  if (K <= 3 && cfg != 2) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
+  if (cfg == 1) return pair_launch<64, 1, 8, 2, false, 4>(a, B, st);
+  return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);
 }

@@ -61,9 +61,10 @@ class ResBlock(HipModule):
         super().__init__()
         self.h, self.channels, self.kernel_size, self.dilation = h, channels, kernel_size, tuple(dilation)
         # channel widths that run each (c1, c2) pair as one vo_resblock_pair launch (bf16 only).
-        # Measured on MI355X at B=32 (k=3/7/11): C=32 0.18/0.20/0.31 ms vs 0.44/0.47/0.57 ms for
-        # two conv launches; C=64 0.28/0.42/0.53 vs 0.54/0.60/0.67 ms.
-        self.fused_pair_channels = (32, 64)
+        # Measured on MI355X at B=32 (k=3/7/11): C=32 0.16/0.21/0.30 ms vs 0.37/0.40/0.48 ms for
+        # two conv launches; C=64 0.24/0.37/0.47 vs 0.44/0.52/0.60; C=128 0.39/0.64/0.93 vs
+        # 0.66/0.80/1.03 (tools/ab_pair.py).
+        self.fused_pair_channels = (32, 64, 128)
         self.convs1 = nn.ModuleList(
             _wn(Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
             for d in self.dilation)

@@ -322,7 +322,7 @@ def transpose_bct(x, out_dtype, ldy=None):
 # ----------------------------------------------------------------------------- fused ResBlock pair
 
 def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None):
-    """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64}."""
+    """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64, 128}."""
     _contig(x, "x")
     B, T, C = x.shape
     if x.dtype != torch.bfloat16 or w1.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16:
