@@ -14,7 +14,8 @@ from visual_onoma_to_wave_amd import ops  # noqa: E402
 SHAPES = {"s0_k11": (256, 4096, 11, 5, 1), "s1_k11": (128, 32768, 11, 5, 2), "s1_k3": (128, 32768, 3, 1, 2),
           "s1_k7": (128, 32768, 7, 3, 2),
           "s2_k7": (64, 65536, 7, 3, 3), "s3_k3": (32, 131072, 3, 1, 4), "s3_k11": (32, 131072, 11, 5, 4)}
-PAIRS = {"pair_s2_k3": (64, 65536, 3, 1), "pair_s2_k11": (64, 65536, 11, 5), "pair_s3_k3": (32, 131072, 3, 1),
+PAIRS = {"pair_s1_k3": (128, 32768, 3, 1), "pair_s1_k7": (128, 32768, 7, 3), "pair_s1_k11": (128, 32768, 11, 5),
+         "pair_s2_k3": (64, 65536, 3, 1), "pair_s2_k11": (64, 65536, 11, 5), "pair_s3_k3": (32, 131072, 3, 1),
          "pair_s3_k11": (32, 131072, 11, 5), "pair_s2_k7": (64, 65536, 7, 3)}
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of the MRF conv kernels from two rocprofv3 --pmc passes.
+"""Per-launch HBM traffic of the MRF kernels from two rocprofv3 --pmc passes.
 
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one TCC
 pass).  Per MI355X_MICROARCH.md section HBM: both are KB; on gfx950 FETCH_SIZE reports
@@ -14,16 +14,22 @@ import re
 import sys
 from collections import defaultdict
 
+PAIR_STAGE = {256: "mrf_s0", 128: "mrf_s1", 64: "mrf_s2", 32: "mrf_s3"}
+
 
 def load(path, counter):
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"conv1d_kernel<.*,\s*(\d+)>", r["Kernel_Name"])
-        if not m or m.group(1) == "0":
+        name = r["Kernel_Name"]
+        m = re.search(r"conv1d_kernel<.*,\s*(\d+)>", name)
+        if m and m.group(1) != "0":
+            acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
             continue
-        acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
+        m = re.search(r"mrf_pair_kernel<(\d+),", name)  # fused pairs: HiFi-GAN V1 stage by width
+        if m and int(m.group(1)) in PAIR_STAGE:
+            acc[PAIR_STAGE[int(m.group(1))]].append(float(r["Counter_Value"]))
     return acc
 
 

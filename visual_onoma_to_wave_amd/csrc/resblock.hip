@@ -64,7 +64,9 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
 }
 
 // WC x WT waves: wave (wc, wt) owns channels [wc*C/WC, (wc+1)*C/WC) of rows [wt*16*NJ, ..+16*NJ)
-template <int C, int WC, int WT, int NJ, bool RES, int TG>
+// ABL (timing ablations only, garbage results): 1 = no weight-group loads, 2 = no window /
+// residual loads, 3 = neither
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0>
 __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -111,11 +113,14 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 #pragma unroll
   for (int s = 0; s < GV; ++s) {
     const int v = tid + s * NT;
+    // plane-major (tap, plane, co, q): 8 consecutive lanes fill 128 contiguous LDS bytes
+    // (row-major order put two planes 4 KB+ apart in one 8-lane store group: 2-way conflicts)
     const int t = v / TAPV, vv = v - t * TAPV;
-    const int co = vv / VPR, rem = vv - co * VPR;
+    const int pl = vv / (C * 4), rem = vv - pl * C * 4;
+    const int co = rem >> 2, q = rem & 3;
     wg_t[s] = v < TG * TAPV ? t : TG;  // TG marks an idle slot (loads tap 0.., never stored)
-    wg_g[s] = co * C + rem * 8;
-    wg_l[s] = t * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW);
+    wg_g[s] = co * C + pl * 32 + q * 8;
+    wg_l[s] = t * TAPE + pl * C * 32 + rb_off(co, q, SHW);
   }
   u32x4 wr[GV];
   auto load_group = [&](int gi) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
@@ -125,7 +130,10 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 #pragma unroll
     for (int s = 0; s < GV; ++s) {
       const int k = k0 + (wg_t[s] < TG ? wg_t[s] : 0);
-      wr[s] = *reinterpret_cast<const u32x4*>(W + (int64_t)min(k, K - 1) * C * C + wg_g[s]);  // taps >= K unused
+      if constexpr (ABL & 1)
+        wr[s] = u32x4{(unsigned)k, 0u, 0u, 0u};
+      else
+        wr[s] = *reinterpret_cast<const u32x4*>(W + (int64_t)min(k, K - 1) * C * C + wg_g[s]);  // taps >= K unused
     }
   };
   auto store_group = [&](int buf) {
@@ -184,7 +192,10 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     for (int s = 0; s < MAXW; ++s) {
       const int t = R0 + xr[s];
       xw_ok[s] = t >= 0 && t < T;
-      xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg[s]);
+      if constexpr ((ABL & 2) != 0)
+        xw[s] = u32x4{(unsigned)t, 0u, 0u, 0u};
+      else
+        xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg[s]);
     }
   };
   auto store_win = [&]() {
@@ -236,8 +247,12 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
-        ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+        if constexpr ((ABL & 2) != 0) {
+          xres[j][h] = ares[j][h] = u32x4{(unsigned)pos, 0u, 0u, 0u};
+        } else {
+          xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+          ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+        }
       }
     }
     load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
@@ -248,7 +263,19 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // P1 epilogue: T1 = lrelu(acc + b1), zero outside [0, T) (c2's zero padding); clears acc
+    // the lane's 8*NH bias values, read (as float4) before the epilogue's LDS stores: read
+    // one by one between the T1 stores they were serialised behind them (possible aliasing)
+    auto lane_bias = [&](int which, float (&bz)[8 * NH]) {
+      const float4* bp = reinterpret_cast<const float4*>(sbias + which * C + n0);
+#pragma unroll
+      for (int u = 0; u < 2 * NH; ++u) {
+        const float4 v = bp[u];
+        bz[4 * u] = v.x; bz[4 * u + 1] = v.y; bz[4 * u + 2] = v.z; bz[4 * u + 3] = v.w;
+      }
+    };
     auto p1_epilogue = [&]() {
+      float bz[8 * NH];
+      lane_bias(0, bz);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int r = wt * 16 * NJ + 16 * j + lr;
@@ -259,7 +286,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
           float f[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float z = acc[2 * h + e / 4][j][e & 3] + sbias[n0 + 8 * h + e];
+            const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
             f[e] = inside ? fmaxf(z, z * slope) : 0.f;
           }
           const int ch = n0 + 8 * h;
@@ -289,12 +316,29 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
         const bf16_t* src = ph ? t1 : win;
         const int plane = ph ? T1R * 32 : win_rows * 32;
         const int step = ph ? 1 : dil;
+        // software-pipelined over the group's TG x NC (tap, plane) steps: the fragments of step
+        // st + 1 are read from LDS before the MFMAs of step st (two named register sets)
+        constexpr int S = TG * NC;
+        Frag<bf16_t> af[2][NI], bq[2][NJ];
+        auto ld = [&](int st, int set) {
+          const int t = st / NC, c = st - t * NC;
+          const bf16_t* wt = wb + t * TAPE + c * C * 32;
 #pragma unroll
-        for (int t = 0; t < TG; ++t) {
-          const int k = g * TG + t;
-          if (k < K)
+          for (int i = 0; i < NI; ++i) af[set][i].load(wt + a_off[i]);
+          const int boff = c * plane + rb_off(brow0 + (g * TG + t) * step, lq, 2);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + k * step);
+          for (int j = 0; j < NJ; ++j) bq[set][j].load(src + boff + 16 * j * 32);
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int st = 0; st < S; ++st) {
+          if (st + 1 < S) ld(st + 1, (st + 1) & 1);
+          if (TG == 1 || g * TG + st / NC < K) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[st & 1][i], bq[st & 1][j], acc[i][j]);
+          }
         }
         if (p1_last) p1_epilogue();
         if (p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
@@ -309,6 +353,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
+    float b2z[8 * NH];
+    lane_bias(1, b2z);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int r = wt * 16 * NJ + 16 * j + lr;
@@ -322,7 +368,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
         unpack8(ares[j][h], af8);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          q[e] = (acc[2 * h + e / 4][j][e & 3] + sbias[C + n0 + 8 * h + e] + xf[e]) * a.out_scale + (a.acc ? af8[e] : 0.f);
+          q[e] = (acc[2 * h + e / 4][j][e & 3] + b2z[8 * h + e] + xf[e]) * a.out_scale + (a.acc ? af8[e] : 0.f);
         store8(a.y + off + 8 * h, q);
       }
     }
@@ -330,7 +376,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RES, int TG>
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -345,7 +391,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -386,13 +432,20 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // pair_cfg selects the alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
   if (C == 32) {
+    if (cfg == 3) return pair_launch<32, 1, 4, 8, true, 1>(a, B, st);
     const bool small = cfg == 0 ? K <= 7 : cfg == 1;
     return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
   }
   if (C == 128) {  // 2 x 4 waves of 64 channels x 32 rows (2 waves/SIMD) beat 2 x 2 waves of 64 x 64
     if (cfg == 1) return pair_launch<128, 2, 2, 4, false, 1>(a, B, st);
+    if (cfg == 3) return pair_launch<128, 1, 4, 2, false, 1>(a, B, st);
+    if (cfg == 11) return pair_launch<128, 2, 4, 2, false, 1, 1>(a, B, st);
+    if (cfg == 12) return pair_launch<128, 2, 4, 2, false, 1, 2>(a, B, st);
+    if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
     return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
   }
+  if (cfg == 3) return pair_launch<64, 1, 4, 4, false, 2>(a, B, st);
+  if (cfg == 4) return pair_launch<64, 1, 4, 8, false, 1>(a, B, st);
   if (K <= 3 && cfg != 2) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
   if (cfg == 1) return pair_launch<64, 1, 8, 2, false, 4>(a, B, st);
   return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);
