@@ -253,7 +253,11 @@ def test_generator(gen, dt, tol):
 @pytest.mark.parametrize("B,T,Ci,Co,K,dil,act", [
     (2, 300, 256, 256, 3, 1, 0), (3, 257, 128, 128, 7, 3, 2), (2, 1000, 64, 64, 11, 5, 2),
     (1, 777, 32, 32, 11, 5, 2), (4, 100, 256, 1024, 9, 1, 1), (2, 64, 1024, 256, 1, 1, 0),
-    (2, 50, 80, 512, 7, 1, 0), (2, 33, 512, 80, 5, 1, 0), (1, 384, 2448, 256, 1, 1, 1)])
+    (2, 50, 80, 512, 7, 1, 0), (2, 33, 512, 80, 5, 1, 0), (1, 384, 2448, 256, 1, 1, 1),
+    # short-sequence tiles (T_out <= 16 / <= 32: encoder / phoneme-level predictors)
+    (32, 12, 256, 1024, 9, 1, 1), (5, 16, 1024, 256, 1, 1, 0), (3, 17, 256, 256, 3, 1, 1), (2, 32, 256, 192, 3, 1, 0),
+    # Co % 8 == 4: the lane's 8-channel run crosses the end of the output row
+    (2, 40, 64, 20, 3, 1, 0), (3, 9, 32, 28, 5, 1, 2)])
 @pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])
 def test_conv1d_vs_torch_fp32(B, T, Ci, Co, K, dil, act, dt, tol):
     """The implicit-GEMM conv against the plain PyTorch fp32 op (CPU) on the same data."""

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""A/B of conv1d tile configurations (vo_tune "conv_cfg") on the MRF stage-0 shapes (B=32)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from visual_onoma_to_wave_amd import _lib, ops  # noqa: E402
+
+
+def t_ms(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+def main(cfgs=(0, 9)):
+    B, C, T = 32, 256, 4096
+    for k, d in ((3, 1), (7, 3), (11, 5)):
+        x = torch.randn(B, T, C, device="cuda").to(torch.bfloat16)
+        w = ops.pack_conv_weight(torch.randn(C, C, k, device="cuda") / (C * k) ** 0.5, torch.bfloat16)
+        b = torch.zeros(C, device="cuda")
+        y = torch.empty_like(x)
+        fl = 2.0 * B * T * C * C * k
+        line = f"C={C} k={k} d={d}:"
+        ref = None
+        for cfg in cfgs:
+            _lib.lib().vo_tune(b"conv_cfg", cfg)
+            f = lambda: ops.conv1d(x, w, b, Co=C, K=k, dil=d, pad=d * (k - 1) // 2, pre_act=ops.ACT_LRELU,  # noqa
+                                   pre_slope=0.1, out=y, variant=1)
+            ms = t_ms(f)
+            f()
+            torch.cuda.synchronize()
+            err = 0.0 if ref is None else float((y.float() - ref).abs().max())
+            ref = y.float().clone() if ref is None else ref
+            line += f"  [{cfg}] {ms:.4f} ms {fl / ms / 1e9:.0f} TF/s (maxdiff {err:.2e})"
+        _lib.lib().vo_tune(b"conv_cfg", 0)
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()

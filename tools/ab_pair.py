@@ -43,7 +43,7 @@ def main():
             fl = 2 * 2.0 * B * T * C * C * k
             a = t_ms(unfused)
             line = f"C={C} k={k} d={d}: unfused {a:.4f} ms ({fl / a / 1e9:.0f} TF/s)"
-            for cfg in {128: (0, 1, 3), 64: (0, 3), 32: (0, 3)}[C]:
+            for cfg in {128: (0, 6), 64: (0,), 32: (0,)}[C]:
                 _lib.lib().vo_tune(b"pair_cfg", cfg)
                 f = t_ms(fused)
                 line += f"  fused[{cfg}] {f:.4f} ms ({fl / f / 1e9:.0f} TF/s)"

@@ -150,6 +150,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
     }
 #pragma unroll
     for (int h = 0; h < NI; ++h) {
+      if (n0 + 4 * h >= a.Co) break;  // Co % (4 * NI) != 0: the lane's run crosses the end
       float q[4] = {v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
       if (R1) {
         float rr[4];
@@ -178,7 +179,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
 // Instruction budget: every staging / fragment address is precomputed once per thread;
 // the loop body is LDS reads + MFMAs + a few global loads / LDS stores per step (the
 // first version spent ~15 VALU+SALU instructions per MFMA on address math).
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE>
+// PRIO: s_setprio(1) around each MFMA cluster (keeps hipcc from moving the cluster across
+// the barriers; guide T5) -- A/B via conv_cfg.  ABL (timing ablation, garbage results):
+// 1 = no global loads in the main loop.
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
+          int PRIO = 0, int ABL = 0>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -259,6 +264,9 @@ conv1d_kernel(ConvArgs a) {
 #pragma unroll
     for (int s = 0; s < MAXV; ++s) {
       win_ok[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
+      if constexpr (ABL == 1) {
+        if (c > 0) { win_r[s].zero(); continue; }
+      }
       win_r[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
     }
   };
@@ -287,6 +295,9 @@ conv1d_kernel(ConvArgs a) {
     for (int s = 0; s < WV; ++s) {
       const int k = min(k0 + wk[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
       w_ok[s] = wok[s] && (NICE || c0 + wq[s] < a.Ci);
+      if constexpr (ABL == 1) {
+        if (c > 0 || k0 > 0) { w_r[s].zero(); continue; }
+      }
       w_r[s].load(Wp + k * tap_stride + wg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - wq[s])));
     }
   };
@@ -339,10 +350,12 @@ conv1d_kernel(ConvArgs a) {
         const int boff = Lds<TC>::template off<2>(br, lq);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + 16 * j * P);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       }
     }
   };
@@ -370,7 +383,8 @@ conv1d_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------ host dispatch
-template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0>
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
+          int PRIO = 0, int ABL = 0>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -396,8 +410,8 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
     return VO_ERR_INVALID;
   }
   const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE>
-                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE>;
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL>
+                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL>;
   dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles);
   hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
   VO_RETURN_LAUNCH();
@@ -406,6 +420,10 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
 template <typename TIN, typename TC, typename TOUT>
 static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   const int64_t rows = (int64_t)d->B * d->T_out;
+  // short sequences (the glyph encoder / phoneme-level predictors run at T_src ~ 12): one
+  // 16- or 32-row time tile, waves spread over output channels
+  if (d->T_out <= 16 && d->Co >= 64) return launch_cfg<TIN, TC, TOUT, 2, 1, 4, 1, 4>(d, st);  // 128 x 16
+  if (d->T_out <= 32 && d->Co >= 64) return launch_cfg<TIN, TC, TOUT, 2, 2, 4, 1, 4>(d, st);  // 128 x 32
   if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4, 4>(d, st);   // 32 x 256
   if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
   if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2, 2>(d, st);  // 64 x 64
@@ -447,7 +465,12 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d->compute_dtype == VO_BF16, "conv1d: bad compute dtype");
   if (xi == VO_BF16 && yo == VO_BF16) {
     switch (d->variant) {  // HiFi-GAN MRF stages: own instantiations (same tiles as generic)
-      case 1: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
+      case 1: {
+        const int cfg = vo_tune_get("conv_cfg");
+        if (cfg == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1, 1>(d, st);
+        if (cfg == 9) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1, 0, 1>(d, st);
+        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
+      }
       case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);
       case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 4, 3>(d, st);
       case 4: return launch_cfg<bf16_t, bf16_t, bf16_t, 2, 4, 1, 4, 4, 4>(d, st);

@@ -66,7 +66,9 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
 // WC x WT waves: wave (wc, wt) owns channels [wc*C/WC, (wc+1)*C/WC) of rows [wt*16*NJ, ..+16*NJ)
 // ABL (timing ablations only, garbage results): 1 = no weight-group loads, 2 = no window /
 // residual loads, 3 = neither
-template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0>
+// PRIO (A/B only; both within run-to-run noise on the C = 128 pair): 1 = s_setprio(1) around
+// each MFMA cluster; 2 = static: the younger half of the waves runs at priority 1 (guide T5)
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0>
 __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -212,6 +214,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   for (int i = 0; i < NI; ++i) a_off[i] = rb_off(cw0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq, SHW);
   const int brow0 = wt * 16 * NJ + lr;
 
+  if constexpr (PRIO == 2)
+    if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   load_win(tile);
   store_win();
   __syncthreads();
@@ -334,10 +338,12 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
         for (int st = 0; st < S; ++st) {
           if (st + 1 < S) ld(st + 1, (st + 1) & 1);
           if (TG == 1 || g * TG + st / NC < K) {
+            if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
               for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[st & 1][i], bq[st & 1][j], acc[i][j]);
+            if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
           }
         }
         if (p1_last) p1_epilogue();
@@ -376,7 +382,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0>
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -391,7 +397,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -439,6 +445,8 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   if (C == 128) {  // 2 x 4 waves of 64 channels x 32 rows (2 waves/SIMD) beat 2 x 2 waves of 64 x 64
     if (cfg == 1) return pair_launch<128, 2, 2, 4, false, 1>(a, B, st);
     if (cfg == 3) return pair_launch<128, 1, 4, 2, false, 1>(a, B, st);
+    if (cfg == 5) return pair_launch<128, 2, 4, 2, false, 1, 0, 1>(a, B, st);
+    if (cfg == 6) return pair_launch<128, 2, 4, 2, false, 1, 0, 2>(a, B, st);
     if (cfg == 11) return pair_launch<128, 2, 4, 2, false, 1, 1>(a, B, st);
     if (cfg == 12) return pair_launch<128, 2, 4, 2, false, 1, 2>(a, B, st);
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);

@@ -13,40 +13,74 @@ namespace vo {
 
 constexpr int CP_ROWS = 256;
 
-template <typename TX>
+// CC > 0: compile-time channel count (HiFi-GAN V1: 32) -- the staging loads are then issued
+// as one batch (a runtime-trip loop serialises one HBM round trip per iteration); CC = 0:
+// any C (multiple of 8).
+template <typename TX, int CC>
 __global__ void __launch_bounds__(256) conv_post_kernel(const TX* __restrict__ x, const float* __restrict__ w,
-                                                        float bias, int T, int C, int K, float slope,
+                                                        float bias, int T, int C_, int K, float slope,
                                                         float* __restrict__ y) {
+  const int C = CC > 0 ? CC : C_;
   extern __shared__ __attribute__((aligned(16))) float cp_lds[];
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * CP_ROWS;
   const int pad = (K - 1) / 2;
   const int rows = CP_ROWS + K - 1;
-  const int P = C + 1;  // odd pitch: lanes reading the same channel of consecutive rows spread banks
+  // pitch C + 4 floats: 16-byte aligned rows, and the 16 lanes of a ds_read_b128 group
+  // (consecutive rows, same channels) land on distinct 4-bank groups
+  const int P = C + 4;
   const TX* xb = x + (int64_t)b * T * C;
   const int vpr = C / 4;
-  for (int v = threadIdx.x; v < rows * vpr; v += 256) {
+  // staging: unconditional (clamped) loads, zeroed out of range -- a load under a divergent
+  // branch is waited for immediately
+  auto stage = [&](int v, const float (&q0)[4]) {
     const int r = v / vpr, c = (v - r * vpr) * 4;
     const int t = t0 - pad + r;
-    float q[4] = {0.f, 0.f, 0.f, 0.f};
-    if (t >= 0 && t < T) {
-      load4(xb + (int64_t)t * C + c, q);
+    const bool in = t >= 0 && t < T;
+    float q[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) q[e] = q[e] > 0.f ? q[e] : q[e] * slope;
+    for (int e = 0; e < 4; ++e) q[e] = in ? fmaxf(q0[e], q0[e] * slope) : 0.f;  // 0 <= slope <= 1
+    *reinterpret_cast<float4*>(cp_lds + r * P + c) = make_float4(q[0], q[1], q[2], q[3]);
+  };
+  auto src = [&](int v) {
+    const int r = v / vpr, c = (v - r * vpr) * 4;
+    return xb + (int64_t)min(max(t0 - pad + r, 0), T - 1) * C + c;
+  };
+  if constexpr (CC > 0) {
+    constexpr int NV = ((CP_ROWS + 30) * (CC / 4) + 255) / 256;  // K <= 31
+    float q[NV][4];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = min(threadIdx.x + i * 256, rows * vpr - 1);
+      load4(src(v), q[i]);
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) cp_lds[r * P + c + e] = q[e];
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * 256;
+      if (v < rows * vpr) stage(v, q[i]);
+    }
+  } else {
+    for (int v = threadIdx.x; v < rows * vpr; v += 256) {
+      float q[4];
+      load4(src(v), q);
+      stage(v, q);
+    }
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= T) return;
-  float acc = bias;
+  float acc0 = bias, acc1 = 0.f;
   for (int k = 0; k < K; ++k) {
     const float* row = cp_lds + (threadIdx.x + k) * P;
-    const float* wk = w + k * C;
-    for (int c = 0; c < C; ++c) acc += wk[c] * row[c];
+    const float* wk = w + k * C;  // wave-uniform: scalar loads
+    for (int c = 0; c < C; c += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(row + c);
+      const float4 d = *reinterpret_cast<const float4*>(row + c + 4);
+      acc0 += wk[c] * a.x + wk[c + 1] * a.y + wk[c + 2] * a.z + wk[c + 3] * a.w;
+      acc1 += wk[c + 4] * d.x + wk[c + 5] * d.y + wk[c + 6] * d.z + wk[c + 7] * d.w;
+    }
   }
-  y[(int64_t)b * T + t] = tanhf(acc);
+  y[(int64_t)b * T + t] = tanhf(acc0 + acc1);
 }
 
 template <typename TY>
@@ -114,15 +148,18 @@ using namespace vo;
 extern "C" int vo_conv_post(const void* x, int x_dtype, const float* w, float bias, int B, int T, int C, int K,
                             float slope, float* y, void* stream) {
   VO_CHECK_ARG(x && w && y, "conv_post: null pointer");
-  VO_CHECK_ARG(C % 4 == 0 && K % 2 == 1 && C <= 512 && K <= 31, "conv_post: C=%d K=%d unsupported", C, K);
+  VO_CHECK_ARG(C % 8 == 0 && K % 2 == 1 && C <= 512 && K <= 31, "conv_post: C=%d K=%d unsupported", C, K);
+  VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "conv_post: slope %g outside [0, 1]", slope);
   VO_CHECK_ARG(B > 0 && T > 0, "conv_post: empty");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)((T + CP_ROWS - 1) / CP_ROWS), (unsigned)B);
-  const size_t lds = (size_t)(CP_ROWS + K - 1) * (C + 1) * sizeof(float);
-  if (x_dtype == VO_BF16)
-    hipLaunchKernelGGL(conv_post_kernel<bf16_t>, grid, dim3(256), lds, st, (const bf16_t*)x, w, bias, T, C, K, slope, y);
+  const size_t lds = (size_t)(CP_ROWS + K - 1) * (C + 4) * sizeof(float);
+  if (x_dtype == VO_BF16 && C == 32)
+    hipLaunchKernelGGL((conv_post_kernel<bf16_t, 32>), grid, dim3(256), lds, st, (const bf16_t*)x, w, bias, T, C, K, slope, y);
+  else if (x_dtype == VO_BF16)
+    hipLaunchKernelGGL((conv_post_kernel<bf16_t, 0>), grid, dim3(256), lds, st, (const bf16_t*)x, w, bias, T, C, K, slope, y);
   else
-    hipLaunchKernelGGL(conv_post_kernel<float>, grid, dim3(256), lds, st, (const float*)x, w, bias, T, C, K, slope, y);
+    hipLaunchKernelGGL((conv_post_kernel<float, 0>), grid, dim3(256), lds, st, (const float*)x, w, bias, T, C, K, slope, y);
   VO_RETURN_LAUNCH();
 }
 
