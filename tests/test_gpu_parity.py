@@ -282,6 +282,33 @@ def test_conv1d_vs_torch_fp32(B, T, Ci, Co, K, dil, act, dt, tol):
     assert rel_l2(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("B,T,C,K,dil", [(2, 1000, 256, 11, 5), (3, 300, 256, 3, 1), (1, 1, 256, 7, 3),
+                                         (2, 4096, 256, 7, 3), (2, 517, 128, 11, 1)])
+def test_conv1d_mrf_stage0_tiles(B, T, C, K, dil, cfg):
+    """MRF stage-0 conv (variant 1: 256 x 256 tile, conv_cfg 1: 128 x 128) with lrelu prologue,
+    residual and accumulate epilogue, against PyTorch fp32 at ragged T and Co < tile."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import _lib, ops
+    g = torch.Generator().manual_seed(T * 7 + K)
+    x = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+    w = torch.randn(C, C, K, generator=g) / (C * K) ** 0.5
+    b = torch.randn(C, generator=g) * 0.1
+    res = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+    pad = dil * (K - 1) // 2
+    ref = F.conv1d(F.leaky_relu(x.float(), 0.1).transpose(1, 2), w, b, padding=pad, dilation=dil).transpose(1, 2)
+    ref = (ref + res.float()) * 0.5
+    wp = ops.pack_conv_weight(w.cuda(), torch.bfloat16)
+    _lib.lib().vo_tune(b"conv_cfg", cfg)
+    try:
+        out = ops.conv1d(x.cuda(), wp, b.cuda(), Co=C, K=K, dil=dil, pad=pad, pre_act=ops.ACT_LRELU, pre_slope=0.1,
+                         res1=res.cuda(), out_scale=0.5, variant=1)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().vo_tune(b"conv_cfg", 0)
+    assert rel_l2(out.float().cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("B,L,lens", [(4, 512, [512, 300, 1, 77]), (2, 1000, [1000, 999]), (3, 12, [12, 7, 5])])
 @pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])
 def test_attention_vs_oracle(B, L, lens, dt, tol):
@@ -299,7 +326,7 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
     assert rel_l2(out.float().cpu(), ref) < tol
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
                                      # several tiles per persistent workgroup (pipelined window/weights)

@@ -427,6 +427,15 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4, 4>(d, st);   // 32 x 256
   if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
   if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2, 2>(d, st);  // 64 x 64
+  if constexpr (sizeof(TC) == 2) {
+    // decoder shapes at B*T = 16384 rows (tools/ab_sb.py gen): wide outputs (FFN w_1 k9 1024,
+    // fused q/k/v 768) -> 256 x 256 tiles (-18 %); 1x1 convs to 256 channels -> 64 x 128
+    // (twice the workgroups, -12 %).  gen_cfg 1 forces the 128 x 128 tile (A/B).
+    if (vo_tune_get("gen_cfg") != 1) {
+      if (d->Co >= 768 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
+      if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
+    }
+  }
   return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }
 
@@ -465,11 +474,11 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d->compute_dtype == VO_BF16, "conv1d: bad compute dtype");
   if (xi == VO_BF16 && yo == VO_BF16) {
     switch (d->variant) {  // HiFi-GAN MRF stages: own instantiations (same tiles as generic)
-      case 1: {
-        const int cfg = vo_tune_get("conv_cfg");
-        if (cfg == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1, 1>(d, st);
-        if (cfg == 9) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1, 0, 1>(d, st);
-        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
+      case 1: {  // C = 256: 256 x 256 tile, 8 waves of 64 co x 128 rows (each weight tap feeds
+                 // twice the rows of the 128 x 128 tile: 0.095/0.151/0.208 -> 0.077/0.125/0.172 ms
+                 // for k = 3/7/11 at B = 32, bit-identical).  conv_cfg 1 = the 128 x 128 tile.
+        if (vo_tune_get("conv_cfg") == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
+        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
       }
       case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);
       case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 4, 3>(d, st);

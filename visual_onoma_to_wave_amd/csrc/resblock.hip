@@ -65,10 +65,19 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
 
 // WC x WT waves: wave (wc, wt) owns channels [wc*C/WC, (wc+1)*C/WC) of rows [wt*16*NJ, ..+16*NJ)
 // ABL (timing ablations only, garbage results): 1 = no weight-group loads, 2 = no window /
-// residual loads, 3 = neither
+// residual loads, 3 = neither; bit 4 = no weight LDS stores
 // PRIO (A/B only; both within run-to-run noise on the C = 128 pair): 1 = s_setprio(1) around
 // each MFMA cluster; 2 = static: the younger half of the waves runs at priority 1 (guide T5)
-template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0>
+// SB: pin the software pipeline with sched_barrier: the fragment reads of step st + 1 are
+// issued before, and kept above, the MFMAs of step st (hipcc otherwise sinks every
+// ds_read down to its first use and waits lgkmcnt right before each MFMA pair, exposing
+// the full LDS latency once per pair)
+// IP: T1 overlays the window (the window is dead once P1's MFMAs end): LDS per tile drops
+// from window + T1 to max(window, T1), so the C = 128 tile can grow to 256 rows and each
+// streamed weight tap feeds twice the MFMAs.  Costs two barriers per tile and a window store
+// after P2 instead of during it.
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
+          bool IP = false>
 __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -92,8 +101,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);  // [NC][win_rows][32]
-  bf16_t* t1 = win + NC * win_rows * 32;               // [NC][T1R][32]
-  bf16_t* wls = t1 + NC * T1R * 32;                    // RES: [2][K] taps; else [2 bufs][TG] taps
+  bf16_t* t1 = IP ? win : win + NC * win_rows * 32;   // [NC][T1R][32]
+  bf16_t* wls = IP ? win + NC * max(win_rows, T1R) * 32 : t1 + NC * T1R * 32;  // RES: [2][K] taps; else [2 bufs][TG] taps
   float* sbias = reinterpret_cast<float*>(wls + (RES ? 2 * K : 2 * TG) * TAPE);  // [b1 | b2]
   bf16_t* spare = reinterpret_cast<bf16_t*>(sbias + 2 * C);  // 16 B sink for idle staging slots
 
@@ -125,10 +134,41 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     wg_l[s] = t * TAPE + pl * C * 32 + rb_off(co, q, SHW);
   }
   u32x4 wr[GV];
-  auto load_group = [&](int gi) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
+  // GL: the group is copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+  // instruction, lane-linear in LDS): no VGPR staging and no ds_write (the ablation without
+  // weight stores ran 25-30 % faster).  The XOR swizzle moves to the source address: LDS
+  // slot p of a group holds (tap t, plane pl, row co, chunk q' = q ^ swz(co)).
+  constexpr int GLN = GL ? (TG * TAPV) / (64 * NW) : 1;  // DMA instructions per wave per group
+  static_assert(!GL || (TG * TAPV) % (64 * NW) == 0, "glds: group must split into whole wave-KiB");
+  int gl_src[GLN];
+  if constexpr (GL) {
+#pragma unroll
+    for (int s = 0; s < GLN; ++s) {
+      const int p = (s * NW + wave) * 64 + lane;
+      const int t = p / TAPV, vv = p - t * TAPV;
+      const int pl = vv / (C * 4), rem = vv - pl * C * 4;
+      const int co = rem >> 2, q = (rem & 3) ^ ((co >> (SHW - 1)) & 2);
+      gl_src[s] = t * C * C + co * C + pl * 32 + q * 8;
+    }
+  }
+  auto load_group = [&](int gi, int buf) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
     const int ph = gi >= NG;
     const int k0 = (gi - ph * NG) * TG;
     const bf16_t* W = ph ? a.w2 : a.w1;
+    if constexpr (GL) {
+      if constexpr ((ABL & 1) != 0) return;
+      typedef __attribute__((address_space(3))) void lds_void;
+      typedef const __attribute__((address_space(1))) void g_void;
+#pragma unroll
+      for (int s = 0; s < GLN; ++s) {
+        // taps past K (last group, K % TG != 0) re-read tap K - 1; their MFMAs are skipped
+        const int kk = min(k0 + gl_src[s] / (C * C), K - 1);
+        const bf16_t* src = W + (int64_t)kk * C * C + (gl_src[s] % (C * C));
+        bf16_t* dst = wls + buf * TG * TAPE + (s * NW + wave) * 64 * 8;
+        __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < GV; ++s) {
       const int k = k0 + (wg_t[s] < TG ? wg_t[s] : 0);
@@ -139,6 +179,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     }
   };
   auto store_group = [&](int buf) {
+    if constexpr ((ABL & 4) != 0 || GL) return;
 #pragma unroll
     for (int s = 0; s < GV; ++s)
       if (GV * NT == TG * TAPV || wg_t[s] < TG) *reinterpret_cast<u32x4*>(wls + buf * TG * TAPE + wg_l[s]) = wr[s];
@@ -168,20 +209,22 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       }
     }
   } else {
-    load_group(0);
+    load_group(0, 0);
     store_group(0);
   }
 
   // ---- input window staging geometry (row-major vectors: consecutive lanes, consecutive 16 B)
   int xr[MAXW], xl[MAXW], xg[MAXW];
-#pragma unroll
-  for (int s = 0; s < MAXW; ++s) {
+  // (IP: recomputed at each use from tid -- a few VALU ops instead of 3 * MAXW live VGPRs)
+  auto win_geom = [&](int s) {
     const int v = tid + s * NT;
     const int r = v / VPR, rem = v - r * VPR;
     xr[s] = r < win_rows ? r : 0x40000000;
     xg[s] = rem * 8;
     xl[s] = (rem >> 2) * win_rows * 32 + rb_off(r, rem & 3, 2);
-  }
+  };
+#pragma unroll
+  for (int s = 0; s < MAXW; ++s) win_geom(s);
   // Global loads are unconditional (clamped rows, zeroed when written to LDS): a load under a
   // divergent branch gets an immediate vmcnt(0) from the compiler and the prefetch is lost.
   u32x4 xw[MAXW];
@@ -192,6 +235,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     const bf16_t* base = a.x + (int64_t)b * T * C;
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
+      if constexpr (IP) win_geom(s);
       const int t = R0 + xr[s];
       xw_ok[s] = t >= 0 && t < T;
       if constexpr ((ABL & 2) != 0)
@@ -203,6 +247,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   auto store_win = [&]() {
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
+      if constexpr (IP) win_geom(s);
       const u32x4 v = lrelu8(xw[s], slope);
       // idle slots (rows past the window) write the spare row after the bias table
       *reinterpret_cast<u32x4*>(xr[s] < win_rows ? win + xl[s] : spare) = xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
@@ -218,6 +263,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   load_win(tile);
   store_win();
+  if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   f32x4 acc[NI][NJ];
@@ -244,22 +290,29 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 
     // residual / accumulator rows of this tile (epilogue layout), consumed after P2
     u32x4 xres[NJ][NH], ares[NJ][NH];
-    const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
+    auto load_res = [&]() {
+      const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);  // rows past the tile are not stored
-      const int64_t off = ((int64_t)b * T + pos) * C + n0;
+      for (int j = 0; j < NJ; ++j) {
+        const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);  // rows past the tile are not stored
+        const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        if constexpr ((ABL & 2) != 0) {
-          xres[j][h] = ares[j][h] = u32x4{(unsigned)pos, 0u, 0u, 0u};
-        } else {
-          xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
-          ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+        for (int h = 0; h < NH; ++h) {
+          if constexpr ((ABL & 2) != 0) {
+            xres[j][h] = ares[j][h] = u32x4{(unsigned)pos, 0u, 0u, 0u};
+          } else {
+            xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+            if constexpr (!IP) ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+          }
         }
       }
+    };
+    // IP keeps the window prefetch live through P2, so its residual rows are fetched one
+    // group (a tap: >= 1k MFMA cycles) before the epilogue instead of a whole tile ahead
+    if constexpr (!IP) {
+      load_res();
+      load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
     }
-    load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
 
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -315,7 +368,11 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       auto group = [&](int ph, int g, bool p1_last, bool p2_first) {
         const int gi = ph * NG + g;
         const bool more = has_next || gi + 1 < 2 * NG;
-        load_group(gi + 1 == 2 * NG ? 0 : gi + 1);  // unconditional; stored only if needed
+        if constexpr (IP) {  // next window: fetched at P2 start, stored after P2 (registers
+          if (gi == NG) load_win(has_next ? tile + 1 : tile);  // are not live during P1)
+          if (gi + 1 == 2 * NG) load_res();
+        }
+        load_group(gi + 1 == 2 * NG ? 0 : gi + 1, (gcount + 1) & 1);  // unconditional; stored only if needed
         const bf16_t* wb = wls + (gcount & 1) * TG * TAPE;
         const bf16_t* src = ph ? t1 : win;
         const int plane = ph ? T1R * 32 : win_rows * 32;
@@ -323,6 +380,15 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
         // software-pipelined over the group's TG x NC (tap, plane) steps: the fragments of step
         // st + 1 are read from LDS before the MFMAs of step st (two named register sets)
         constexpr int S = TG * NC;
+        if constexpr (!SB) {  // plain steps: hipcc schedules the reads (fewer live fragments)
+#pragma unroll
+          for (int st = 0; st < S; ++st) {
+            if (TG == 1 || g * TG + st / NC < K) {
+              const int t = st / NC, c = st - t * NC;
+              tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + (g * TG + t) * step);
+            }
+          }
+        }
         Frag<bf16_t> af[2][NI], bq[2][NJ];
         auto ld = [&](int st, int set) {
           const int t = st / NC, c = st - t * NC;
@@ -333,10 +399,11 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 #pragma unroll
           for (int j = 0; j < NJ; ++j) bq[set][j].load(src + boff + 16 * j * 32);
         };
-        ld(0, 0);
+        if constexpr (SB) ld(0, 0);
 #pragma unroll
-        for (int st = 0; st < S; ++st) {
+        for (int st = 0; st < (SB ? S : 0); ++st) {
           if (st + 1 < S) ld(st + 1, (st + 1) & 1);
+          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
           if (TG == 1 || g * TG + st / NC < K) {
             if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -345,12 +412,18 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
               for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[st & 1][i], bq[st & 1][j], acc[i][j]);
             if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
           }
+          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
         }
-        if (p1_last) p1_epilogue();
-        if (p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
+        if (!IP && p1_last) p1_epilogue();
+        if (!IP && p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
         if (more) store_group((gcount + 1) & 1);
+        if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed
         __syncthreads();
         ++gcount;
+        if (IP && p1_last) {  // every wave is past its window reads: T1 may overwrite them
+          p1_epilogue();
+          __syncthreads();
+        }
       };
       for (int g = 0; g < NG - 1; ++g) group(0, g, false, false);
       group(0, NG - 1, true, false);
@@ -359,6 +432,17 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
+    if constexpr (IP) {  // IP: the MRF accumulator rows are read here (registers are short)
+      if (a.acc) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);
+          const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) ares[j][h] = *reinterpret_cast<const u32x4*>(a.acc + off + 8 * h);
+        }
+      }
+    }
     float b2z[8 * NH];
     lane_bias(1, b2z);
 #pragma unroll
@@ -379,10 +463,15 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       }
     }
     if constexpr (RES) __syncthreads();
+    if constexpr (IP) {  // P2's T1 reads ended at the last group barrier
+      if (has_next) store_win();
+      __syncthreads();
+    }
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0>
+template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
+          bool IP = false>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -391,13 +480,14 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
   a.tiles_per_b = (a.T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
   const size_t wtaps = RES ? 2 * (size_t)a.K : 2 * (size_t)TG;
-  const size_t lds = ((size_t)(R1 + 2 * h1) + (R1 + 16) + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t) +
+  const size_t act_rows = IP ? std::max<size_t>(R1 + 2 * h1, R1 + 16) : (size_t)(R1 + 2 * h1) + (R1 + 16);
+  const size_t lds = (act_rows + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t) +
                      2 * C * sizeof(float) + 16;
   if (lds > 160 * 1024) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -432,29 +522,31 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   a.T = T; a.K = K; a.dil = dil; a.slope = slope; a.out_scale = out_scale;
   a.tiles_per_b = a.ntiles = 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // measured on MI355X, B=32 MRF shapes (tools/ab_pair.py): C=32 K<=7 -> 256-row tiles (3
-  // workgroups/CU), K=11 -> 512-row tiles; C=64 K=3 -> resident weights, K>=7 -> 2-tap groups;
-  // C=128 -> 128-row tiles, one streamed tap per group.
-  // pair_cfg selects the alternatives for A/B runs.
+  // measured on MI355X, B=32 MRF shapes (tools/ab_pair.py, tools/ab_sb.py): C=32 K<=7 ->
+  // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
+  // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
   if (C == 32) {
     if (cfg == 3) return pair_launch<32, 1, 4, 8, true, 1>(a, B, st);
     const bool small = cfg == 0 ? K <= 7 : cfg == 1;
     return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
   }
-  if (C == 128) {  // 2 x 4 waves of 64 channels x 32 rows (2 waves/SIMD) beat 2 x 2 waves of 64 x 64
-    if (cfg == 1) return pair_launch<128, 2, 2, 4, false, 1>(a, B, st);
-    if (cfg == 3) return pair_launch<128, 1, 4, 2, false, 1>(a, B, st);
-    if (cfg == 5) return pair_launch<128, 2, 4, 2, false, 1, 0, 1>(a, B, st);
-    if (cfg == 6) return pair_launch<128, 2, 4, 2, false, 1, 0, 2>(a, B, st);
-    if (cfg == 11) return pair_launch<128, 2, 4, 2, false, 1, 1>(a, B, st);
-    if (cfg == 12) return pair_launch<128, 2, 4, 2, false, 1, 2>(a, B, st);
+  if (C == 128) {
+    // 2 x 4 waves of 64 channels (2 waves/SIMD), weights by LDS-DMA.  k = 3: 128-row tiles;
+    // k >= 7: 192-row tiles with T1 over the window (IP), 8 % faster at k = 11 (tools/ab_sb.py).
+    // pair_cfg 1 = the register-staged 128-row kernel, 13 = its no-global-load timing ablation.
+    // In the bench step: s1 0.62 -> 0.545 ms per launch (tools/bench_ab.sh).
+    if (cfg == 1) return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
-    return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
+    if (cfg == 2) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
+    if (cfg == 3) return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
+    if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
+    return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
   }
-  if (cfg == 3) return pair_launch<64, 1, 4, 4, false, 2>(a, B, st);
-  if (cfg == 4) return pair_launch<64, 1, 4, 8, false, 1>(a, B, st);
+  // C = 64: k = 3 -> both convs resident in LDS; k >= 7 -> 2-tap groups, register staged.
+  // pair_cfg 1 = LDS-DMA weights + pinned fragment pipeline: 7 % faster alone (tools/ab_sb.py)
+  // but 15 % slower inside the bench step with the MRF accumulator (tools/bench_ab.sh)
   if (K <= 3 && cfg != 2) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
-  if (cfg == 1) return pair_launch<64, 1, 8, 2, false, 4>(a, B, st);
+  if (cfg == 1) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, true, true>(a, B, st);
   return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);
 }

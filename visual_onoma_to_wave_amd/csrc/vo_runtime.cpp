@@ -2,6 +2,7 @@
 // the loader test checks against include/vonoma.h.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/vonoma.h"
@@ -19,11 +20,30 @@ extern "C" const char* vo_last_error(void) { return g_err; }
 
 extern "C" int vo_version(void) { return 1; }
 
-// experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0
-static const char* const kKnobs[] = {"pair_cfg", "conv_cfg"};
-static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {0, 0};
+// experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0.
+// VO_TUNE="pair_cfg=1,conv_cfg=1" presets them for a whole process (bench A/B).
+static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg"};
+static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {0, 0, 0};
+
+static void knobs_from_env() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = getenv("VO_TUNE");
+  if (!e) return;
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s", e);
+  for (char* tok = strtok(buf, ","); tok; tok = strtok(nullptr, ",")) {
+    char* eq = strchr(tok, '=');
+    if (!eq) continue;
+    *eq = 0;
+    for (size_t i = 0; i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
+      if (!strcmp(tok, kKnobs[i])) g_knobs[i] = atoi(eq + 1);
+  }
+}
 
 extern "C" int vo_tune(const char* key, int value) {
+  knobs_from_env();
   for (size_t i = 0; key && i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
     if (!strcmp(key, kKnobs[i])) {
       g_knobs[i] = value;
@@ -34,6 +54,7 @@ extern "C" int vo_tune(const char* key, int value) {
 }
 
 extern "C" int vo_tune_get(const char* key) {
+  knobs_from_env();
   for (size_t i = 0; i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
     if (!strcmp(key, kKnobs[i])) return g_knobs[i];
   return 0;
