@@ -85,6 +85,10 @@ typedef struct vo_conv1d_desc {
   int transposed, up_stride, up_pad, up_cout, up_tout; /* polyphase ConvTranspose1d */
   int variant;        /* 0 = generic; 1..4 = HiFi-GAN MRF stage 0..3 (bf16 I/O): a kernel
                          instantiation of its own, so profiles attribute the stages   */
+  int stride;         /* 0/1 = 1; 2..4: output row o reads input rows o*stride + k*dil - pad
+                         (HiFi-GAN MPD Conv2d (k,1)/(s,1) per period column, MSD Conv1d)  */
+  int groups;         /* 0/1 = dense; g: grouped conv, w packed dense [K][Co][Ci] with zeros
+                         outside the g diagonal blocks (MSD grouped Conv1d)              */
 } vo_conv1d_desc;
 int vo_conv1d(const vo_conv1d_desc* d, void* stream);
 
@@ -215,6 +219,34 @@ int vo_transpose_bct(const float* x, int B, int C, int T, void* y, int y_dtype, 
  * 22-36,323-337).  window: (n_fft) fp32; fb: (n_fft/2+1, n_mels) fp32. */
 int vo_stft_mel(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
                 int hop, int n_mels, float log_floor, float* mel, float* energy, void* stream);
+/* General framing: frame f covers reflect-padded samples [f*hop - pad, f*hop - pad + n_fft),
+ * F = 1 + (N + 2*pad - n_fft) / hop; |X| = sqrt(re^2 + im^2 + mag_eps); clip != 0 clamps the
+ * input to [-1, 1].  HiFi-GAN's training mel (pad (n_fft - hop)/2, center=False, mag_eps 1e-9,
+ * no clip, slaney fb) and vo_stft_mel (pad n_fft/2, eps 0, clip). */
+int vo_stft_mel_ex(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
+                   int hop, int n_mels, int pad, float mag_eps, int clip, float log_floor, float* mel,
+                   float* energy, void* stream);
+
+/* ------------------------------------------------------------------ HiFi-GAN training (C5)
+ * Discriminator glue (the reference ships no discriminator code, only
+ * the training hyper-parameters of scripts/hifigan/config.json):
+ *  vo_pack_grouped: (Co, Ci/groups, K) fp32 -> dense [K][Co][Ci_pad] block-diagonal (zeros
+ *    outside the groups and for ci >= Ci) for vo_conv1d's groups mode;
+ *  vo_period_fold: wav (B, T) -> (B*P, ceil(T/P), 8) channels-last, the MPD's reflect pad to a
+ *    multiple of P and (T/P, P) view with each period column a separate sequence;
+ *  vo_wav_cl8: (B, T) -> (B, T, 8) (channel 0); vo_avgpool_wav: AvgPool1d(4, 2, padding 2),
+ *    (B, T) -> (B, T/2 + 1);
+ *  vo_gan_reduce: *out += sum over a (rows x width) view of |a-b| (kind 0), (1-a)^2 (kind 1)
+ *    or a^2 (kind 2); vo_gan_reduce_grad: ga = *scale * d(sum)/da. */
+int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
+                    int dst_dtype, void* stream);
+int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
+int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
+int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);
+int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
+                  int dtype, float* out, void* stream);
+int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
+                       int width, int dtype, const float* scale, void* ga, int ldg, void* stream);
 
 #ifdef __cplusplus
 }

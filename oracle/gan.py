@@ -1,0 +1,124 @@
+"""ORACLE (test infrastructure only) -- HiFi-GAN V1 training objective restated on the CPU.
+
+PARITY UNPINNED: the reference repository contains no discriminator, loss or training-mel
+code for its vocoder -- only the generator (scripts/hifigan/models.py) and the training
+hyper-parameters (scripts/hifigan/config.json:1-31: batch 16, AdamW lr 2e-4, betas
+(0.8, 0.99), lr_decay 0.999, segment 8192, n_fft/win 1024, hop 256, fmax_for_loss null).
+This file restates the published HiFi-GAN V1 recipe that config belongs to (Kong et al.
+2020, "HiFi-GAN", sections 2.2-2.3 and appendix A) as plain fp32 PyTorch-CPU functional ops
+over effective (weight-norm / spectral-norm resolved) weights, in the reference layouts
+(NCW / NCHW), as the checker for visual_onoma_to_wave_amd.hifigan.discriminators:
+
+* mpd(): per period p, reflect-pad T to a multiple of p, view (B, 1, T/p, p), 5 x
+  [Conv2d (5,1) stride (3,1) (last stride 1) -> lrelu 0.1] + Conv2d (3,1) post; score flattened.
+* msd(): 3 scales (raw, AvgPool1d(4,2,2) once / twice) x [Conv1d 1->128 k15, grouped strided
+  k41 convs, Conv1d k5] + post Conv1d k3.
+* losses: feature 2*sum mean|r-g|, discriminator sum mean((1-r)^2) + mean(g^2), generator
+  sum mean((1-g)^2); mel L1 on the training mel (reflect pad (n_fft-hop)/2, center=False,
+  periodic Hann, sqrt(|X|^2 + 1e-9), librosa slaney mel to sr/2, log clamp 1e-5) x 45.
+"""
+
+import torch
+import torch.nn.functional as F
+
+from .mel import librosa_mel
+
+LRELU = 0.1
+PERIODS = (2, 3, 5, 7, 11)
+MSD_CFG = [(1, 128, 15, 1, 1, 7), (128, 128, 41, 2, 4, 20), (128, 256, 41, 2, 16, 20), (256, 512, 41, 4, 16, 20),
+           (512, 1024, 41, 4, 16, 20), (1024, 1024, 41, 1, 16, 20), (1024, 1024, 5, 1, 1, 2)]
+
+
+def disc_p(ws, bs, wav, period):
+    """DiscriminatorP.forward: ws / bs = 5 conv weights (Co, Ci, 5, 1) + post (1, 1024, 3, 1)."""
+    x = wav[:, None, :]
+    b, c, t = x.shape
+    if t % period:
+        x = F.pad(x, (0, period - t % period), "reflect")
+        t = x.shape[-1]
+    x = x.view(b, c, t // period, period)
+    fmap = []
+    for i in range(5):
+        x = F.leaky_relu(F.conv2d(x, ws[i], bs[i], stride=(3, 1) if i < 4 else 1, padding=(2, 0)), LRELU)
+        fmap.append(x)
+    x = F.conv2d(x, ws[5], bs[5], padding=(1, 0))
+    fmap.append(x)
+    return torch.flatten(x, 1, -1), fmap
+
+
+def disc_s(ws, bs, wav):
+    """DiscriminatorS.forward: 7 convs of MSD_CFG + post Conv1d(1024, 1, 3, pad 1)."""
+    x = wav[:, None, :]
+    fmap = []
+    for (ci, co, k, s, g, p), w, b in zip(MSD_CFG, ws[:7], bs[:7]):
+        x = F.leaky_relu(F.conv1d(x, w, b, stride=s, padding=p, groups=g), LRELU)
+        fmap.append(x)
+    x = F.conv1d(x, ws[7], bs[7], padding=1)
+    fmap.append(x)
+    return torch.flatten(x, 1, -1), fmap
+
+
+def mpd(params, y):
+    """params: [(ws, bs)] per period -> (scores, fmaps) lists over PERIODS."""
+    out = [disc_p(ws, bs, y, p) for (ws, bs), p in zip(params, PERIODS)]
+    return [o[0] for o in out], [o[1] for o in out]
+
+
+def msd(params, y):
+    scores, fmaps = [], []
+    x = y
+    for i, (ws, bs) in enumerate(params):
+        if i:
+            x = F.avg_pool1d(x[:, None, :], 4, 2, padding=2)[:, 0]
+        s, f = disc_s(ws, bs, x)
+        scores.append(s)
+        fmaps.append(f)
+    return scores, fmaps
+
+
+def feature_loss(fmap_r, fmap_g):
+    loss = 0
+    for dr, dg in zip(fmap_r, fmap_g):
+        for rl, gl in zip(dr, dg):
+            loss = loss + torch.mean(torch.abs(rl - gl))
+    return loss * 2
+
+
+def discriminator_loss(real, gen):
+    loss = 0
+    for dr, dg in zip(real, gen):
+        loss = loss + torch.mean((1 - dr) ** 2) + torch.mean(dg ** 2)
+    return loss
+
+
+def generator_loss(gen):
+    loss = 0
+    for dg in gen:
+        loss = loss + torch.mean((1 - dg) ** 2)
+    return loss
+
+
+def mel_spectrogram(y, n_fft=1024, num_mels=80, sr=22050, hop=256, win=1024, fmin=0.0, fmax=None):
+    basis = torch.from_numpy(librosa_mel(sr, n_fft, num_mels, fmin, sr / 2.0 if fmax is None else fmax))
+    p = (n_fft - hop) // 2
+    yy = F.pad(y[:, None, :], (p, p), mode="reflect")[:, 0]
+    spec = torch.stft(yy, n_fft, hop_length=hop, win_length=win, window=torch.hann_window(win), center=False,
+                      return_complex=True)
+    mag = torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-9)
+    return torch.log(torch.clamp(torch.matmul(basis, mag), min=1e-5))
+
+
+def gan_losses(mpd_params, msd_params, y, y_hat, y_mel):
+    """The discriminator loss and the generator loss of one HiFi-GAN V1 step on the same
+    (y, y_hat): (loss_disc_all, loss_gen_all, parts)."""
+    r1, g1 = mpd(mpd_params, y)[0], mpd(mpd_params, y_hat)[0]
+    r2, g2 = msd(msd_params, y)[0], msd(msd_params, y_hat)[0]
+    loss_disc = discriminator_loss(r1, g1) + discriminator_loss(r2, g2)
+    sr1, fr1 = mpd(mpd_params, y)
+    sg1, fg1 = mpd(mpd_params, y_hat)
+    sr2, fr2 = msd(msd_params, y)
+    sg2, fg2 = msd(msd_params, y_hat)
+    mel = F.l1_loss(y_mel, mel_spectrogram(y_hat)) * 45
+    fm = feature_loss(fr1, fg1) + feature_loss(fr2, fg2)
+    adv = generator_loss(sg1) + generator_loss(sg2)
+    return loss_disc, adv + fm + mel, dict(mel=mel, fm=fm, adv=adv)

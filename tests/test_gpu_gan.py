@@ -1,0 +1,270 @@
+"""GPU parity of the HiFi-GAN training path (config C5) against the CPU
+oracle (oracle/gan.py) and plain PyTorch fp32 ops.  PARITY UNPINNED: the reference holds no
+discriminator / loss code, so the oracle restates the published HiFi-GAN V1 recipe.
+
+Tolerances (relative L2): fp32 compute 1e-4 (forward), 2e-3 (gradients: MIOpen fp32 and
+exact-f32 MFMA sum in different orders); bf16 compute 2e-2; data movement (fold, pool,
+channel padding) bit-exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import hifigan_arrays, hifigan_h, rel_l2
+from weights import load_into
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
+    (2, 1000, 128, 128, 41, 2, 4, 20), (2, 777, 128, 256, 41, 2, 16, 20), (3, 300, 256, 512, 41, 4, 16, 20),
+    (2, 129, 512, 1024, 41, 4, 16, 20), (2, 64, 1024, 1024, 41, 1, 16, 20), (4, 2731, 32, 128, 5, 3, 1, 2),
+    (6, 100, 512, 1024, 5, 3, 1, 2), (2, 5, 1024, 1024, 5, 1, 1, 2), (2, 1, 128, 256, 41, 2, 16, 20)])
+def test_strided_grouped_conv_vs_torch(B, T, Ci, Co, K, s, g, pad, dt, tol):
+    """vo_conv1d stride / groups modes (block-diagonal packed weights) + lrelu epilogue."""
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(B * T + K + s + g)
+    x = torch.randn(B, T, Ci, generator=gen)
+    w = torch.randn(Co, Ci // g, K, generator=gen) / (Ci // g * K) ** 0.5
+    b = torch.randn(Co, generator=gen) * 0.1
+    ref = F.leaky_relu(F.conv1d(x.transpose(1, 2), w, b, stride=s, padding=pad, groups=g), 0.1).transpose(1, 2)
+    wp = ops.pack_grouped_weight(w.cuda(), dt, g)
+    out = ops.conv1d(x.cuda().to(dt), wp, b.cuda(), Co=Co, K=K, pad=pad, stride=s, groups=g,
+                     post_act=ops.ACT_LRELU, post_slope=0.1, compute_dtype=dt, out_dtype=torch.float32 if
+                     dt == torch.float32 else dt)
+    assert out.shape == ref.shape
+    assert rel_l2(out.float().cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("T,p", [(8192, 2), (8192, 3), (8192, 5), (8191, 7), (8000, 11), (13, 11)])
+def test_period_fold_exact(T, p):
+    from visual_onoma_to_wave_amd import ops
+    wav = torch.randn(3, T)
+    x = wav[:, None, :]
+    if T % p:
+        x = F.pad(x, (0, p - T % p), "reflect")
+    ref = x.view(3, 1, -1, p)[:, 0]  # (B, H, p)
+    out = ops.period_fold(wav.cuda(), p, torch.float32).cpu()  # (B * p, H, 8)
+    got = out[..., 0].reshape(3, p, -1).transpose(1, 2)
+    assert torch.equal(got, ref) and torch.count_nonzero(out[..., 1:]) == 0
+
+
+def test_avgpool_and_cl8_exact():
+    from visual_onoma_to_wave_amd import ops
+    for T in (8192, 4097, 10):
+        wav = torch.randn(2, T)
+        ref = F.avg_pool1d(wav[:, None], 4, 2, padding=2)[:, 0]
+        assert torch.allclose(ops.avgpool_wav(wav.cuda()).cpu(), ref, rtol=0, atol=1e-6)
+    cl = ops.wav_cl8(wav.cuda(), torch.float32).cpu()
+    assert torch.equal(cl[..., 0], wav) and torch.count_nonzero(cl[..., 1:]) == 0
+
+
+def test_gan_reductions_and_grads():
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    a = torch.randn(6, 33, 17, dtype=torch.float64).float()
+    b = torch.randn(6, 33, 17).float()
+    ac = a.cuda().requires_grad_(True)
+    for fn, ref in ((lambda x: G.l1_mean(x, b.cuda()), lambda x: torch.mean(torch.abs(x - b))),
+                    (G.one_minus_sq_mean, lambda x: torch.mean((1 - x) ** 2)),
+                    (G.sq_mean, lambda x: torch.mean(x ** 2))):
+        ar = a.clone().requires_grad_(True)
+        r = ref(ar)
+        r.backward()
+        ac.grad = None
+        o = fn(ac)
+        o.backward()
+        assert abs(float(o) - float(r)) < 1e-5 * max(1.0, abs(float(r)))
+        assert rel_l2(ac.grad.cpu(), ar.grad) < 1e-6
+
+
+def _disc_params_mpd(mpd):
+    from visual_onoma_to_wave_amd.hifigan.discriminators import effective_weight
+    out = []
+    for d in mpd.discriminators:
+        ms = list(d.convs) + [d.conv_post]
+        out.append(([effective_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
+    return out
+
+
+def _disc_params_msd(msd):
+    from visual_onoma_to_wave_amd.hifigan.discriminators import effective_weight
+    out = []
+    for d in msd.discriminators:
+        ms = list(d.convs) + [d.conv_post]
+        out.append(([effective_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
+    return out
+
+
+def _mpd_layout(s, fm, B, p):
+    """ours (B*p, H, C) -> reference (B, C, H, p); score (B*p, H) -> flattened (B, H*p)"""
+    score = s.float().cpu().reshape(B, p, -1).transpose(1, 2).reshape(B, -1)
+    fmaps = [f.float().cpu().reshape(B, p, f.shape[1], -1).permute(0, 3, 2, 1) for f in fm[:-1]]
+    return score, fmaps
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+def test_discriminators_vs_oracle(dt, tol):
+    from oracle import gan as O
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MultiPeriodDiscriminator, MultiScaleDiscriminator
+    torch.manual_seed(0)
+    mpd, msd = MultiPeriodDiscriminator().eval(), MultiScaleDiscriminator().eval()
+    y = torch.randn(2, 8192) * 0.3
+    yh = torch.randn(2, 8192) * 0.3
+    ref_s, ref_f = O.mpd(_disc_params_mpd(mpd), yh)
+    ref_ss, ref_sf = O.msd(_disc_params_msd(msd), yh)
+    mpd, msd = mpd.cuda().set_compute_dtype(dt), msd.cuda().set_compute_dtype(dt)
+    with torch.no_grad():
+        _, gs, _, fgs = mpd(y.cuda(), yh.cuda())
+        _, gss, _, fgss = msd(y.cuda(), yh.cuda())
+    for d, p in enumerate((2, 3, 5, 7, 11)):
+        score, fmaps = _mpd_layout(gs[d], fgs[d], 2, p)
+        assert rel_l2(score, ref_s[d]) < tol, (p, rel_l2(score, ref_s[d]))
+        for l, (a, r) in enumerate(zip(fmaps, ref_f[d][:-1])):
+            assert a.shape == r.shape and rel_l2(a, r) < tol, (p, l)
+    for d in range(3):
+        assert rel_l2(gss[d].float().cpu(), ref_ss[d]) < tol, d
+        for l, (a, r) in enumerate(zip(fgss[d][:-1], ref_sf[d][:-1])):
+            assert rel_l2(a.float().cpu().transpose(1, 2), r) < tol, (d, l)
+
+
+def test_training_mel_vs_oracle():
+    from oracle import gan as O
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MelLoss
+    y = torch.randn(3, 8192) * 0.2
+    ref = O.mel_spectrogram(y)
+    m = MelLoss().cuda()
+    got = m.mel(y.cuda()).cpu()
+    assert got.shape == ref.shape == (3, 80, 32)
+    assert rel_l2(got, ref) < 1e-5
+
+
+def _gen(device):
+    from visual_onoma_to_wave_amd import hifigan
+    g = hifigan.Generator(hifigan.AttrDict(hifigan_h()))
+    load_into(g, hifigan_arrays())
+    return g.to(device)
+
+
+def test_generator_train_forward_matches_inference():
+    g = _gen("cuda").set_compute_dtype(torch.float32)
+    mel = torch.randn(2, 32, 80).cuda()
+    with torch.no_grad():
+        a = g.train_forward(mel)
+        g.eval()
+        b = g.run(mel)
+    assert rel_l2(a.cpu(), b.cpu()) < 1e-5
+
+
+def _leaves(m):
+    """(leaf copies, effective-weight fn) of a weight-normed / spectral-normed (eval) conv: the
+    same parameterisation on both sides, so leaf gradients compare directly."""
+    if hasattr(m, "weight_g"):
+        v = m.weight_v.detach().clone().requires_grad_(True)
+        g = m.weight_g.detach().clone().requires_grad_(True)
+        return [v, g], lambda: torch._weight_norm(v, g, 0)
+    w = m.weight_orig.detach().clone().requires_grad_(True)
+    u, vv = m.weight_u.detach().clone(), m.weight_v.detach().clone()
+    return [w], lambda: w / torch.dot(u, torch.mv(w.reshape(w.shape[0], -1), vv))
+
+
+def _module_leaves(m):
+    return [m.weight_v, m.weight_g] if hasattr(m, "weight_g") else [m.weight_orig]
+
+
+def test_gan_step_gradients_vs_oracle():
+    """L_D and L_G of one HiFi-GAN step and their gradients wrt every G and D parameter, HIP
+    autograd (fp32 compute) vs the CPU oracle's autograd, on the same weights and batch."""
+    from oracle import gan as O
+    from oracle import vocoder as V
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MelLoss, MultiPeriodDiscriminator,
+                                                                  MultiScaleDiscriminator, discriminator_loss,
+                                                                  feature_loss, generator_loss)
+    from visual_onoma_to_wave_amd.hifigan.train import _single
+    torch.manual_seed(1)
+    B = 2
+    mel = torch.randn(B, 80, 32) - 4.0
+    y = torch.tanh(torch.randn(B, 8192) * 0.3)
+    g = _gen("cpu")
+    mpd, msd = MultiPeriodDiscriminator().eval(), MultiScaleDiscriminator().eval()
+    dmods = [m for d in list(mpd.discriminators) + list(msd.discriminators) for m in list(d.convs) + [d.conv_post]]
+    # ---- oracle on CPU leaf copies, fp32 autograd
+    gp = {k: v.detach().clone().requires_grad_(True) for k, v in g.state_dict().items()}
+    leaves, effs = [], []
+    for m in dmods:
+        lv, fn = _leaves(m)
+        leaves.append(lv)
+        effs.append(fn)
+    dbias = [m.bias.detach().clone().requires_grad_(True) for m in dmods]
+
+    def params():
+        ws = [fn() for fn in effs]
+        out, i = [], 0
+        for n in [6] * 5 + [8] * 3:
+            out.append((ws[i:i + n], dbias[i:i + n]))
+            i += n
+        return out[:5], out[5:]
+
+    h = hifigan_h()
+    yh_ref = V.generator(V.fold_weight_norm(gp), mel, h)[:, 0]
+    y_mel = O.mel_spectrogram(y)
+    mp, sp = params()
+    ld_ref = O.discriminator_loss(O.mpd(mp, y)[0], O.mpd(mp, yh_ref.detach())[0]) + \
+        O.discriminator_loss(O.msd(sp, y)[0], O.msd(sp, yh_ref.detach())[0])
+    dl_flat = [t for lv in leaves for t in lv] + dbias
+    gd_ref = torch.autograd.grad(ld_ref, dl_flat)
+    mp, sp = params()
+    _, lg_ref, _ = O.gan_losses(mp, sp, y, yh_ref, y_mel)
+    gg_ref = torch.autograd.grad(lg_ref, [gp[k] for k in gp])
+    # ---- HIP path, fp32 compute (D in eval: spectral norm without power iteration)
+    g = g.cuda().set_compute_dtype(torch.float32)
+    g.train()
+    mpd, msd = mpd.cuda().set_compute_dtype(torch.float32), msd.cuda().set_compute_dtype(torch.float32)
+    dmods = [m for d in list(mpd.discriminators) + list(msd.discriminators) for m in list(d.convs) + [d.conv_post]]
+    mloss = MelLoss().cuda()
+    yc = y.cuda()
+    yh = g.train_forward(mel.transpose(1, 2).contiguous().cuda())
+    assert rel_l2(yh.detach().cpu(), yh_ref.detach()) < 1e-4
+    r1, g1, _, _ = mpd(yc, yh.detach())
+    r2, g2, _, _ = msd(yc, yh.detach())
+    ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
+    assert abs(float(ld) - float(ld_ref)) < 1e-4 * abs(float(ld_ref))
+    gd = torch.autograd.grad(ld, [t for m in dmods for t in _module_leaves(m)] + [m.bias for m in dmods])
+    assert len(gd) == len(gd_ref)
+    for i, (a, r) in enumerate(zip(gd, gd_ref)):
+        assert rel_l2(a.cpu(), r) < 2e-3, (i, rel_l2(a.cpu(), r))
+    # generator step (D frozen, real features without graph)
+    with torch.no_grad():
+        y_mel_c = mloss.mel(yc)
+    for p in list(mpd.parameters()) + list(msd.parameters()):
+        p.requires_grad_(False)
+    loss_mel = mloss(yh, y_mel_c) * 45
+    _, fr_f = _single(mpd, yc, False)
+    _, fr_s = _single(msd, yc, False)
+    sg_f, fg_f = _single(mpd, yh, True)
+    sg_s, fg_s = _single(msd, yh, True)
+    lg = (generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
+          + loss_mel)
+    assert abs(float(lg) - float(lg_ref)) < 1e-4 * abs(float(lg_ref))
+    names = list(gp)
+    named = dict(g.named_parameters())
+    gg = torch.autograd.grad(lg, [named[k] for k in names])
+    for k, a, r in zip(names, gg, gg_ref):
+        assert rel_l2(a.cpu(), r) < 2e-3, (k, rel_l2(a.cpu(), r))
+
+
+def test_trainer_step_bf16():
+    from visual_onoma_to_wave_amd import hifigan
+    g = _gen("cuda")
+    h = hifigan.AttrDict(hifigan_h())
+    tr = hifigan.HifiGanTrainer(g, h).set_compute_dtype(torch.bfloat16)
+    before = g.conv_pre.weight_v.detach().clone()
+    mel = (torch.randn(4, 32, 80) - 4).cuda()
+    y = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
+    for _ in range(2):
+        losses = tr.step(mel, y)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(v) for v in losses.values())
+    assert not torch.equal(before, g.conv_pre.weight_v.detach())

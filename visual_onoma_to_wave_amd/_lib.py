@@ -38,6 +38,7 @@ class Conv1dDesc(ctypes.Structure):
         ("transposed", c_int), ("up_stride", c_int), ("up_pad", c_int), ("up_cout", c_int),
         ("up_tout", c_int),
         ("variant", c_int),
+        ("stride", c_int), ("groups", c_int),
     ]
 
 
@@ -88,6 +89,16 @@ _SIGNATURES = {
     "vo_transpose_bct": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "vo_stft_mel": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p, c_void_p, c_void_p]),
+    "vo_stft_mel_ex": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                               c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    "vo_pack_grouped": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "vo_period_fold": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "vo_wav_cl8": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
+    "vo_avgpool_wav": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "vo_gan_reduce": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
+                              c_void_p]),
+    "vo_gan_reduce_grad": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
+                                   c_void_p, c_int, c_void_p]),
 }
 
 _lib = None

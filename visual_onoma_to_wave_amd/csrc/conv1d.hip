@@ -45,6 +45,7 @@ struct ConvArgs {
   int pre_act; float pre_slope; int post_act; float post_slope; float out_scale;
   int transposed, up_stride, up_pad, up_cout, up_tout;
   int tiles_per_b, co_tiles, B;
+  int cig, cog;  // channels per group (in / out): grouped conv = block-diagonal packed weights
 };
 
 template <typename T> struct Raw8;  // 8 elements of T held in registers
@@ -183,7 +184,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
 // the barriers; guide T5) -- A/B via conv_cfg.  ABL (timing ablation, garbage results):
 // 1 = no global loads in the main loop.
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0>
+          int PRIO = 0, int ABL = 0, int S = 1>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -191,14 +192,14 @@ conv1d_kernel(ConvArgs a) {
   constexpr int BT = 16 * NJ * WT;
   constexpr int P = Lds<TC>::PITCH;
   constexpr int VPR = KC / 8;                 // 8-element vectors per row (4)
-  constexpr int MAXV = ((BT + HALO_MAX) * VPR + NT - 1) / NT;
+  constexpr int MAXV = (((BT - 1) * S + 1 + HALO_MAX) * VPR + NT - 1) / NT;
   constexpr int WV = (TPS * BCO * VPR + NT - 1) / NT;
   constexpr int SHW = ilog2(4 * NI);
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TC* smem = reinterpret_cast<TC*>(smem_raw);
 
-  const int win_rows = BT + (a.K - 1) * a.dil;
+  const int win_rows = (BT - 1) * S + 1 + (a.K - 1) * a.dil;  // S: conv stride
   TC* const win0 = smem;
   TC* const wt0 = smem + 2 * win_rows * P;
   const int win_stride = win_rows * P;      // elements between the two window buffers
@@ -217,7 +218,13 @@ conv1d_kernel(ConvArgs a) {
 
   const TIN* __restrict__ X = reinterpret_cast<const TIN*>(a.x) + (int64_t)b * a.xbs;
   const TC* __restrict__ Wp = reinterpret_cast<const TC*>(a.w);
-  const int n_chunks = (a.Ci + KC - 1) / KC;
+  // grouped conv: this block's output channels [co_blk, co_blk + BCO) read only input
+  // channels [ci_lo, ci_hi) of their groups (32-aligned; the packed weights are
+  // block-diagonal, so the extra channels of a partial chunk multiply zeros)
+  const int co_last = min(co_blk + BCO, a.Co) - 1;
+  const int ci_lo = (co_blk / a.cog) * a.cig / KC * KC;
+  const int ci_hi = min(a.Ci, (co_last / a.cog + 1) * a.cig);
+  const int n_chunks = (ci_hi - ci_lo + KC - 1) / KC;
   const int tsteps = (a.K + TPS - 1) / TPS;
   const int n_steps = n_chunks * tsteps;
   const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE;
@@ -235,7 +242,7 @@ conv1d_kernel(ConvArgs a) {
   for (int s = 0; s < MAXV; ++s) {
     const int v = tid + s * NT;
     const int r = v / VPR, q = v % VPR;
-    const int row = t0 - a.pad + r;
+    const int row = t0 * S - a.pad + r;
     xr[s] = r < win_rows && row >= 0 && row < a.T_in;  // row in range
     xc[s] = q * 8;
     xg[s] = min(max(row, 0), a.T_in - 1) * a.ldx + q * 8;
@@ -260,7 +267,7 @@ conv1d_kernel(ConvArgs a) {
   bool win_ok[MAXV], w_ok[WV];
 
   auto load_window = [&](int c) {
-    const int c0 = c * KC;
+    const int c0 = ci_lo + c * KC;
 #pragma unroll
     for (int s = 0; s < MAXV; ++s) {
       win_ok[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
@@ -290,7 +297,7 @@ conv1d_kernel(ConvArgs a) {
     }
   };
   auto load_w = [&](int c, int k0) {
-    const int c0 = c * KC;
+    const int c0 = ci_lo + c * KC;
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
       const int k = min(k0 + wk[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
@@ -346,10 +353,10 @@ conv1d_kernel(ConvArgs a) {
         Frag<TC> af[NI], bfr[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) af[i].load(wb + t * BCO * P + a_off[i]);
-        const int br = brow0 + (k0 + t) * a.dil;
+        const int br = brow0 * S + (k0 + t) * a.dil;
         const int boff = Lds<TC>::template off<2>(br, lq);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + 16 * j * P);
+        for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + 16 * S * j * P);  // +16S rows keeps the swizzle
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -384,8 +391,8 @@ conv1d_kernel(ConvArgs a) {
 
 // ------------------------------------------------------------------ host dispatch
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0>
-static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
+          int PRIO = 0, int ABL = 0, int S = 1>
+static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
   constexpr int TPS = sizeof(TC) == 2 ? TPS_BF16 : 1;
@@ -403,18 +410,52 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   a.tiles_per_b = (d->T_out + BT - 1) / BT;
   a.co_tiles = (d->Co + BCO - 1) / BCO;
   a.B = d->B;
-  const int win_rows = BT + (d->K - 1) * d->dil;
+  const int groups = d->groups > 1 ? d->groups : 1;
+  a.cig = d->Ci / groups;
+  a.cog = d->Co / groups;
+  const int win_rows = (BT - 1) * S + 1 + (d->K - 1) * d->dil;
   const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO + 1) * Lds<TC>::PITCH * sizeof(TC);
   if (lds > 160 * 1024) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
   const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL>
-                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL>;
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S>
+                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
   dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles);
   hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
   VO_RETURN_LAUNCH();
+}
+
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
+          int PRIO = 0, int ABL = 0>
+static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
+  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1>(d, st);
+}
+
+// HiFi-GAN discriminator layers (strided and/or grouped, C5): 64-row tiles so that a stride-4
+// window ((64 - 1) * 4 + 1 + 40 rows) still double-buffers in LDS; output-channel tiles no
+// wider than a group where groups are narrow (block-diagonal weights: a tile spanning g
+// groups reduces over g groups' input channels).
+template <typename TIN, typename TC, typename TOUT, int S>
+static int launch_disc_s(const vo_conv1d_desc* d, hipStream_t st) {
+  const int groups = d->groups > 1 ? d->groups : 1;
+  const int cog = d->Co / groups;
+  if constexpr (S >= 8) return launch_cfg_s<TIN, TC, TOUT, 4, 1, 2, 2, 2, 0, 0, 0, S>(d, st);  // 128 x 32
+  if (d->Co <= 32 || cog <= 32) return launch_cfg_s<TIN, TC, TOUT, 2, 1, 1, 4, 4, 0, 0, 0, S>(d, st);  // 32 x 64
+  if (d->Co <= 64 || cog <= 64) return launch_cfg_s<TIN, TC, TOUT, 4, 1, 1, 4, 4, 0, 0, 0, S>(d, st);  // 64 x 64
+  return launch_cfg_s<TIN, TC, TOUT, 4, 2, 2, 2, 2, 0, 0, 0, S>(d, st);                                 // 128 x 64
+}
+template <typename TIN, typename TC, typename TOUT>
+static int launch_disc(const vo_conv1d_desc* d, hipStream_t st) {
+  switch (d->stride > 1 ? d->stride : 1) {
+    case 1: return launch_disc_s<TIN, TC, TOUT, 1>(d, st);
+    case 2: return launch_disc_s<TIN, TC, TOUT, 2>(d, st);
+    case 3: return launch_disc_s<TIN, TC, TOUT, 3>(d, st);
+    case 4: return launch_disc_s<TIN, TC, TOUT, 4>(d, st);
+    case 8: return launch_disc_s<TIN, TC, TOUT, 8>(d, st);  // ConvTranspose1d(k 16, s 8) input gradient
+    default: vo_set_error("conv1d: stride %d unsupported (1..4, 8)", d->stride); return VO_ERR_INVALID;
+  }
 }
 
 template <typename TIN, typename TC, typename TOUT>
@@ -467,6 +508,19 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(const_cast<void*>(stream));
   const int xi = d->x_dtype, yo = d->y_dtype;
+  if (d->stride > 1 || d->groups > 1) {  // discriminator layers
+    const int g = d->groups > 1 ? d->groups : 1;
+    VO_CHECK_ARG(!d->transposed && d->variant == 0, "conv1d: stride/groups exclude transposed and variants");
+    VO_CHECK_ARG(d->Ci % g == 0 && d->Co % g == 0, "conv1d: Ci %d / Co %d not divisible by groups %d", d->Ci,
+                 d->Co, g);
+    if (d->compute_dtype == VO_F32) {
+      VO_CHECK_ARG(xi == VO_F32 && yo == VO_F32, "conv1d: fp32 compute needs fp32 I/O");
+      return launch_disc<float, float, float>(d, st);
+    }
+    VO_CHECK_ARG(d->compute_dtype == VO_BF16 && xi == VO_BF16, "conv1d: strided/grouped bf16 needs bf16 input");
+    if (yo == VO_BF16) return launch_disc<bf16_t, bf16_t, bf16_t>(d, st);
+    return launch_disc<bf16_t, bf16_t, float>(d, st);
+  }
   if (d->compute_dtype == VO_F32) {
     VO_CHECK_ARG(xi == VO_F32 && yo == VO_F32, "conv1d: fp32 compute needs fp32 I/O");
     return launch_types<float, float, float>(d, st);

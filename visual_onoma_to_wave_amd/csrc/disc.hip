@@ -1,0 +1,211 @@
+// HiFi-GAN training (config C5) glue around the discriminator convs: weight packing for
+// grouped convs, the MPD period fold, the MSD average pool, the (B, T) -> (B, T, 8)
+// channels-last input, and the GAN / feature-matching / L1 reductions with their gradients.
+//
+// The reference ships only the HiFi-GAN generator and its training hyper-parameters
+// (scripts/hifigan/models.py, scripts/hifigan/config.json:1-31); the discriminators and
+// losses follow the HiFi-GAN V1 recipe the config belongs to:
+//   MPD  : periods 2, 3, 5, 7, 11; wav reflect-padded to a multiple of p, viewed (T/p, p);
+//          Conv2d (k, 1) / (s, 1) = Conv1d along T/p per period column (conv1d stride);
+//   MSD  : raw wav, AvgPool1d(4, 2, padding 2) x1, x2; grouped strided Conv1d (conv1d groups);
+//   loss : D = sum mean((1 - D(y))^2) + mean(D(G(x))^2); G = sum mean((1 - D(G(x)))^2)
+//          + 2 * sum_layers mean|f(y) - f(G(x))| + 45 * L1(mel(y), mel(G(x))).
+
+#include <algorithm>
+
+#include "vo_common.h"
+
+namespace vo {
+
+// dense [K][Co][Ci_pad] from (Co, Ci / groups, K): block-diagonal, zero outside the groups and
+// past Ci (Ci_pad >= Ci rounds the 1-channel input layers up to the 8-channel minimum)
+template <typename TD>
+__global__ void __launch_bounds__(256) pack_grouped_kernel(const float* __restrict__ src, int Co, int Ci, int K,
+                                                           int groups, int Ci_pad, TD* __restrict__ dst) {
+  const int cig = Ci / groups, cog = Co / groups;
+  const int64_t n = (int64_t)K * Co * Ci_pad;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int ci = (int)(i % Ci_pad);
+    const int64_t r = i / Ci_pad;
+    const int co = (int)(r % Co), k = (int)(r / Co);
+    float v = 0.f;
+    if (ci < Ci && ci / cig == co / cog) v = src[((int64_t)co * cig + (ci - (co / cog) * cig)) * K + k];
+    dst[i] = from_f32<TD>(v);
+  }
+}
+
+// wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
+// reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
+template <typename TD>
+__global__ void __launch_bounds__(256) period_fold_kernel(const float* __restrict__ wav, int T, int P, int H,
+                                                          TD* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int64_t n = (int64_t)P * H;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i / H), h = (int)(i % H);
+    int t = h * P + c;
+    if (t >= T) t = 2 * (T - 1) - t;  // F.pad(..., "reflect") on the right
+    float v[8] = {wav[(int64_t)b * T + t], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    store8(out + (((int64_t)b * P + c) * H + h) * 8, v);
+  }
+}
+
+// (B, T) fp32 -> (B, T, 8) channels-last (channel 0)
+template <typename TD>
+__global__ void __launch_bounds__(256) wav_cl8_kernel(const float* __restrict__ wav, int64_t n, TD* __restrict__ out) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float v[8] = {wav[i], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    store8(out + i * 8, v);
+  }
+}
+
+// AvgPool1d(4, stride 2, padding 2, count_include_pad): y[o] = sum_{i<4} x[2o + i - 2] / 4
+__global__ void __launch_bounds__(256) avgpool_kernel(const float* __restrict__ x, int T, int T_out,
+                                                      float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const float* xb = x + (int64_t)b * T;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < T_out; o += gridDim.x * 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 2 * o + i - 2;
+      s += (t >= 0 && t < T) ? xb[t] : 0.f;
+    }
+    y[(int64_t)b * T_out + o] = 0.25f * s;
+  }
+}
+
+// reductions over a (rows x width) view with leading dimensions lda / ldb:
+//   0: sum |a - b|     1: sum (1 - a)^2     2: sum a^2
+template <typename TA>
+__global__ void __launch_bounds__(256) gan_reduce_kernel(int kind, const TA* __restrict__ a, int lda,
+                                                         const TA* __restrict__ b, int ldb, int64_t rows, int width,
+                                                         float* __restrict__ out) {
+  __shared__ float red[4];
+  const int64_t n = rows * width;
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / width;
+    const int c = (int)(i - r * width);
+    const float x = to_f32(a[r * lda + c]);
+    if (kind == 0) {
+      s += fabsf(x - to_f32(b[r * ldb + c]));
+    } else if (kind == 1) {
+      s += (1.f - x) * (1.f - x);
+    } else {
+      s += x * x;
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// gradient of scale * reduction wrt a (b held constant), written in a's layout
+template <typename TA>
+__global__ void __launch_bounds__(256) gan_reduce_grad_kernel(int kind, const TA* __restrict__ a, int lda,
+                                                              const TA* __restrict__ b, int ldb, int64_t rows,
+                                                              int width, const float* __restrict__ scale,
+                                                              TA* __restrict__ ga, int ldg) {
+  const int64_t n = rows * width;
+  const float s = *scale;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / width;
+    const int c = (int)(i - r * width);
+    const float x = to_f32(a[r * lda + c]);
+    float g;
+    if (kind == 0) {
+      const float d = x - to_f32(b[r * ldb + c]);
+      g = d > 0.f ? s : (d < 0.f ? -s : 0.f);
+    } else if (kind == 1) {
+      g = -2.f * (1.f - x) * s;
+    } else {
+      g = 2.f * x * s;
+    }
+    ga[r * ldg + c] = from_f32<TA>(g);
+  }
+}
+
+static int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 4096); }
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
+                               int dst_dtype, void* stream) {
+  VO_CHECK_ARG(src && dst, "pack_grouped: null pointer");
+  VO_CHECK_ARG(groups >= 1 && Co % groups == 0 && Ci % groups == 0 && Ci_pad >= Ci && K >= 1,
+               "pack_grouped: bad sizes Co=%d Ci=%d groups=%d Ci_pad=%d", Co, Ci, groups, Ci_pad);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int g = grid_for((int64_t)K * Co * Ci_pad);
+  if (dst_dtype == VO_BF16)
+    hipLaunchKernelGGL(pack_grouped_kernel<bf16_t>, dim3(g), dim3(256), 0, st, src, Co, Ci, K, groups, Ci_pad,
+                       (bf16_t*)dst);
+  else
+    hipLaunchKernelGGL(pack_grouped_kernel<float>, dim3(g), dim3(256), 0, st, src, Co, Ci, K, groups, Ci_pad,
+                       (float*)dst);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream) {
+  VO_CHECK_ARG(wav && out, "period_fold: null pointer");
+  VO_CHECK_ARG(B > 0 && P >= 1 && T > P, "period_fold: need T > P (B=%d T=%d P=%d)", B, T, P);
+  const int H = (T + P - 1) / P;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(grid_for((int64_t)P * H), B);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(period_fold_kernel<bf16_t>, grid, dim3(256), 0, st, wav, T, P, H, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(period_fold_kernel<float>, grid, dim3(256), 0, st, wav, T, P, H, (float*)out);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream) {
+  VO_CHECK_ARG(wav && out && n > 0, "wav_cl8: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(wav_cl8_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, wav, n, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(wav_cl8_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, wav, n, (float*)out);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream) {
+  VO_CHECK_ARG(x && y && B > 0 && T > 0, "avgpool_wav: bad arguments");
+  const int T_out = T / 2 + 1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(T_out), B), dim3(256), 0, st, x, T, T_out, y);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
+                             int dtype, float* out, void* stream) {
+  VO_CHECK_ARG(a && out && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce: bad arguments");
+  VO_CHECK_ARG(rows > 0 && width > 0 && lda >= width && (kind != 0 || ldb >= width), "gan_reduce: bad shape");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int g = grid_for(rows * width);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(gan_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
+                       (const bf16_t*)b, ldb, rows, width, out);
+  else
+    hipLaunchKernelGGL(gan_reduce_kernel<float>, dim3(g), dim3(256), 0, st, kind, (const float*)a, lda,
+                       (const float*)b, ldb, rows, width, out);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
+                                  int dtype, const float* scale, void* ga, int ldg, void* stream) {
+  VO_CHECK_ARG(a && ga && scale && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce_grad: bad arguments");
+  VO_CHECK_ARG(rows > 0 && width > 0 && lda >= width && ldg >= width, "gan_reduce_grad: bad shape");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int g = grid_for(rows * width);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(gan_reduce_grad_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
+                       (const bf16_t*)b, ldb, rows, width, scale, (bf16_t*)ga, ldg);
+  else
+    hipLaunchKernelGGL(gan_reduce_grad_kernel<float>, dim3(g), dim3(256), 0, st, kind, (const float*)a, lda,
+                       (const float*)b, ldb, rows, width, scale, (float*)ga, ldg);
+  VO_RETURN_LAUNCH();
+}

@@ -29,7 +29,8 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
                                                        const float* __restrict__ window,
                                                        const float* __restrict__ fb, int n_fft, int hop,
                                                        int n_mels, float log_floor, float* __restrict__ mel,
-                                                       float* __restrict__ energy) {
+                                                       float* __restrict__ energy, int pad, float mag_eps,
+                                                       int clip) {
   __shared__ float2 buf[2][STFT_MAX_N / 2];
   __shared__ float mag[STFT_MAX_N / 2 + 1];
   __shared__ float red[4];
@@ -37,13 +38,15 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
   const int tid = threadIdx.x;
   const int half = n_fft / 2;
   const float* x = wav + (int64_t)b * N;
-  const int start = f * hop - half;  // unpadded index of frame sample 0
+  const int start = f * hop - pad;  // unpadded index of frame sample 0
 
   // load + clip + window, packed even/odd into complex
   for (int m = tid; m < half; m += 256) {
     const int i0 = reflect(start + 2 * m, N), i1 = reflect(start + 2 * m + 1, N);
-    const float a = fminf(fmaxf(x[i0], -1.f), 1.f) * window[2 * m];
-    const float c = fminf(fmaxf(x[i1], -1.f), 1.f) * window[2 * m + 1];
+    const float x0 = clip ? fminf(fmaxf(x[i0], -1.f), 1.f) : x[i0];
+    const float x1 = clip ? fminf(fmaxf(x[i1], -1.f), 1.f) : x[i1];
+    const float a = x0 * window[2 * m];
+    const float c = x1 * window[2 * m + 1];
     buf[0][m] = make_float2(a, c);
   }
   __syncthreads();
@@ -79,7 +82,7 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
     sincospif(-2.f * (float)k / (float)n_fft, &s, &c);
     const float xr = er + (orr * c - oi * s);
     const float xi = ei + (orr * s + oi * c);
-    const float mg = sqrtf(xr * xr + xi * xi);
+    const float mg = sqrtf(xr * xr + xi * xi + mag_eps);
     mag[k] = mg;
     e2 += mg * mg;
   }
@@ -103,16 +106,24 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
 
 using namespace vo;
 
-extern "C" int vo_stft_mel(const float* wav, int B, int N, const float* window, const float* fb, int n_fft, int hop,
-                           int n_mels, float log_floor, float* mel, float* energy, void* stream) {
+extern "C" int vo_stft_mel_ex(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
+                              int hop, int n_mels, int pad, float mag_eps, int clip, float log_floor, float* mel,
+                              float* energy, void* stream) {
   VO_CHECK_ARG(wav && window && fb && mel, "stft_mel: null pointer");
   VO_CHECK_ARG(n_fft >= 8 && n_fft <= STFT_MAX_N && (n_fft & (n_fft - 1)) == 0, "stft_mel: n_fft=%d must be a power of "
                "two in [8, %d]", n_fft, STFT_MAX_N);
-  VO_CHECK_ARG(hop > 0 && n_mels > 0 && B > 0, "stft_mel: bad sizes");
-  VO_CHECK_ARG(N > n_fft / 2, "stft_mel: reflect padding needs N (%d) > n_fft/2", N);
-  const int F = 1 + N / hop;
+  VO_CHECK_ARG(hop > 0 && n_mels > 0 && B > 0 && pad >= 0, "stft_mel: bad sizes");
+  VO_CHECK_ARG(N > pad, "stft_mel: reflect padding needs N (%d) > pad (%d)", N, pad);
+  VO_CHECK_ARG(N + 2 * pad >= n_fft, "stft_mel: signal shorter than one frame");
+  const int F = 1 + (N + 2 * pad - n_fft) / hop;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(stft_mel_kernel, dim3((unsigned)F, (unsigned)B), dim3(256), 0, st, wav, N, F, window, fb, n_fft,
-                     hop, n_mels, log_floor, mel, energy);
+                     hop, n_mels, log_floor, mel, energy, pad, mag_eps, clip);
   VO_RETURN_LAUNCH();
+}
+
+// torchaudio center=True framing (pad n_fft / 2, F = 1 + N / hop), clipped input, |X|
+extern "C" int vo_stft_mel(const float* wav, int B, int N, const float* window, const float* fb, int n_fft, int hop,
+                           int n_mels, float log_floor, float* mel, float* energy, void* stream) {
+  return vo_stft_mel_ex(wav, B, N, window, fb, n_fft, hop, n_mels, n_fft / 2, 0.f, 1, log_floor, mel, energy, stream);
 }

@@ -7,3 +7,15 @@ class AttrDict(dict):
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
         self.__dict__ = self
+
+
+def __getattr__(name):
+    # training-side modules (config C5) load on first use
+    if name in ("MultiPeriodDiscriminator", "MultiScaleDiscriminator", "DiscriminatorP", "DiscriminatorS",
+                "feature_loss", "discriminator_loss", "generator_loss", "MelLoss"):
+        from . import discriminators
+        return getattr(discriminators, name)
+    if name == "HifiGanTrainer":
+        from .train import HifiGanTrainer
+        return HifiGanTrainer
+    raise AttributeError(name)

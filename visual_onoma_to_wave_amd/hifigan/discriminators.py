@@ -1,0 +1,226 @@
+"""HiFi-GAN V1 discriminators and losses on HIP kernels (config C5).
+
+The reference ships the generator and the training hyper-parameters only
+(scripts/hifigan/models.py, scripts/hifigan/config.json); these modules follow the HiFi-GAN
+V1 recipe that config belongs to, with its module / parameter names (``mpd.discriminators.N.
+convs.M.weight_g`` ...), so an upstream HiFi-GAN ``do_*`` discriminator checkpoint loads:
+
+* DiscriminatorP(period): wav reflect-padded to a multiple of p and viewed (T/p, p); five
+  Conv2d (5, 1) / (3, 1) (1 -> 32 -> 128 -> 512 -> 1024, last one stride 1) + leaky ReLU 0.1,
+  conv_post Conv2d (3, 1) -> 1.  Here: each period column is a sequence of a channels-last
+  (B * p, T/p, C) batch and each Conv2d (k, 1) is one strided ``vo_conv1d`` launch.
+* DiscriminatorS: Conv1d 1 -> 128 (15), grouped strided Conv1d (41, groups 4 / 16, strides
+  2, 2, 4, 4, 1), Conv1d (5), conv_post (3); the first of the three scales spectral-normed.
+  Grouped convs run as ``vo_conv1d`` groups mode over block-diagonal packed weights.
+* MultiScaleDiscriminator: raw wav, AvgPool1d(4, 2, padding 2) once and twice.
+* Losses: feature_loss = 2 * sum mean|f_r - f_g|; discriminator_loss = sum mean((1 - D(y))^2)
+  + mean(D(G(x))^2); generator_loss = sum mean((1 - D(G(x)))^2) (fp32 ``vo_gan_reduce``).
+
+Activations are bf16 (``compute_dtype`` float32 = exact-f32 parity mode).  Scores and
+feature maps come back in this layout: MPD (B * p, H, C), MSD (B, T, C); the losses are
+means, independent of it.
+"""
+
+import warnings
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.nn import Conv1d, Conv2d
+
+from . import gan_ops as G
+
+LRELU_SLOPE = 0.1
+
+with warnings.catch_warnings():
+    warnings.simplefilter("ignore")
+    from torch.nn.utils import spectral_norm, weight_norm
+    from torch.nn.utils.spectral_norm import SpectralNorm
+
+
+def get_padding(kernel_size, dilation=1):
+    return int((kernel_size * dilation - dilation) / 2)
+
+
+def effective_weight(m):
+    """The weight a weight-normed / spectral-normed conv would use in this forward (torch
+    parameterisation math: w = g v / ||v||, or the power-iteration sigma in training mode)."""
+    if hasattr(m, "weight_g"):
+        return torch._weight_norm(m.weight_v, m.weight_g, 0)
+    for hook in m._forward_pre_hooks.values():
+        if isinstance(hook, SpectralNorm):
+            hook(m, None)
+            return m.weight
+    return m.weight
+
+
+class _DiscBase(nn.Module):
+    compute_dtype = torch.bfloat16
+
+    def set_compute_dtype(self, dt):
+        for m in self.modules():
+            if isinstance(m, _DiscBase):
+                m.compute_dtype = dt
+        return self
+
+    def _act_dtype(self):
+        return torch.float32 if self.compute_dtype == torch.float32 else torch.bfloat16
+
+
+class DiscriminatorP(_DiscBase):
+    def __init__(self, period, kernel_size=5, stride=3, use_spectral_norm=False):
+        super().__init__()
+        self.period, self.kernel_size, self.stride = period, kernel_size, stride
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        pad = (get_padding(5, 1), 0)
+        chans = [1, 32, 128, 512, 1024]
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            self.convs = nn.ModuleList(
+                [norm_f(Conv2d(chans[i], chans[i + 1], (kernel_size, 1), (stride, 1), padding=pad)) for i in range(4)]
+                + [norm_f(Conv2d(1024, 1024, (kernel_size, 1), 1, padding=(2, 0)))])
+            self.conv_post = norm_f(Conv2d(1024, 1, (3, 1), 1, padding=(1, 0)))
+
+    def _specs(self):
+        k, s = self.kernel_size, self.stride
+        specs = [G.ConvSpec(K=k, pad=get_padding(5, 1), stride=s, post="lrelu", post_slope=LRELU_SLOPE,
+                            ci_pad=8 if i == 0 else None) for i in range(4)]
+        specs.append(G.ConvSpec(K=k, pad=2, post="lrelu", post_slope=LRELU_SLOPE))
+        return specs, G.ConvSpec(K=3, pad=1, co_pad=4)
+
+    def forward(self, wav):
+        """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)])."""
+        cdt, adt = self.compute_dtype, self._act_dtype()
+        x = G.PeriodFoldFn.apply(wav, self.period, adt)
+        specs, post = self._specs()
+        fmap = []
+        for m, sp in zip(self.convs, specs):
+            x = G.conv(x, effective_weight(m)[..., 0], m.bias, sp, cdt)
+            fmap.append(x)
+        m = self.conv_post
+        y = G.conv(x, effective_weight(m)[..., 0], m.bias, post, cdt)
+        score = y[..., 0].contiguous()
+        fmap.append(score)
+        return score, fmap
+
+
+class MultiPeriodDiscriminator(_DiscBase):
+    def __init__(self, periods=(2, 3, 5, 7, 11)):
+        super().__init__()
+        self.discriminators = nn.ModuleList(DiscriminatorP(p) for p in periods)
+
+    def forward(self, y, y_hat):
+        """Reference call convention: (y_d_rs, y_d_gs, fmap_rs, fmap_gs).  y and y_hat run as one
+        batch (one launch per layer for both)."""
+        B = y.shape[0]
+        both = torch.cat([y, y_hat], 0)
+        rs, gs, frs, fgs = [], [], [], []
+        for d in self.discriminators:
+            p = d.period
+            s, fm = d(both)
+            rs.append(s[: B * p])
+            gs.append(s[B * p:])
+            frs.append([f[: B * p] for f in fm])
+            fgs.append([f[B * p:] for f in fm])
+        return rs, gs, frs, fgs
+
+
+class DiscriminatorS(_DiscBase):
+    def __init__(self, use_spectral_norm=False):
+        super().__init__()
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        cfg = [(1, 128, 15, 1, 1, 7), (128, 128, 41, 2, 4, 20), (128, 256, 41, 2, 16, 20), (256, 512, 41, 4, 16, 20),
+               (512, 1024, 41, 4, 16, 20), (1024, 1024, 41, 1, 16, 20), (1024, 1024, 5, 1, 1, 2)]
+        self.cfg = cfg
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            self.convs = nn.ModuleList(norm_f(Conv1d(ci, co, k, s, groups=g, padding=p)) for ci, co, k, s, g, p in cfg)
+            self.conv_post = norm_f(Conv1d(1024, 1, 3, 1, padding=1))
+
+    def forward(self, wav):
+        """wav (B, T) fp32 -> (score (B, T'), fmaps [(B, T_l, C_l)])."""
+        cdt, adt = self.compute_dtype, self._act_dtype()
+        x = G.WavCl8Fn.apply(wav, adt)
+        fmap = []
+        for m, (ci, co, k, s, g, p) in zip(self.convs, self.cfg):
+            sp = G.ConvSpec(K=k, pad=p, stride=s, groups=g, post="lrelu", post_slope=LRELU_SLOPE,
+                            ci_pad=8 if ci == 1 else None)
+            x = G.conv(x, effective_weight(m), m.bias, sp, cdt)
+            fmap.append(x)
+        m = self.conv_post
+        y = G.conv(x, effective_weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt)
+        score = y[..., 0].contiguous()
+        fmap.append(score)
+        return score, fmap
+
+
+class MultiScaleDiscriminator(_DiscBase):
+    def __init__(self):
+        super().__init__()
+        self.discriminators = nn.ModuleList(
+            [DiscriminatorS(use_spectral_norm=True), DiscriminatorS(), DiscriminatorS()])
+
+    def forward(self, y, y_hat):
+        B = y.shape[0]
+        x = torch.cat([y, y_hat], 0)
+        rs, gs, frs, fgs = [], [], [], []
+        for i, d in enumerate(self.discriminators):
+            if i != 0:
+                x = G.AvgPoolFn.apply(x)
+            s, fm = d(x)
+            rs.append(s[:B])
+            gs.append(s[B:])
+            frs.append([f[:B] for f in fm])
+            fgs.append([f[B:] for f in fm])
+        return rs, gs, frs, fgs
+
+
+def feature_loss(fmap_r, fmap_g):
+    loss = 0
+    for dr, dg in zip(fmap_r, fmap_g):
+        for rl, gl in zip(dr, dg):
+            loss = loss + G.l1_mean(gl, rl)
+    return loss * 2
+
+
+def discriminator_loss(disc_real_outputs, disc_generated_outputs):
+    loss = 0
+    r_losses, g_losses = [], []
+    for dr, dg in zip(disc_real_outputs, disc_generated_outputs):
+        r_loss = G.one_minus_sq_mean(dr)
+        g_loss = G.sq_mean(dg)
+        loss = loss + (r_loss + g_loss)
+        r_losses.append(r_loss)
+        g_losses.append(g_loss)
+    return loss, r_losses, g_losses
+
+
+def generator_loss(disc_outputs):
+    loss = 0
+    gen_losses = []
+    for dg in disc_outputs:
+        l_ = G.one_minus_sq_mean(dg)
+        gen_losses.append(l_)
+        loss = loss + l_
+    return loss, gen_losses
+
+
+class MelLoss(nn.Module):
+    """HiFi-GAN training mel (meldataset.mel_spectrogram with fmax_for_loss) on vo_stft_mel_ex."""
+
+    def __init__(self, n_fft=1024, num_mels=80, sampling_rate=22050, hop_size=256, win_size=1024, fmin=0,
+                 fmax=None):
+        super().__init__()
+        from ..audio import librosa_mel
+        if win_size != n_fft:
+            raise NotImplementedError("win_size != n_fft")
+        self.n_fft, self.hop = n_fft, hop_size
+        fb = librosa_mel(sampling_rate, n_fft, num_mels, fmin, fmax)  # (n_mels, n_fft/2 + 1)
+        self.register_buffer("fb", torch.from_numpy(fb).t().contiguous(), persistent=False)
+        self.register_buffer("window", torch.hann_window(win_size), persistent=False)
+
+    def mel(self, wav):
+        return G.MelFn.apply(wav, self.window, self.fb, self.n_fft, self.hop)
+
+    def forward(self, wav_hat, mel_target):
+        return G.l1_mean(self.mel(wav_hat), mel_target)

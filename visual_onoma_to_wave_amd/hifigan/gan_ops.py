@@ -1,0 +1,283 @@
+"""Autograd ops of the HiFi-GAN training path (config C5).
+
+Every forward is a HIP kernel of libvonoma.so on channels-last (B, T, C) activations:
+``vo_conv1d`` (dense, strided, grouped, polyphase-transposed; pre / post activation,
+residual, MRF accumulate fused), ``vo_period_fold`` / ``vo_wav_cl8`` / ``vo_avgpool_wav``
+(discriminator inputs), ``vo_gan_reduce`` (losses) and ``vo_stft_mel_ex`` (mel loss).
+
+Backward, per op:
+  * input gradient of a stride-1 dense conv: the conv kernel over dY with the weights
+    re-packed taps-reversed / channels-swapped (as in C4); of a polyphase ConvTranspose1d:
+    the strided conv kernel (dX = conv1d(dY, W, stride s, pad p));
+  * loss gradients: ``vo_gan_reduce_grad``;
+  * weight / bias gradients, the input gradient of strided / grouped discriminator convs and
+    the mel-loss STFT: PyTorch-ROCm (MIOpen ``convolution_backward``, ``torch.stft``) -- the
+    fallback SURVEY.md 8(b) sanctions for training backward.
+"""
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass(frozen=True)
+class ConvSpec:
+    K: int
+    pad: int
+    dil: int = 1
+    stride: int = 1
+    groups: int = 1
+    pre_slope: Optional[float] = None       # leaky-ReLU applied to the input while staging
+    post: Optional[str] = None              # None | "lrelu" | "tanh" (not combined with residuals)
+    post_slope: float = 0.1
+    out_scale: float = 1.0
+    transposed: Optional[Tuple[int, int]] = None  # (stride, pad) of a ConvTranspose1d (K = 2 stride)
+    ci_pad: Optional[int] = None            # input channels padded with zeros (1-channel inputs -> 8)
+    co_pad: Optional[int] = None            # output channels padded with zero rows (Co = 1 -> 4)
+
+    def plain(self):
+        return (self.stride == 1 and self.groups == 1 and self.transposed is None and self.ci_pad is None
+                and self.co_pad is None)
+
+
+_POST = {None: ops.ACT_NONE, "lrelu": ops.ACT_LRELU, "tanh": ops.ACT_TANH}
+
+
+def _pack(w, spec, dtype):
+    if spec.transposed is not None:
+        return ops.pack_conv_weight(w, dtype, transposed_stride=spec.transposed[0])
+    if spec.plain():
+        return ops.pack_conv_weight(w, dtype)
+    if spec.co_pad is not None and spec.co_pad > w.shape[0]:
+        w = torch.cat([w.detach(), w.new_zeros((spec.co_pad - w.shape[0],) + tuple(w.shape[1:]))])
+    return ops.pack_grouped_weight(w, dtype, spec.groups, spec.ci_pad)
+
+
+def _bias(b, spec, n):
+    b = b.detach().float()
+    if b.numel() < n:
+        b = torch.cat([b, b.new_zeros(n - b.numel())])
+    return b.contiguous()
+
+
+def out_len(spec, T_in):
+    if spec.transposed is not None:
+        s, p = spec.transposed
+        return (T_in - 1) * s - 2 * p + spec.K
+    return (T_in + 2 * spec.pad - spec.dil * (spec.K - 1) - 1) // spec.stride + 1
+
+
+def _conv_fwd(x, w, b, res1, res2, spec, cdt):
+    wp = _pack(w, spec, cdt)
+    if spec.transposed is not None:
+        s, p = spec.transposed
+        cout = w.shape[1]
+        return ops.conv1d(x, wp, _bias(b, spec, cout), Co=s * cout, K=2, pad=1,
+                          pre_act=ops.ACT_LRELU if spec.pre_slope is not None else ops.ACT_NONE,
+                          pre_slope=spec.pre_slope or 0.0, transposed=dict(stride=s, pad=p, cout=cout),
+                          res1=res1, res2=res2, out_scale=spec.out_scale, out_dtype=x.dtype, compute_dtype=cdt)
+    Co = wp.shape[1]
+    return ops.conv1d(x, wp, _bias(b, spec, Co), Co=Co, K=spec.K, dil=spec.dil, pad=spec.pad,
+                      T_out=out_len(spec, x.shape[1]),
+                      pre_act=ops.ACT_LRELU if spec.pre_slope is not None else ops.ACT_NONE,
+                      pre_slope=spec.pre_slope or 0.0, post_act=_POST[spec.post], post_slope=spec.post_slope,
+                      res1=res1, res2=res2, out_scale=spec.out_scale, out_dtype=x.dtype, compute_dtype=cdt,
+                      stride=spec.stride, groups=spec.groups)
+
+
+def _ncw(t):
+    return t.transpose(1, 2).float().contiguous()
+
+
+class ConvFn(torch.autograd.Function):
+    """y = (post(conv(pre(x), w) + b) + res1) * out_scale + res2, channels-last."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res1, res2, spec, cdt):
+        if spec.post is not None and (res1 is not None or res2 is not None):
+            raise ValueError("ConvFn: post-activation with residual inputs is not differentiable here")
+        y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt)
+        ctx.spec, ctx.cdt = spec, cdt
+        ctx.has = (res1 is not None, res2 is not None)
+        ctx.save_for_backward(x, w, y if spec.post is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        spec, cdt = ctx.spec, ctx.cdt
+        gy = gy.contiguous()
+        g_res2 = gy if ctx.has[1] and ctx.needs_input_grad[4] else None
+        gz = gy * spec.out_scale if spec.out_scale != 1.0 else gy
+        g_res1 = gz if ctx.has[0] and ctx.needs_input_grad[3] else None
+        if spec.post == "lrelu":
+            gz = gz * torch.where(y > 0, 1.0, spec.post_slope).to(gz.dtype)
+        elif spec.post == "tanh":
+            yf = y.float()
+            gz = (gz.float() * (1.0 - yf * yf)).to(gz.dtype)
+        if spec.co_pad is not None:
+            gz = gz[..., : w.shape[0]].contiguous()
+        ci = w.shape[0] if spec.transposed is not None else w.shape[1] * spec.groups
+        xin = x[..., :ci] if x.shape[-1] != ci else x
+        a = xin if spec.pre_slope is None else torch.where(xin > 0, xin, xin * spec.pre_slope)
+        gx = gw = gb = None
+        need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        if need_x and spec.plain():
+            wd = ops.pack_dgrad_weight(w, cdt)
+            ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
+                            pad=(spec.K - 1) * spec.dil - spec.pad, T_out=x.shape[1], out_dtype=x.dtype,
+                            compute_dtype=cdt)
+            need_x = False
+        elif need_x and spec.transposed is not None:
+            s, p = spec.transposed
+            # ConvTranspose1d(Ci -> Co, k, s, p) adjoint = Conv1d(Co -> Ci, W as (Ci, Co, k), stride s, pad p)
+            wc = ops.pack_conv_weight(w, cdt)
+            ga = ops.conv1d(gz.to(cdt), wc, None, Co=w.shape[0], K=spec.K, pad=p, stride=s, T_out=x.shape[1],
+                            out_dtype=x.dtype, compute_dtype=cdt)
+            need_x = False
+        else:
+            ga = None
+        if need_x or need_w or need_b:
+            if spec.transposed is not None:
+                s, p = spec.transposed
+                stride, pad, tr = [s], [p], True
+            else:
+                stride, pad, tr = [spec.stride], [spec.pad], False
+            gi, gw, gb = torch.ops.aten.convolution_backward(
+                _ncw(gz), _ncw(a), w.float(), [w.shape[1] if tr else w.shape[0]], stride, pad, [spec.dil], tr, [0],
+                spec.groups, [need_x, need_w, need_b])
+            if need_x:
+                ga = gi.transpose(1, 2).to(x.dtype)
+            if gw is not None:
+                gw = gw.to(w.dtype)
+            if gb is not None and spec.co_pad is not None:
+                gb = gb[: w.shape[0]]
+        if ga is not None:
+            if spec.pre_slope is not None:
+                ga = ga * torch.where(xin > 0, 1.0, spec.pre_slope).to(ga.dtype)
+            if ga.shape[-1] != x.shape[-1]:
+                ga = F.pad(ga, (0, x.shape[-1] - ga.shape[-1]))
+            gx = ga
+        if not ctx.needs_input_grad[1]:
+            gw = None
+        if not ctx.needs_input_grad[2]:
+            gb = None
+        return gx, gw, gb, g_res1, g_res2, None, None
+
+
+def conv(x, w, b, spec, cdt, res1=None, res2=None):
+    return ConvFn.apply(x, w, b, res1, res2, spec, cdt)
+
+
+class PeriodFoldFn(torch.autograd.Function):
+    """wav (B, T) fp32 -> (B * p, ceil(T / p), 8): reflect pad to a multiple of p, (T/p, p) view."""
+
+    @staticmethod
+    def forward(ctx, wav, period, dtype):
+        ctx.shape, ctx.period = wav.shape, period
+        return ops.period_fold(wav.contiguous(), period, dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, T = ctx.shape
+        p = ctx.period
+        H = g.shape[1]
+        gf = g[..., 0].float().reshape(B, p, H).transpose(1, 2).reshape(B, H * p)  # padded time order
+        gw = gf[:, :T].clone()
+        n_pad = H * p - T
+        if n_pad:  # reflect: padded sample T + i came from T - 2 - i
+            src = torch.arange(T - 2, T - 2 - n_pad, -1, device=g.device)
+            gw.index_add_(1, src, gf[:, T:])
+        return gw, None, None
+
+
+class WavCl8Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, wav, dtype):
+        return ops.wav_cl8(wav.contiguous(), dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[..., 0].float().contiguous(), None
+
+
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, wav):
+        ctx.T = wav.shape[1]
+        return ops.avgpool_wav(wav.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        # adjoint of AvgPool1d(4, 2, padding 2, count_include_pad): each output spreads g / 4
+        T = ctx.T
+        gx = F.conv_transpose1d(g[:, None, :], g.new_full((1, 1, 4), 0.25), stride=2, padding=2)
+        gx = gx[:, 0, :T]
+        if gx.shape[1] < T:
+            gx = F.pad(gx, (0, T - gx.shape[1]))
+        return gx.contiguous()
+
+
+class GanLossFn(torch.autograd.Function):
+    """scale * sum over a of |a - b| / (1 - a)^2 / a^2 (b held constant)."""
+
+    @staticmethod
+    def forward(ctx, a, b, kind, scale):
+        s = ops.gan_reduce(kind, a, b)
+        ctx.kind, ctx.scale = kind, scale
+        ctx.save_for_backward(a, b)
+        return s * scale
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        ga = ops.gan_reduce_grad(ctx.kind, a, b, (g.float() * ctx.scale).reshape(()))
+        return ga, None, None, None
+
+
+def l1_mean(a, b):
+    return GanLossFn.apply(a, b.detach(), ops.GAN_L1, 1.0 / a.numel())
+
+
+def one_minus_sq_mean(a):
+    return GanLossFn.apply(a, None, ops.GAN_ONE_MINUS_SQ, 1.0 / a.numel())
+
+
+def sq_mean(a):
+    return GanLossFn.apply(a, None, ops.GAN_SQ, 1.0 / a.numel())
+
+
+class MelFn(torch.autograd.Function):
+    """HiFi-GAN training log-mel of wav (B, N) (meldataset.mel_spectrogram semantics: reflect pad
+    (n_fft - hop) / 2, center=False, periodic Hann, sqrt(|X|^2 + 1e-9), slaney mel, log clamp 1e-5)."""
+
+    @staticmethod
+    def forward(ctx, wav, window, fb, n_fft, hop):
+        ctx.save_for_backward(wav, window, fb)
+        ctx.cfg = (n_fft, hop)
+        return ops.stft_mel_ex(wav.contiguous(), window, fb, n_fft=n_fft, hop=hop, n_mels=fb.shape[1],
+                               pad=(n_fft - hop) // 2, mag_eps=1e-9, clip=False)
+
+    @staticmethod
+    def backward(ctx, g):
+        wav, window, fb = ctx.saved_tensors
+        n_fft, hop = ctx.cfg
+        with torch.enable_grad():
+            w = wav.detach().requires_grad_(True)
+            mel = mel_reference(w, window, fb, n_fft, hop)
+            (gw,) = torch.autograd.grad(mel, w, g)
+        return gw, None, None, None, None
+
+
+def mel_reference(wav, window, fb, n_fft, hop):
+    """torch restatement used only for MelFn's backward (recomputation)."""
+    p = (n_fft - hop) // 2
+    y = F.pad(wav[:, None, :], (p, p), mode="reflect")[:, 0]
+    spec = torch.stft(y, n_fft, hop_length=hop, win_length=n_fft, window=window, center=False,
+                      return_complex=True)
+    mag = torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-9)
+    return torch.log(torch.clamp(torch.matmul(fb.t(), mag), min=1e-5))

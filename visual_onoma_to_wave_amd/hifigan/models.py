@@ -166,6 +166,42 @@ class Generator(HipModule):
         wk, bp = p["post"]
         return ops.conv_post(x, wk, bp, slope=0.01)
 
+    def train_forward(self, mel_cl):
+        """Differentiable forward for HiFi-GAN training (config C5): mel_cl (B, T, 80)
+        channels-last -> wav (B, 256 T) fp32.  Same HIP conv kernels as ``run`` (pre-lrelu while
+        staging, residual and MRF sum in the epilogue), one launch per conv (the fused pair
+        kernel has no backward), gradients through ``gan_ops.ConvFn``; the weight-norm
+        reparameterisation w = g v / ||v|| is differentiated by torch."""
+        from . import gan_ops as G
+        dt = self.compute_dtype
+        adt = torch.float32 if dt == torch.float32 else torch.bfloat16
+
+        def wgt(m):
+            return torch._weight_norm(m.weight_v, m.weight_g, 0) if hasattr(m, "weight_g") else m.weight
+
+        x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, G.ConvSpec(K=7, pad=3), dt)
+        for i, (u, k) in enumerate(zip(self.h.upsample_rates, self.h.upsample_kernel_sizes)):
+            m = self.ups[i]
+            x = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=k, pad=(k - u) // 2, pre_slope=LRELU_SLOPE,
+                                                     transposed=(u, (k - u) // 2)), dt)
+            xs = None
+            for j in range(self.num_kernels):
+                rb = self.resblocks[i * self.num_kernels + j]
+                kk = rb.kernel_size
+                cur = x
+                for n, (d, c1, c2) in enumerate(zip(rb.dilation, rb.convs1, rb.convs2)):
+                    t = G.conv(cur, wgt(c1), c1.bias, G.ConvSpec(K=kk, pad=get_padding(kk, d), dil=d,
+                                                                 pre_slope=LRELU_SLOPE, post="lrelu",
+                                                                 post_slope=LRELU_SLOPE), dt)
+                    last = n == len(rb.dilation) - 1
+                    sp = G.ConvSpec(K=kk, pad=get_padding(kk, 1), out_scale=1.0 / self.num_kernels if last else 1.0)
+                    cur = G.conv(t, wgt(c2), c2.bias, sp, dt, res1=cur, res2=xs if last else None)
+                xs = cur
+            x = xs
+        m = self.conv_post
+        y = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=7, pad=3, pre_slope=0.01, post="tanh", co_pad=4), dt)
+        return y[..., 0].float()
+
     def forward(self, x):
         """x (B, 80, T) mel -> (B, 1, 256 * T) waveform (reference: models.py:149-165)."""
         self._check_inference()

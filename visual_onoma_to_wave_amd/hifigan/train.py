@@ -1,0 +1,121 @@
+"""HiFi-GAN V1 training step (config C5) with data parallelism.
+
+Hyper-parameters come from the reference's scripts/hifigan/config.json (batch 16 per GPU,
+segment 8192, AdamW lr 2e-4, betas (0.8, 0.99), per-epoch ExponentialLR 0.999, fmax_for_loss
+null); the step follows the HiFi-GAN V1 recipe that config belongs to:
+
+  D step: L_D = sum_{MPD, MSD} [mean((1 - D(y))^2) + mean(D(G(x).detach())^2)]
+  G step: L_G = sum adv mean((1 - D(G(x)))^2) + 2 sum_l mean|D_l(y) - D_l(G(x))| + 45 L1(mel)
+
+Multi-GPU: one process per GPU; generator and discriminator gradients are averaged by two
+bucketed RCCL all-reduces (``train.GradBucketer``) launched from backward hooks, so each
+overlaps the rest of its backward.  In the G step the discriminators are frozen (their
+gradients would be discarded by the next D step's zero_grad) and run on the real batch
+under no_grad: one backward through D on the generated half only.
+"""
+
+import itertools
+
+import torch
+
+from ..train import GradBucketer
+from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiScaleDiscriminator, discriminator_loss,
+                             feature_loss, generator_loss)
+
+
+def _single(disc, wav, grad):
+    """(scores, fmaps) of a Multi*Discriminator on one batch."""
+    scores, fmaps = [], []
+    ctx = torch.enable_grad() if grad else torch.no_grad()
+    with ctx:
+        x = wav
+        for i, d in enumerate(disc.discriminators):
+            if isinstance(disc, MultiScaleDiscriminator) and i:
+                from . import gan_ops
+                x = gan_ops.AvgPoolFn.apply(x)
+            s, f = d(x)
+            scores.append(s)
+            fmaps.append(f)
+    return scores, fmaps
+
+
+class HifiGanTrainer:
+    def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None):
+        self.generator = generator
+        device = device or next(generator.parameters()).device
+        self.mpd = (mpd or MultiPeriodDiscriminator()).to(device)
+        self.msd = (msd or MultiScaleDiscriminator()).to(device)
+        self.h = h
+        self.optim_g = torch.optim.AdamW(generator.parameters(), h.learning_rate, betas=[h.adam_b1, h.adam_b2])
+        self.optim_d = torch.optim.AdamW(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
+                                         h.learning_rate, betas=[h.adam_b1, h.adam_b2])
+        self.sched_g = torch.optim.lr_scheduler.ExponentialLR(self.optim_g, gamma=h.lr_decay)
+        self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
+        self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,
+                                h.fmax_for_loss).to(device)
+        self.bk_g = self.bk_d = None
+        if distributed:
+            self.bk_g = GradBucketer(list(generator.parameters()))
+            self.bk_d = GradBucketer(list(self.msd.parameters()) + list(self.mpd.parameters()))
+            self.bk_g.broadcast_parameters(generator)
+            self.bk_d.broadcast_parameters(self.mpd)
+            self.bk_d.broadcast_parameters(self.msd)
+
+    def set_compute_dtype(self, dt):
+        self.generator.set_compute_dtype(dt)
+        self.mpd.set_compute_dtype(dt)
+        self.msd.set_compute_dtype(dt)
+        return self
+
+    def _d_params(self):
+        return itertools.chain(self.mpd.parameters(), self.msd.parameters())
+
+    def step(self, x_mel_cl, y):
+        """x_mel_cl (B, frames, 80) generator input mel (channels-last), y (B, 256 frames) fp32
+        target segment -> dict of fp32 loss tensors (device scalars, no host sync)."""
+        self.generator.train()
+        self.mpd.train()
+        self.msd.train()
+        y_g_hat = self.generator.train_forward(x_mel_cl)
+        with torch.no_grad():
+            y_mel = self.mel_loss.mel(y)
+
+        # discriminators: real and generated halves as one batch per layer
+        for p in self._d_params():
+            p.requires_grad_(True)
+        self.optim_d.zero_grad(set_to_none=True)
+        yd = y_g_hat.detach()
+        r, g, _, _ = self.mpd(y, yd)
+        loss_disc_f, _, _ = discriminator_loss(r, g)
+        r, g, _, _ = self.msd(y, yd)
+        loss_disc_s, _, _ = discriminator_loss(r, g)
+        loss_disc_all = loss_disc_s + loss_disc_f
+        loss_disc_all.backward()
+        if self.bk_d is not None:
+            self.bk_d.finish()
+        self.optim_d.step()
+
+        # generator: D frozen, real features without graph
+        for p in self._d_params():
+            p.requires_grad_(False)
+        self.optim_g.zero_grad(set_to_none=True)
+        loss_mel = self.mel_loss(y_g_hat, y_mel) * 45
+        _, fr_f = _single(self.mpd, y, False)
+        _, fr_s = _single(self.msd, y, False)
+        g_f, fg_f = _single(self.mpd, y_g_hat, True)
+        g_s, fg_s = _single(self.msd, y_g_hat, True)
+        loss_fm = feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
+        loss_adv = generator_loss(g_f)[0] + generator_loss(g_s)[0]
+        loss_gen_all = loss_adv + loss_fm + loss_mel
+        loss_gen_all.backward()
+        if self.bk_g is not None:
+            self.bk_g.finish()
+        self.optim_g.step()
+        for p in self._d_params():
+            p.requires_grad_(True)
+        return dict(disc=loss_disc_all.detach(), gen=loss_gen_all.detach(), mel=loss_mel.detach(),
+                    fm=loss_fm.detach(), adv=loss_adv.detach())
+
+    def end_epoch(self):
+        self.sched_g.step()
+        self.sched_d.step()

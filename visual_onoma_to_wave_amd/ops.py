@@ -45,12 +45,14 @@ def _contig(t, name):
 def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_dtype=None,
            pre_act=ACT_NONE, pre_slope=0.0, post_act=ACT_NONE, post_slope=0.0, res1=None,
            res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None, variant=0,
-           tag=None):
+           tag=None, stride=1, groups=1):
     """Channels-last conv: x (B, T_in, Ci) -> y (B, T_out, Co).
 
     ``w_packed``: [K][Co][Ci] in ``compute_dtype`` (see pack_conv_weight).
     ``transposed``: None or dict(stride=s, pad=p, cout=C_out) for the polyphase
     ConvTranspose1d; then Co = s*C_out, K = 2, pad = 1 and y is (B, s*T_in, C_out).
+    ``stride`` / ``groups``: strided and grouped convs (HiFi-GAN discriminators); grouped
+    weights are packed dense with zeros outside the diagonal blocks (pack_conv_weight groups=).
     """
     if x.dim() == 2:
         x = x.unsqueeze(0)
@@ -70,7 +72,7 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
         shape = (B, up_tout, cout)
         ldy = cout
     else:
-        T_rows = T_out if T_out is not None else T_in + 2 * pad - dil * (K - 1)
+        T_rows = T_out if T_out is not None else (T_in + 2 * pad - dil * (K - 1) - 1) // stride + 1
         shape = (B, T_rows, Co)
         ldy = Co
     if out is None:
@@ -96,12 +98,13 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     if transposed is not None:
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
     d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
+    d.stride, d.groups = stride, groups
     timer = profiling.active()
     ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
     _lib.check(_lib.lib().vo_conv1d(ctypes.byref(d), _stream(x)), "vo_conv1d")
     if ev is not None:
         esz = x.element_size()
-        flops = 2.0 * B * T_rows * Co * Ci * K
+        flops = 2.0 * B * T_rows * Co * Ci * K / groups
         nbytes = (B * T_in * Ci * esz + out.numel() * out.element_size() +
                   (res1.numel() * res1.element_size() if res1 is not None else 0) +
                   (res2.numel() * res2.element_size() if res2 is not None else 0) +
@@ -355,3 +358,104 @@ def stft_mel(wav, window, fb, n_fft=1024, hop=256, n_mels=80, log_floor=1e-5):
                                       float(log_floor), _ptr(mel), _ptr(energy), _stream(wav)),
                "vo_stft_mel")
     return mel, energy
+
+
+def stft_mel_ex(wav, window, fb, n_fft=1024, hop=256, n_mels=80, pad=None, mag_eps=0.0, clip=False,
+                log_floor=1e-5):
+    """General framing (vo_stft_mel_ex): wav (B, N) fp32 -> log-mel (B, n_mels, F),
+    F = 1 + (N + 2 pad - n_fft) // hop.  HiFi-GAN training mel: pad=(n_fft-hop)//2, mag_eps=1e-9."""
+    _contig(wav, "wav")
+    B, N = wav.shape
+    pad = n_fft // 2 if pad is None else pad
+    F = 1 + (N + 2 * pad - n_fft) // hop
+    mel = torch.empty((B, n_mels, F), dtype=torch.float32, device=wav.device)
+    _lib.check(_lib.lib().vo_stft_mel_ex(_ptr(wav), B, N, _ptr(window), _ptr(fb), n_fft, hop, n_mels, pad,
+                                         float(mag_eps), int(bool(clip)), float(log_floor), _ptr(mel), None,
+                                         _stream(wav)), "vo_stft_mel_ex")
+    return mel
+
+
+# ----------------------------------------------------------------------------- HiFi-GAN training (C5)
+
+def pack_grouped_weight(w, dtype, groups=1, ci_pad=None):
+    """(Co, Ci/groups, K) fp32 -> dense [K][Co][Ci_pad] block-diagonal (vo_conv1d groups mode)."""
+    w = w.detach().float().contiguous()
+    Co, cig, K = w.shape
+    Ci = cig * groups
+    ci_pad = Ci if ci_pad is None else ci_pad
+    out = torch.empty((K, Co, ci_pad), dtype=dtype, device=w.device)
+    _lib.check(_lib.lib().vo_pack_grouped(_ptr(w), Co, Ci, K, groups, ci_pad, _ptr(out), vo_dtype(dtype),
+                                          _stream(w)), "vo_pack_grouped")
+    return out
+
+
+def period_fold(wav, period, dtype):
+    """wav (B, T) fp32 -> (B * period, ceil(T / period), 8) channels-last (MPD input)."""
+    _contig(wav, "wav")
+    B, T = wav.shape
+    H = (T + period - 1) // period
+    out = torch.empty((B * period, H, 8), dtype=dtype, device=wav.device)
+    _lib.check(_lib.lib().vo_period_fold(_ptr(wav), B, T, period, _ptr(out), vo_dtype(dtype), _stream(wav)),
+               "vo_period_fold")
+    return out
+
+
+def wav_cl8(wav, dtype):
+    """(B, T) fp32 -> (B, T, 8) channels-last, channel 0 = wav (MSD input)."""
+    _contig(wav, "wav")
+    out = torch.empty(wav.shape + (8,), dtype=dtype, device=wav.device)
+    _lib.check(_lib.lib().vo_wav_cl8(_ptr(wav), wav.numel(), _ptr(out), vo_dtype(dtype), _stream(wav)),
+               "vo_wav_cl8")
+    return out
+
+
+def avgpool_wav(wav):
+    """AvgPool1d(4, 2, padding=2) over (B, T) fp32 -> (B, T // 2 + 1)."""
+    _contig(wav, "wav")
+    B, T = wav.shape
+    out = torch.empty((B, T // 2 + 1), dtype=torch.float32, device=wav.device)
+    _lib.check(_lib.lib().vo_avgpool_wav(_ptr(wav), B, T, _ptr(out), _stream(wav)), "vo_avgpool_wav")
+    return out
+
+
+GAN_L1, GAN_ONE_MINUS_SQ, GAN_SQ = 0, 1, 2
+
+
+def _rows_view(t):
+    """(..., width) view with unit column stride -> (rows, width, ld) for the reductions."""
+    if t.stride(-1) != 1:
+        raise ValueError("gan_reduce: last dim must be contiguous")
+    width = t.shape[-1]
+    lead = t.reshape(-1, width) if t.dim() != 2 else t
+    if lead.dim() != 2 or (lead.shape[0] > 1 and lead.stride(0) < width):
+        raise ValueError("gan_reduce: view not expressible as rows x width")
+    return lead, lead.shape[0], width, lead.stride(0) if lead.shape[0] > 1 else width
+
+
+def gan_reduce(kind, a, b=None, out=None):
+    """sum over a of |a - b| (GAN_L1), (1 - a)^2 or a^2 -> fp32 scalar tensor (accumulated into out)."""
+    la, rows, width, lda = _rows_view(a)
+    ldb = 0
+    if b is not None:
+        lb, rb, wb, ldb = _rows_view(b)
+        if (rb, wb) != (rows, width) or b.dtype != a.dtype:
+            raise ValueError("gan_reduce: a / b mismatch")
+        b = lb
+    if out is None:
+        out = torch.zeros((), dtype=torch.float32, device=a.device)
+    _lib.check(_lib.lib().vo_gan_reduce(kind, _ptr(la), lda, _ptr(b), ldb, rows, width, vo_dtype(a), _ptr(out),
+                                        _stream(a)), "vo_gan_reduce")
+    return out
+
+
+def gan_reduce_grad(kind, a, b, scale):
+    """d(scale * sum)/da in a contiguous tensor shaped like a (scale: fp32 device scalar)."""
+    la, rows, width, lda = _rows_view(a)
+    ldb = 0
+    if b is not None:
+        b, _, _, ldb = _rows_view(b)
+    ga = torch.empty((rows, width), dtype=a.dtype, device=a.device)
+    _lib.check(_lib.lib().vo_gan_reduce_grad(kind, _ptr(la), lda, _ptr(b), ldb, rows, width, vo_dtype(a),
+                                             _ptr(scale.float().contiguous()), _ptr(ga), width, _stream(a)),
+               "vo_gan_reduce_grad")
+    return ga.reshape(a.shape)
