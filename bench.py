@@ -48,8 +48,9 @@ def parse():
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
-    ap.add_argument("--mode", default="infer", choices=["infer", "train"],
-                    help="infer: end-to-end synthesis (headline); train: C4 training step (DDP)")
+    ap.add_argument("--mode", default="infer", choices=["infer", "train", "gan"],
+                    help="infer: end-to-end synthesis (headline); train: C4 training step (DDP); "
+                         "gan: C5 HiFi-GAN training step (DDP)")
     return ap.parse_args()
 
 
@@ -102,6 +103,58 @@ def bench_train(a, dev, rank, world, dist):
             "final_loss": round(float(losses[0]), 5),
             "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
                        "seq_len": a.mel_len, "src_len": a.src_len, "parallelism": f"dp{world} (RCCL bucketed all-reduce)"}}))
+
+
+def bench_gan(a, dev, rank, world, dist):
+    """C5: HiFi-GAN V1 training step (generator + MPD + MSD, D step then G step with adversarial,
+    feature-matching and 45 x mel-L1 losses, AdamW) on B segments of 8192 samples per GPU
+    (scripts/hifigan/config.json: batch 16, segment 8192)."""
+    from helpers import hifigan_arrays, hifigan_h
+    from weights import load_into
+    from visual_onoma_to_wave_amd import hifigan
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MelLoss
+    h = hifigan.AttrDict(hifigan_h())
+    g = hifigan.Generator(h)
+    load_into(g, hifigan_arrays())
+    g = g.to(dev)
+    torch.manual_seed(1234)  # identical discriminator init on every rank (broadcast anyway)
+    tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev)
+    tr.set_compute_dtype(torch.float32 if a.precision == "fp32" else torch.bfloat16)
+    B, seg = a.batch, h.segment_size
+    gen = torch.Generator().manual_seed(99 + rank)
+    t = torch.arange(seg, dtype=torch.float32) / h.sampling_rate
+    f0 = 110.0 + 330.0 * torch.rand(B, 1, generator=gen)
+    y = (0.3 * torch.sin(2 * np.pi * f0 * t) + 0.05 * torch.randn(B, seg, generator=gen)).to(dev)
+    with torch.no_grad():
+        x = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin, h.fmax).to(dev).mel(y)
+    x = x.transpose(1, 2).contiguous()  # (B, 32, 80) channels-last generator input
+    for _ in range(a.warmup):
+        tr.step(x, y)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        losses = tr.step(x, y)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    samples = B * seg * a.steps * world
+    if rank == 0:
+        print(json.dumps({
+            "metric": "C5 HiFi-GAN training audio samples/sec (G + MPD + MSD, DDP)", "value": round(samples / elapsed, 1),
+            "unit": "audio samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16" if a.precision != "fp32" else "f32",
+            "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
+            "losses": {k: round(float(v), 4) for k, v in losses.items()},
+            "config": {"workload": "C5 HiFi-GAN V1 train step", "per_gpu_batch": B, "global_batch": B * world,
+                       "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D)"}}))
 
 
 def build_models(device, precision):
@@ -174,6 +227,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    if a.mode == "gan":
+        if a.batch == 32:
+            a.batch = 16  # scripts/hifigan/config.json batch_size
+        bench_gan(a, dev, rank, world, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     if a.mode == "train":
         bench_train(a, dev, rank, world, dist)
         if dist:

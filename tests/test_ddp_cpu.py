@@ -66,3 +66,63 @@ def test_unused_parameters_are_identified():
     skip = unused_on_path(m)
     names = {n for n, p in m.named_parameters() if id(p) in skip}
     assert names == {"encoder.src_word_emb.weight", "variance_adaptor.kurt_embedding.weight"}
+
+
+def _gan_models():
+    torch.manual_seed(0)
+    g = torch.nn.Sequential(torch.nn.Linear(8, 64), torch.nn.Tanh(), torch.nn.Linear(64, 16))
+    d = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.LeakyReLU(0.1), torch.nn.Linear(32, 1))
+    return g, d
+
+
+def _gan_step(g, d, x, y, bk_g=None, bk_d=None):
+    """HifiGanTrainer.step's structure: D step on detached G output, then G step with D frozen."""
+    yh = g(x)
+    for p in d.parameters():
+        p.requires_grad_(True)
+    d.zero_grad()
+    ((1 - d(y)) ** 2).mean().add((d(yh.detach()) ** 2).mean()).backward()
+    if bk_d is not None:
+        bk_d.finish()
+    gd = [p.grad.clone() for p in d.parameters()]
+    for p in d.parameters():
+        p.requires_grad_(False)
+    g.zero_grad()
+    (((1 - d(yh)) ** 2).mean() + (yh - y).abs().mean() * 45).backward()
+    if bk_g is not None:
+        bk_g.finish()
+    return gd, [p.grad.clone() for p in g.parameters()]
+
+
+def _gan_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from visual_onoma_to_wave_amd.train import GradBucketer
+    g, d = _gan_models()
+    bk_g = GradBucketer(g.parameters(), bucket_mb=0.002)
+    bk_d = GradBucketer(d.parameters(), bucket_mb=0.002)
+    torch.manual_seed(7)
+    x, y = torch.randn(8, 8), torch.randn(8, 16)
+    sl = slice(rank * 4, (rank + 1) * 4)
+    for _ in range(2):
+        res = _gan_step(g, d, x[sl], y[sl], bk_g, bk_d)
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_gan_two_bucketers_match_global_batch():
+    """Generator and discriminator gradients averaged by their own bucketers (D frozen in the
+    G step, so its hooks stay silent there) equal the single-process global-batch gradients."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gan_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    g, d = _gan_models()
+    torch.manual_seed(7)
+    x, y = torch.randn(8, 8), torch.randn(8, 16)
+    gd, gg = _gan_step(g, d, x, y)
+    for r in range(world):
+        for a, b in zip(out[r][0], gd):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        for a, b in zip(out[r][1], gg):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
