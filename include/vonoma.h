@@ -225,7 +225,19 @@ int vo_stft_mel(const float* wav, int B, int N, const float* window, const float
  * no clip, slaney fb) and vo_stft_mel (pad n_fft/2, eps 0, clip). */
 int vo_stft_mel_ex(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
                    int hop, int n_mels, int pad, float mag_eps, int clip, float log_floor, float* mel,
-                   float* energy, void* stream);
+                   float* energy, float* fstats, void* stream);
+/* fstats (nullable, (B, F, 2)): per frame sum_k |X_k|^2 and sum_k log(|X_k|^2 + 1e-8), the
+ * power-spectrum statistics of Preprocessor._get_kurtosis. */
+
+/* Character-level acoustic features (Preprocessor._process energy
+ * averaging and _get_kurtosis, scripts/preprocessor/preprocessor.py:339-357,395-403): for
+ * utterance b with characters j in [char_off[b], char_off[b+1]) of dur[j] frames (consecutive,
+ * from frame 0): e_char[j] = mean(energy[b, span]) (0 if dur 0); k_char[j] = (eta+2)(eta+3)/
+ * (eta(eta+1)+1e-8), eta = (3 - g + sqrt((g-3)^2 + 24 g)) / (12 g),
+ * g = log(mean p + 1e-8) - mean log(p + 1e-8) over the span's n_bins x dur[j] power values. */
+int vo_char_features(const float* energy, const float* fstats, int F, const int32_t* dur,
+                     const int32_t* char_off, int B, int n_bins, float* e_char, float* k_char,
+                     void* stream);
 
 /* ------------------------------------------------------------------ HiFi-GAN training (C5)
  * Discriminator glue (the reference ships no discriminator code, only
@@ -247,6 +259,19 @@ int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int6
                   int dtype, float* out, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
                        int width, int dtype, const float* scale, void* ga, int ldg, void* stream);
+
+/* ------------------------------------------------------------------ training input pipeline
+ * Glyph batch: B grayscale strips packed in px (strip b at img_off[b],
+ * H rows of img_w[b] uint8 columns) -> out (B, 1, H, W_out) fp32 = pixel / 255 with each
+ * character j of sample b (char_off[b] <= j < char_off[b+1]: columns [char_start[j],
+ * char_start[j] + char_len[j]) of its strip) centred in a `cell`-wide white cell
+ * (pleft = (cell-len)/2 + (cell-len)%2), white right-padding to W_out and `margin` white
+ * columns on the left.  char_off == NULL: strips copied as they are (already centred).
+ * Replaces Dataset.character_padding_forinput (scripts/dataset.py:71-92), pad_2D_gray_image
+ * (scripts/utils/tools.py:616-635) and to_device's ToTensor (tools.py:18-20,50-51). */
+int vo_glyph_batch(const uint8_t* px, const int64_t* img_off, const int32_t* img_w,
+                   const int32_t* char_off, const int32_t* char_start, const int32_t* char_len,
+                   int B, int H, int cell, int margin, int W_out, float* out, void* stream);
 
 #ifdef __cplusplus
 }

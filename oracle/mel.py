@@ -96,3 +96,29 @@ def tacotron_mel(wav, n_fft=1024, hop=256, n_mels=80, sr=22050, fmin=0.0, fmax=8
     basis = torch.from_numpy(librosa_mel(sr, n_fft, n_mels, fmin, fmax))
     mel = torch.matmul(basis, mag)
     return torch.log(torch.clamp(mel, min=1e-5)), torch.linalg.vector_norm(mag, dim=-2)
+
+
+def char_features(wav, duration, n_fft=1024, hop=256, n_mels=80, sr=22050, fmin=0.0, fmax=8000.0):
+    """Preprocessor._process feature steps (scripts/preprocessor/preprocessor.py:386-403) and
+    _get_kurtosis (:339-357): (mel (sum d, 80), char energy, char kurtosis)."""
+    wav = torch.clip(torch.as_tensor(np.asarray(wav, np.float32)), -1, 1)
+    logmel, energy = get_spec(wav, n_fft, hop, n_fft, n_mels, sr, fmin, fmax)
+    d = [int(x) for x in duration]
+    T = sum(d)
+    mel = logmel[:, :T].numpy().T
+    e = energy[:T].numpy().copy()
+    pos = 0
+    for i, di in enumerate(d):
+        e[i] = np.mean(e[pos:pos + di]) if di > 0 else 0
+        pos += di
+    e = e[:len(d)]
+    eps = 1e-8
+    power = magnitude(wav, n_fft, hop, n_fft) ** 2
+    dd = [0] + d
+    kurt = np.zeros(len(d))
+    for i in range(len(d)):
+        spec = power[:, sum(dd[:i + 1]): sum(dd[:i + 2])]
+        gamma = torch.log(torch.mean(spec) + eps) - torch.mean(torch.log(spec + eps))
+        eta = (3 - gamma + torch.sqrt((gamma - 3) ** 2 + 24 * gamma)) / (12 * gamma)
+        kurt[i] = (eta + 2) * (eta + 3) / (eta * (eta + 1) + eps)
+    return mel, e, kurt

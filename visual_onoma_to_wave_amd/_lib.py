@@ -90,7 +90,9 @@ _SIGNATURES = {
     "vo_stft_mel": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p, c_void_p, c_void_p]),
     "vo_stft_mel_ex": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                               c_int, c_float, c_void_p, c_void_p, c_void_p]),
+                               c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
     "vo_pack_grouped": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "vo_period_fold": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "vo_wav_cl8": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
@@ -99,6 +101,8 @@ _SIGNATURES = {
                               c_void_p]),
     "vo_gan_reduce_grad": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
                                    c_void_p, c_int, c_void_p]),
+    "vo_glyph_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                               c_int, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None

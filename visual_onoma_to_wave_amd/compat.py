@@ -35,6 +35,7 @@ _MAP = {
     "utils.tools": "utils.tools",
     "utils.symbols": "utils.symbols",
     "audio": "audio",
+    "dataset": "dataset",
 }
 
 

@@ -30,10 +30,10 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
                                                        const float* __restrict__ fb, int n_fft, int hop,
                                                        int n_mels, float log_floor, float* __restrict__ mel,
                                                        float* __restrict__ energy, int pad, float mag_eps,
-                                                       int clip) {
+                                                       int clip, float* __restrict__ fstats) {
   __shared__ float2 buf[2][STFT_MAX_N / 2];
   __shared__ float mag[STFT_MAX_N / 2 + 1];
-  __shared__ float red[4];
+  __shared__ float red[4], red_p[4], red_l[4];
   const int f = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x;
   const int half = n_fft / 2;
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
   }
 
   // split into the n_fft-point real spectrum, magnitudes
-  float e2 = 0.f;
+  float e2 = 0.f, sp = 0.f, sl = 0.f;
   for (int k = tid; k <= half; k += 256) {
     const float2 zk = buf[src][k & (L - 1)];
     const float2 zn = buf[src][(L - k) & (L - 1)];
@@ -85,11 +85,28 @@ __global__ void __launch_bounds__(256) stft_mel_kernel(const float* __restrict__
     const float mg = sqrtf(xr * xr + xi * xi + mag_eps);
     mag[k] = mg;
     e2 += mg * mg;
+    if (fstats) {  // power-spectrum statistics of the frame (kurtosis feature)
+      const float p = mg * mg;
+      sp += p;
+      sl += logf(p + 1e-8f);
+    }
   }
   e2 = wave_sum(e2);
   if ((tid & 63) == 0) red[tid >> 6] = e2;
+  if (fstats) {
+    sp = wave_sum(sp);
+    sl = wave_sum(sl);
+    if ((tid & 63) == 0) {
+      red_p[tid >> 6] = sp;
+      red_l[tid >> 6] = sl;
+    }
+  }
   __syncthreads();
   if (tid == 0 && energy) energy[(int64_t)b * F + f] = sqrtf(red[0] + red[1] + red[2] + red[3]);
+  if (tid == 0 && fstats) {
+    fstats[((int64_t)b * F + f) * 2] = red_p[0] + red_p[1] + red_p[2] + red_p[3];
+    fstats[((int64_t)b * F + f) * 2 + 1] = red_l[0] + red_l[1] + red_l[2] + red_l[3];
+  }
 
   // mel projection: wave w handles bins w, w+4, ...; lanes stride over frequency
   const int lane = tid & 63, wave = tid >> 6;
@@ -108,7 +125,7 @@ using namespace vo;
 
 extern "C" int vo_stft_mel_ex(const float* wav, int B, int N, const float* window, const float* fb, int n_fft,
                               int hop, int n_mels, int pad, float mag_eps, int clip, float log_floor, float* mel,
-                              float* energy, void* stream) {
+                              float* energy, float* fstats, void* stream) {
   VO_CHECK_ARG(wav && window && fb && mel, "stft_mel: null pointer");
   VO_CHECK_ARG(n_fft >= 8 && n_fft <= STFT_MAX_N && (n_fft & (n_fft - 1)) == 0, "stft_mel: n_fft=%d must be a power of "
                "two in [8, %d]", n_fft, STFT_MAX_N);
@@ -118,12 +135,13 @@ extern "C" int vo_stft_mel_ex(const float* wav, int B, int N, const float* windo
   const int F = 1 + (N + 2 * pad - n_fft) / hop;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(stft_mel_kernel, dim3((unsigned)F, (unsigned)B), dim3(256), 0, st, wav, N, F, window, fb, n_fft,
-                     hop, n_mels, log_floor, mel, energy, pad, mag_eps, clip);
+                     hop, n_mels, log_floor, mel, energy, pad, mag_eps, clip, fstats);
   VO_RETURN_LAUNCH();
 }
 
 // torchaudio center=True framing (pad n_fft / 2, F = 1 + N / hop), clipped input, |X|
 extern "C" int vo_stft_mel(const float* wav, int B, int N, const float* window, const float* fb, int n_fft, int hop,
                            int n_mels, float log_floor, float* mel, float* energy, void* stream) {
-  return vo_stft_mel_ex(wav, B, N, window, fb, n_fft, hop, n_mels, n_fft / 2, 0.f, 1, log_floor, mel, energy, stream);
+  return vo_stft_mel_ex(wav, B, N, window, fb, n_fft, hop, n_mels, n_fft / 2, 0.f, 1, log_floor, mel, energy, nullptr,
+                        stream);
 }

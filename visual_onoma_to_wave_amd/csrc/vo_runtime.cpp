@@ -66,7 +66,7 @@ static const char* const kSymbols[] = {
     "vo_variance_head",  "vo_vfe_stencil",   "vo_add_pos_class", "vo_conv_post",   "vo_transpose_bct",
     "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair", "vo_stft_mel_ex",
     "vo_pack_grouped",   "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
-    "vo_gan_reduce_grad",
+    "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -7,6 +7,8 @@ tensors; there is no CPU path -- a CPU tensor raises.
 
 import ctypes
 
+import numpy as np
+
 import torch
 
 from . import _lib, profiling
@@ -370,7 +372,7 @@ def stft_mel_ex(wav, window, fb, n_fft=1024, hop=256, n_mels=80, pad=None, mag_e
     F = 1 + (N + 2 * pad - n_fft) // hop
     mel = torch.empty((B, n_mels, F), dtype=torch.float32, device=wav.device)
     _lib.check(_lib.lib().vo_stft_mel_ex(_ptr(wav), B, N, _ptr(window), _ptr(fb), n_fft, hop, n_mels, pad,
-                                         float(mag_eps), int(bool(clip)), float(log_floor), _ptr(mel), None,
+                                         float(mag_eps), int(bool(clip)), float(log_floor), _ptr(mel), None, None,
                                          _stream(wav)), "vo_stft_mel_ex")
     return mel
 
@@ -459,3 +461,79 @@ def gan_reduce_grad(kind, a, b, scale):
                                              _ptr(scale.float().contiguous()), _ptr(ga), width, _stream(a)),
                "vo_gan_reduce_grad")
     return ga.reshape(a.shape)
+
+
+# ----------------------------------------------------------------------------- training input pipeline
+
+def glyph_batch(strips, char_widths, cell, margin, device, W_out=None):
+    """Grayscale uint8 strips (list of (H, W_b)) + per-character widths (list of int arrays, or
+    None for already-centred strips) -> (B, 1, H, W_out) fp32 on ``device`` (vo_glyph_batch:
+    per-character centring into ``cell`` columns, white padding, ToTensor)."""
+    B = len(strips)
+    H = int(strips[0].shape[0])
+    widths = [int(s.shape[1]) for s in strips]
+    if any(int(s.shape[0]) != H for s in strips):
+        raise ValueError("glyph_batch: strips must share their height")
+    offs = np.zeros(B, np.int64)
+    offs[1:] = np.cumsum([H * w for w in widths])[:-1]
+    packed = np.concatenate([np.ascontiguousarray(s, dtype=np.uint8).reshape(-1) for s in strips])
+    if char_widths is not None:
+        cw = [np.asarray(w, np.int64).reshape(-1) for w in char_widths]
+        if any(int(w.max(initial=0)) > cell for w in cw):
+            raise ValueError(f"glyph_batch: a character is wider than the {cell}-pixel cell")
+        for w, s in zip(cw, widths):
+            if int(w.sum()) > s:
+                raise ValueError("glyph_batch: character widths exceed the strip")
+        char_off = np.zeros(B + 1, np.int32)
+        char_off[1:] = np.cumsum([len(w) for w in cw])
+        starts = np.concatenate([np.concatenate([[0], np.cumsum(w)[:-1]]) if len(w) else np.zeros(0, np.int64)
+                                 for w in cw]).astype(np.int32)
+        lens = np.concatenate(cw).astype(np.int32)
+        w_out = max(len(w) for w in cw) * cell + 2 * margin
+    else:
+        char_off = starts = lens = None
+        w_out = max(widths) + 2 * margin
+    W_out = W_out or w_out
+    dev = torch.device(device)
+    t = lambda a: torch.from_numpy(a).to(dev, non_blocking=True) if a is not None else None  # noqa: E731
+    px_d, off_d, w_d = t(packed), t(offs), t(np.asarray(widths, np.int32))
+    co_d, cs_d, cl_d = t(char_off), t(starts), t(lens)
+    out = torch.empty((B, 1, H, W_out), dtype=torch.float32, device=dev)
+    _lib.check(_lib.lib().vo_glyph_batch(_ptr(px_d), _ptr(off_d), _ptr(w_d), _ptr(co_d), _ptr(cs_d), _ptr(cl_d), B,
+                                         H, int(cell), int(margin), int(W_out), _ptr(out), _stream(out)),
+               "vo_glyph_batch")
+    return out
+
+
+# ----------------------------------------------------------------------------- offline feature extraction
+
+def spec_features(wav, window, fb, n_fft=1024, hop=256, log_floor=1e-5):
+    """torchaudio-framed log-mel (B, n_mels, F), frame energy (B, F) and per-frame power
+    statistics (B, F, 2) of wav (B, N) (vo_stft_mel_ex, clipped input, center=True)."""
+    _contig(wav, "wav")
+    B, N = wav.shape
+    F = 1 + N // hop
+    mel = torch.empty((B, fb.shape[1], F), dtype=torch.float32, device=wav.device)
+    energy = torch.empty((B, F), dtype=torch.float32, device=wav.device)
+    fstats = torch.empty((B, F, 2), dtype=torch.float32, device=wav.device)
+    _lib.check(_lib.lib().vo_stft_mel_ex(_ptr(wav), B, N, _ptr(window), _ptr(fb), n_fft, hop, fb.shape[1],
+                                         n_fft // 2, 0.0, 1, float(log_floor), _ptr(mel), _ptr(energy),
+                                         _ptr(fstats), _stream(wav)), "vo_stft_mel_ex")
+    return mel, energy, fstats
+
+
+def char_features(energy, fstats, durations, n_bins):
+    """energy (B, F), fstats (B, F, 2), durations: list of B int arrays -> (energy_char, kurtosis_char)
+    lists (per-character mean energy, spectral kurtosis) via vo_char_features."""
+    B, F = energy.shape
+    dur = np.concatenate([np.asarray(d, np.int32).reshape(-1) for d in durations])
+    off = np.zeros(B + 1, np.int32)
+    off[1:] = np.cumsum([len(d) for d in durations])
+    dev = energy.device
+    dur_d, off_d = torch.from_numpy(dur).to(dev), torch.from_numpy(off).to(dev)
+    e = torch.empty(int(off[-1]), dtype=torch.float32, device=dev)
+    k = torch.empty(int(off[-1]), dtype=torch.float32, device=dev)
+    _lib.check(_lib.lib().vo_char_features(_ptr(energy.contiguous()), _ptr(fstats.contiguous()), F, _ptr(dur_d),
+                                           _ptr(off_d), B, int(n_bins), _ptr(e), _ptr(k), _stream(energy)),
+               "vo_char_features")
+    return [e[off[i]:off[i + 1]] for i in range(B)], [k[off[i]:off[i + 1]] for i in range(B)]

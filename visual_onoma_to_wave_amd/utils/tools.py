@@ -1,6 +1,7 @@
 """Batch / mask / padding helpers on the path (reference: scripts/utils/tools.py).
 
-to_device              <- tools.py:22-72   (the host -> device crossing of a 13-item batch)
+to_device              <- tools.py:22-72   (the host -> device crossing of a 13-item batch; glyph
+                          batches are laid out on the GPU, dataset.GlyphBatch / vo_glyph_batch)
 get_mask_from_lengths  <- tools.py:164-171 (HIP kernel; True = padding)
 expand                 <- tools.py:173-177
 pad_1D / pad_2D / pad_2D_gray_image <- tools.py:585-635 (host-side collate padding)
@@ -26,6 +27,21 @@ def _to_tensor_image(im):
     return t.float().div_(255.0) if t.dtype == torch.uint8 else t.float()
 
 
+def _images_to_device(images, device):
+    """Glyph batches are laid out on the GPU (vo_glyph_batch: per-character centring, white
+    padding and ToTensor in one launch); an already padded (B, H, W) uint8 batch (the
+    reference's pad_2D_gray_image output) gets the device ToTensor only."""
+    from ..dataset import GlyphBatch
+    if isinstance(images, GlyphBatch):
+        return images.to(device)
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        arr = [np.asarray(im) for im in images]
+        if all(a.dtype == np.uint8 and a.ndim == 2 for a in arr):
+            return ops.glyph_batch(arr, None, 0, 0, dev)
+    return torch.stack([_to_tensor_image(im) for im in images]).to(device)
+
+
 def to_device(data, device):
     (ids, audiotypes, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len, energies,
      kurtosises, durations, images, event_image_features) = data
@@ -42,7 +58,7 @@ def to_device(data, device):
     if durations is not None:
         durations = torch.from_numpy(durations).float().to(device)
     if images is not None:
-        images = torch.stack([_to_tensor_image(im) for im in images]).to(device)
+        images = _images_to_device(images, device)
     if event_image_features is not None and event_image_features[0] is not None:
         event_image_features = torch.from_numpy(event_image_features).float().to(device)
     else:
