@@ -23,7 +23,7 @@ def load(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        m = re.search(r"conv1d_kernel<.*,\s*(\d+)>", name)
+        m = re.search(r"conv1d_kernel<[^>]*?(?:true|false),\s*(\d+)", name)  # ROLE follows the NICE flag
         if m and m.group(1) != "0":
             acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
             continue
