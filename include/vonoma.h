@@ -260,6 +260,20 @@ int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int6
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
                        int width, int dtype, const float* scale, void* ga, int ldg, void* stream);
 
+/* ------------------------------------------------------------------ training backward
+ * Weight gradient of a channels-last conv on MFMA (replaces the MIOpen weight pass of the
+ * training backward):
+ *   dw[(m*N + n)*K + k] += sum_{b, t < T_A} A[b, t, m] * B[b, t*S + k*dil - pad, n]
+ * (B rows outside [0, T_B) read as 0; pre_a / pre_b: leaky-ReLU(slope) applied to that operand).
+ * Conv1d (Co, Ci, K): A = dY (T_out rows, M = Co), B = pre(x) (T_in rows, N = Ci).
+ * ConvTranspose1d (Ci, Co, 2s): A = pre(x) (T_in, M = Ci), B = dY (T_up, N = Co), S = s, pad p.
+ * dw fp32, accumulated with atomics: the caller zeroes it.  dtype: VO_BF16 or VO_F32 for both.
+ * vo_colsum: out[c] += sum_r x[r*ld + c] (bias gradient). */
+int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
+                    int N, int K, int S, int dil, int pad, int pre_a, int pre_b, float slope,
+                    int dtype, float* dw, void* stream);
+int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream);
+
 /* ------------------------------------------------------------------ training input pipeline
  * Glyph batch: B grayscale strips packed in px (strip b at img_off[b],
  * H rows of img_w[b] uint8 columns) -> out (B, 1, H, W_out) fp32 = pixel / 255 with each

@@ -268,3 +268,40 @@ def test_trainer_step_bf16():
     torch.cuda.synchronize()
     assert all(torch.isfinite(v) for v in losses.values())
     assert not torch.equal(before, g.conv_pre.weight_v.detach())
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,T,Ci,Co,K,dil,s,pad,pre", [
+    (2, 1000, 32, 32, 11, 5, 1, 25, 0.1), (3, 517, 256, 256, 3, 1, 1, 1, 0.1), (2, 300, 80, 512, 7, 1, 1, 3, None),
+    (4, 2731, 32, 128, 5, 1, 3, 2, None), (2, 777, 1024, 256, 1, 1, 1, 0, None), (1, 5, 64, 64, 7, 3, 1, 9, 0.1)])
+def test_conv1d_wgrad_vs_torch(B, T, Ci, Co, K, dil, s, pad, pre, dt, tol):
+    """vo_conv1d_wgrad (dense conv: A = dY, B = pre(x)) against torch's conv1d weight gradient."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(T + K + Ci)
+    x = torch.randn(B, T, Ci, generator=g).to(dt).float()
+    T_out = (T + 2 * pad - dil * (K - 1) - 1) // s + 1
+    gy = torch.randn(B, T_out, Co, generator=g).to(dt).float()
+    xa = F.leaky_relu(x, pre) if pre is not None else x
+    ref = torch.nn.grad.conv1d_weight(xa.transpose(1, 2), (Co, Ci, K), gy.transpose(1, 2), stride=s, padding=pad,
+                                      dilation=dil)
+    got = ops.conv1d_wgrad(gy.cuda().to(dt), x.cuda().to(dt), K, S=s, dil=dil, pad=pad, pre_b=pre)
+    assert rel_l2(got.cpu(), ref) < tol
+    gb = ops.colsum(gy.cuda().to(dt).contiguous()).cpu()
+    assert rel_l2(gb, gy.sum(dim=(0, 1))) < 1e-5
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("Ci,Co,u,T", [(512, 256, 8, 32), (128, 64, 2, 1000), (64, 32, 2, 7)])
+def test_convtranspose_wgrad_vs_torch(Ci, Co, u, T, dt, tol):
+    """vo_conv1d_wgrad transposed form (A = lrelu(x), B = dY) against torch's ConvTranspose1d grad."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(Ci + T)
+    K, p = 2 * u, u // 2
+    x = torch.randn(2, Ci, T, generator=g).to(dt).float()
+    w = (torch.randn(Ci, Co, K, generator=g) * 0.05).requires_grad_(True)
+    y = F.conv_transpose1d(F.leaky_relu(x, 0.1), w, stride=u, padding=p)
+    gy = torch.randn(y.shape, generator=g).to(dt).float()
+    (ref,) = torch.autograd.grad(y, w, gy)
+    got = ops.conv1d_wgrad(x.transpose(1, 2).contiguous().cuda().to(dt), gy.transpose(1, 2).contiguous().cuda().to(dt),
+                           K, S=u, pad=p, pre_a=0.1, transposed=True)
+    assert rel_l2(got.cpu(), ref) < tol

@@ -4,9 +4,10 @@ The forward of every op is the same HIP kernel the inference path runs.  Backwar
 
 * Conv1d / Linear input-gradient: HIP -- the conv kernel itself over dY with the weights
   re-packed taps-reversed / channels-swapped (``vo_pack_weight`` mode DGRAD);
-* Conv1d weight / bias gradients, attention, LayerNorm and LengthRegulator backward:
-  PyTorch-ROCm (rocBLAS / MIOpen) recomputation -- the initial fallback SURVEY.md 8(b)
-  sanctions for C4; the HIP ``_bwd`` kernels replace them one by one.
+* Conv1d / Linear weight and bias gradients: HIP -- ``vo_conv1d_wgrad`` (MFMA, fragments
+  read transposed from LDS) and ``vo_colsum``;
+* attention, LayerNorm and LengthRegulator backward: PyTorch-ROCm recomputation -- the
+  initial fallback SURVEY.md 8(b) sanctions for C4.
 
 All functions take and return channels-last (B, T, C) activations.
 """
@@ -44,10 +45,14 @@ class Conv1dFn(torch.autograd.Function):
             gx = ops.conv1d(gz.to(cdt) if gz.dtype != cdt else gz, wd, None, Co=w.shape[1], K=K, dil=dil,
                             pad=(K - 1) * dil - pad, T_out=x.shape[1], out_dtype=x.dtype, compute_dtype=cdt)
         if ctx.needs_input_grad[1]:
-            gw = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), w.shape, gz.float().transpose(1, 2),
-                                             padding=pad, dilation=dil)
+            if x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
+                # MFMA weight gradient over transposed LDS reads (vo_conv1d_wgrad)
+                gw = ops.conv1d_wgrad(gz.to(x.dtype).contiguous(), x.contiguous(), K, dil=dil, pad=pad).to(w.dtype)
+            else:
+                gw = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), w.shape, gz.float().transpose(1, 2),
+                                                 padding=pad, dilation=dil)
         if has_b and ctx.needs_input_grad[2]:
-            gb = gz.float().sum(dim=(0, 1))
+            gb = ops.colsum(gz.contiguous())
         return gx, gw, gb, None, None, None, None, None, None
 
 

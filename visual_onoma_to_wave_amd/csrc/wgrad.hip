@@ -1,0 +1,240 @@
+// Weight / bias gradients of the channels-last Conv1d and polyphase ConvTranspose1d on MFMA
+// (training paths C4 / C5): replaces the MIOpen ``convolution_backward`` weight pass that
+// SURVEY.md 8(b) allowed as the initial fallback.
+//
+//   dW[(m * N + n) * K + k] += sum_{b, t < T_A} A[b, t, m] * B[b, t * S + k * dil - pad, n]
+//
+// (rows of B outside [0, T_B) are zero; optional leaky-ReLU applied to either operand as it is
+// staged).  Conv1d (Co, Ci, K):      A = dY (rows T_out, M = Co), B = pre(x) (rows T_in, N = Ci),
+//                                    S = stride, dil, pad of the conv.
+// ConvTranspose1d (Ci, Co, K = 2s):  A = pre(x) (rows T_in, M = Ci), B = dY (rows T_up, N = Co),
+//                                    S = s, dil = 1, pad = p.
+// GEMM view per tap: M x N output, reduction over the B*T_A rows.  Grid: (row splits, M/64 x
+// N/64 tiles, taps); each workgroup stages 64-row chunks of both operands into LDS in their
+// natural channels-last layout and reads the MFMA fragments transposed -- ds_read_b64_tr_b16
+// (gfx950) delivers 4 rows of one channel per lane, so the reduction dimension (rows) lands
+// on the fragment's k without a transpose pass.  Partial sums of the row splits meet in fp32
+// atomics (the caller zeroes dW).  fp32 parity mode: the same tiles with 16x16x4 f32 MFMAs.
+
+#include <algorithm>
+
+#include "vo_common.h"
+
+namespace vo {
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int WG_R = 64;   // rows per staged chunk (two 32-deep MFMA k-steps)
+constexpr int WG_T = 64;   // output tile (M and N)
+
+struct WgradArgs {
+  const void* a; int lda; int T_A;
+  const void* bsrc; int ldb; int T_B;
+  int M, N, K, S, dil, pad, Bn;
+  int pre_a, pre_b; float slope;
+  int rows_per_split;
+  float* dw;
+};
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+template <typename T> struct WgTile;
+template <> struct WgTile<bf16_t> { static constexpr int PITCH = 72; };  // 144-B rows: tr reads of 4 rows hit distinct banks
+template <> struct WgTile<float> { static constexpr int PITCH = 68; };
+
+__device__ __forceinline__ uint32_t lrelu_pack(uint32_t w, float s) {
+  const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
+  return (uint32_t)from_f32<bf16_t>(fmaxf(lo, lo * s)) | ((uint32_t)from_f32<bf16_t>(fmaxf(hi, hi * s)) << 16);
+}
+
+// 4 waves as 2 x 2, each a 32 x 32 sub-tile = 2 x 2 MFMA tiles
+template <typename TC>
+__global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
+  constexpr int P = WgTile<TC>::PITCH;
+  __shared__ __attribute__((aligned(16))) TC sa[WG_R * P];
+  __shared__ __attribute__((aligned(16))) TC sb[WG_R * P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+  const int tiles_n = (p.N + WG_T - 1) / WG_T;
+  const int m0 = (blockIdx.y / tiles_n) * WG_T, n0 = (blockIdx.y % tiles_n) * WG_T;
+  const int k = blockIdx.z;
+  const int64_t rows = (int64_t)p.Bn * p.T_A;
+  const int64_t r_begin = (int64_t)blockIdx.x * p.rows_per_split;
+  const int64_t r_end = min(rows, r_begin + p.rows_per_split);
+  const TC* A = reinterpret_cast<const TC*>(p.a);
+  const TC* Bs = reinterpret_cast<const TC*>(p.bsrc);
+  constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
+  constexpr int VPR = WG_T / EV;            // vectors per staged row
+  constexpr int NV = WG_R * VPR / 256;      // vectors per thread per operand
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
+    // ---- stage 64 rows of A (rows r0..) and of B (gathered rows of the same utterances)
+    u32x4_t va[NV], vb[NV];
+#pragma unroll
+    for (int s = 0; s < NV; ++s) {
+      const int v = tid + s * 256;
+      const int r = v / VPR, c = (v % VPR) * EV;
+      const int64_t q = r0 + r;
+      const bool qok = q < r_end;
+      const int64_t qq = qok ? q : r_begin;
+      const int b = (int)(qq / p.T_A), t = (int)(qq - (int64_t)b * p.T_A);
+      const int tb = t * p.S + k * p.dil - p.pad;
+      const bool bok = qok && tb >= 0 && tb < p.T_B;
+      const int ma = min(m0 + c, p.M - EV), nb = min(n0 + c, p.N - EV);
+      va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + ma);
+      vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + min(max(tb, 0), p.T_B - 1)) * p.ldb + nb);
+      if (!qok || m0 + c >= p.M) va[s] = u32x4_t{0u, 0u, 0u, 0u};
+      if (!bok || n0 + c >= p.N) vb[s] = u32x4_t{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // previous chunk's fragment reads are done
+#pragma unroll
+    for (int s = 0; s < NV; ++s) {
+      const int v = tid + s * 256;
+      const int r = v / VPR, c = (v % VPR) * EV;
+      u32x4_t x = va[s], y = vb[s];
+      if constexpr (sizeof(TC) == 2) {
+        if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
+        if (p.pre_b) y = u32x4_t{lrelu_pack(y.x, p.slope), lrelu_pack(y.y, p.slope), lrelu_pack(y.z, p.slope), lrelu_pack(y.w, p.slope)};
+      } else {
+        if (p.pre_a) {
+          float f[4] = {__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+          x = u32x4_t{__float_as_uint(fmaxf(f[0], f[0] * p.slope)), __float_as_uint(fmaxf(f[1], f[1] * p.slope)),
+                      __float_as_uint(fmaxf(f[2], f[2] * p.slope)), __float_as_uint(fmaxf(f[3], f[3] * p.slope))};
+        }
+        if (p.pre_b) {
+          float f[4] = {__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w)};
+          y = u32x4_t{__float_as_uint(fmaxf(f[0], f[0] * p.slope)), __float_as_uint(fmaxf(f[1], f[1] * p.slope)),
+                      __float_as_uint(fmaxf(f[2], f[2] * p.slope)), __float_as_uint(fmaxf(f[3], f[3] * p.slope))};
+        }
+      }
+      *reinterpret_cast<u32x4_t*>(sa + r * P + c) = x;
+      *reinterpret_cast<u32x4_t*>(sb + r * P + c) = y;
+    }
+    __syncthreads();
+
+    // ---- two 32-row k-steps
+#pragma unroll
+    for (int ks = 0; ks < WG_R / 32; ++ks) {
+      const int kr = ks * 32;
+      if constexpr (sizeof(TC) == 2) {
+        // fragment of 16 channels (c0..c0+15) x 8 rows (kr + 8g ..): two transposed 4-row reads
+        const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+        auto frag = [&](const TC* tile, int c0) {
+          const TC* base = tile + (kr + 8 * g + q) * P + c0 + 4 * pp;
+          typedef __attribute__((address_space(3))) v4s lds_v4s;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)base);
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + 4 * P));
+          // whole-vector bit cast: per-element __bf16 inserts were mis-lowered by hipcc (only the
+          // low dword of each read survived)
+          typedef short v8s __attribute__((ext_vector_type(8)));
+          const v8s all = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          Frag<bf16_t> f;
+          f.v = __builtin_bit_cast(bf16x8, all);
+          return f;
+        };
+        Frag<bf16_t> fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = frag(sa, wm + 16 * i);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = frag(sb, wn + 16 * j);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      } else {
+        // f32: element j of lane l = row kr + 8 (l >> 4) + j, channel l & 15 (scalar LDS reads)
+        const int g = lane >> 4, li = lane & 15;
+        Frag<float> fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            fa[i].v[e] = sa[(kr + 8 * g + e) * P + wm + 16 * i + li];
+          }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) fb[j].v[e] = sb[(kr + 8 * g + e) * P + wn + 16 * j + li];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      }
+    }
+  }
+
+  // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[(m N + n) K + k]
+  const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
+        if (m < p.M && n < p.N) atomicAdd(p.dw + ((int64_t)m * p.N + n) * p.K + k, acc[i][j][e]);
+      }
+}
+
+// column sums of a (rows x C) channels-last tensor -> db[C] (fp32 atomics; caller zeroes)
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, int64_t rows, int C, int ld,
+                                                     int rows_per_block, float* __restrict__ out) {
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int64_t r = r0; r < min(rows, r0 + rows_per_block); ++r) s += to_f32(x[r * ld + c]);
+    atomicAdd(out + c, s);
+  }
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M, int N,
+                               int K, int S, int dil, int pad, int pre_a, int pre_b, float slope, int dtype, float* dw,
+                               void* stream) {
+  VO_CHECK_ARG(a && b && dw, "conv1d_wgrad: null pointer");
+  VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1, "conv1d_wgrad: bad sizes");
+  const int ev = dtype == VO_BF16 ? 8 : 4;
+  VO_CHECK_ARG(M % ev == 0 && N % ev == 0 && lda % ev == 0 && ldb % ev == 0 && lda >= M && ldb >= N,
+               "conv1d_wgrad: M=%d N=%d (and leading dims) must be multiples of %d", M, N, ev);
+  WgradArgs p;
+  p.a = a; p.lda = lda; p.T_A = T_A; p.bsrc = b; p.ldb = ldb; p.T_B = T_B;
+  p.M = M; p.N = N; p.K = K; p.S = S; p.dil = dil; p.pad = pad; p.Bn = B;
+  p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope; p.dw = dw;
+  const int64_t rows = (int64_t)B * T_A;
+  const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
+  // enough workgroups to fill 256 CUs ~4 deep, at least 4 chunks of 64 rows each
+  int64_t splits = std::max<int64_t>(1, (1024 + (int64_t)tiles * K - 1) / ((int64_t)tiles * K));
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
+  p.rows_per_split = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
+  splits = (rows + p.rows_per_split - 1) / p.rows_per_split;
+  VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && K < 65536, "conv1d_wgrad: grid too large");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)K);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream) {
+  VO_CHECK_ARG(x && out && rows > 0 && C > 0 && ld >= C, "colsum: bad arguments");
+  const int rpb = 256;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned g = (unsigned)((rows + rpb - 1) / rpb);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, rows, C, ld, rpb, out);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, rows, C, ld, rpb, out);
+  VO_RETURN_LAUNCH();
+}

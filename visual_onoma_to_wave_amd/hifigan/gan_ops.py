@@ -10,9 +10,11 @@ Backward, per op:
     re-packed taps-reversed / channels-swapped (as in C4); of a polyphase ConvTranspose1d:
     the strided conv kernel (dX = conv1d(dY, W, stride s, pad p));
   * loss gradients: ``vo_gan_reduce_grad``;
-  * weight / bias gradients, the input gradient of strided / grouped discriminator convs and
-    the mel-loss STFT: PyTorch-ROCm (MIOpen ``convolution_backward``, ``torch.stft``) -- the
-    fallback SURVEY.md 8(b) sanctions for training backward.
+  * weight / bias gradients of dense convs (generator, MPD, conv_post): ``vo_conv1d_wgrad``
+    (MFMA over transposed LDS reads) and ``vo_colsum``;
+  * the grouped MSD convs' weight gradients, the input gradient of strided / grouped
+    discriminator convs and the mel-loss STFT: PyTorch-ROCm (MIOpen ``convolution_backward``,
+    ``torch.stft``) -- the fallback SURVEY.md 8(b) sanctions for training backward.
 """
 
 from dataclasses import dataclass
@@ -89,6 +91,14 @@ def _conv_fwd(x, w, b, res1, res2, spec, cdt):
                       stride=spec.stride, groups=spec.groups)
 
 
+def _pad_channels(t, mult=8):
+    """(B, T, C) -> C zero-padded to a multiple of ``mult`` (the wgrad kernel's vector width)."""
+    C = t.shape[-1]
+    if C % mult:
+        t = F.pad(t, (0, mult - C % mult))
+    return t.contiguous()
+
+
 def _ncw(t):
     return t.transpose(1, 2).float().contiguous()
 
@@ -123,9 +133,9 @@ class ConvFn(torch.autograd.Function):
             gz = gz[..., : w.shape[0]].contiguous()
         ci = w.shape[0] if spec.transposed is not None else w.shape[1] * spec.groups
         xin = x[..., :ci] if x.shape[-1] != ci else x
-        a = xin if spec.pre_slope is None else torch.where(xin > 0, xin, xin * spec.pre_slope)
         gx = gw = gb = None
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        ga = None
         if need_x and spec.plain():
             wd = ops.pack_dgrad_weight(w, cdt)
             ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
@@ -139,23 +149,38 @@ class ConvFn(torch.autograd.Function):
             ga = ops.conv1d(gz.to(cdt), wc, None, Co=w.shape[0], K=spec.K, pad=p, stride=s, T_out=x.shape[1],
                             out_dtype=x.dtype, compute_dtype=cdt)
             need_x = False
-        else:
-            ga = None
+        if (need_w or need_b) and spec.groups == 1:
+            # weight / bias gradient on MFMA (vo_conv1d_wgrad, vo_colsum)
+            gzc = _pad_channels(gz.to(x.dtype))
+            if need_w:
+                if spec.transposed is not None:
+                    s, p = spec.transposed
+                    dw = ops.conv1d_wgrad(_pad_channels(x), gzc, spec.K, S=s, pad=p, pre_a=spec.pre_slope,
+                                          transposed=True)
+                    gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
+                else:
+                    dw = ops.conv1d_wgrad(gzc, _pad_channels(x), spec.K, S=spec.stride, dil=spec.dil, pad=spec.pad,
+                                          pre_b=spec.pre_slope)
+                    gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
+            if need_b:
+                gb = ops.colsum(gz.contiguous())[: w.shape[1] if spec.transposed is not None else w.shape[0]]
+            need_w = need_b = False
         if need_x or need_w or need_b:
+            a = xin if spec.pre_slope is None else torch.where(xin > 0, xin, xin * spec.pre_slope)
             if spec.transposed is not None:
                 s, p = spec.transposed
                 stride, pad, tr = [s], [p], True
             else:
                 stride, pad, tr = [spec.stride], [spec.pad], False
-            gi, gw, gb = torch.ops.aten.convolution_backward(
+            gi, gw2, gb2 = torch.ops.aten.convolution_backward(
                 _ncw(gz), _ncw(a), w.float(), [w.shape[1] if tr else w.shape[0]], stride, pad, [spec.dil], tr, [0],
                 spec.groups, [need_x, need_w, need_b])
             if need_x:
                 ga = gi.transpose(1, 2).to(x.dtype)
-            if gw is not None:
-                gw = gw.to(w.dtype)
-            if gb is not None and spec.co_pad is not None:
-                gb = gb[: w.shape[0]]
+            if need_w:
+                gw = gw2.to(w.dtype)
+            if need_b:
+                gb = gb2
         if ga is not None:
             if spec.pre_slope is not None:
                 ga = ga * torch.where(xin > 0, 1.0, spec.pre_slope).to(ga.dtype)

@@ -537,3 +537,34 @@ def char_features(energy, fstats, durations, n_bins):
                                            _ptr(off_d), B, int(n_bins), _ptr(e), _ptr(k), _stream(energy)),
                "vo_char_features")
     return [e[off[i]:off[i + 1]] for i in range(B)], [k[off[i]:off[i + 1]] for i in range(B)]
+
+
+# ----------------------------------------------------------------------------- training backward
+
+def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False):
+    """Weight gradient on MFMA (vo_conv1d_wgrad).  Conv1d: a = dY (B, T_out, Co), b = x (B, T_in, Ci)
+    -> dW (Co, Ci, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY (B, T_up, Co)
+    -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand (None = identity)."""
+    _contig(a, "a")
+    _contig(b, "b")
+    if a.dtype != b.dtype:
+        raise TypeError("conv1d_wgrad: operand dtypes differ")
+    B, T_A, M = a.shape
+    _, T_B, N = b.shape
+    dw = torch.zeros((M, N, K), dtype=torch.float32, device=a.device)
+    slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
+    if pre_a is not None and pre_b is not None and pre_a != pre_b:
+        raise ValueError("conv1d_wgrad: one slope for both operands")
+    _lib.check(_lib.lib().vo_conv1d_wgrad(_ptr(a), M, T_A, _ptr(b), N, T_B, B, M, N, K, S, dil, pad,
+                                          int(pre_a is not None), int(pre_b is not None), float(slope),
+                                          vo_dtype(a), _ptr(dw), _stream(a)), "vo_conv1d_wgrad")
+    return dw
+
+
+def colsum(x):
+    """(..., C) -> (C,) fp32 column sums (bias gradient)."""
+    _contig(x, "x")
+    C = x.shape[-1]
+    out = torch.zeros(C, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().vo_colsum(_ptr(x), x.numel() // C, C, C, vo_dtype(x), _ptr(out), _stream(x)), "vo_colsum")
+    return out
