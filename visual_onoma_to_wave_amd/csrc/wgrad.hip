@@ -182,14 +182,32 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       }
 }
 
-// column sums of a (rows x C) channels-last tensor -> db[C] (fp32 atomics; caller zeroes)
+// column sums of a (rows x C) channels-last tensor -> out[C] (fp32 atomics; caller zeroes).
+// Thread t owns the 8-channel vector t % (C / 8) of rows t / (C / 8) + k * (256 / (C / 8)):
+// coalesced 16-byte loads, register accumulation, one LDS reduction and C atomics per block.
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, int64_t rows, int C, int ld,
                                                      int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int nv = C / 8;                       // 8-channel vectors per row (C % 8 == 0, nv <= 256)
+  const int per = 256 / nv;                   // row lanes per block
+  const int tid = threadIdx.x, cv = tid % nv, ro = tid / nv;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ro < per)
+    for (int64_t r = r0 + ro; r < r1; r += per) {
+      float v[8];
+      load8(x + r * ld + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {  // channel c = vector c / 8, element c % 8
     float s = 0.f;
-    for (int64_t r = r0; r < min(rows, r0 + rows_per_block); ++r) s += to_f32(x[r * ld + c]);
+    for (int q = 0; q < per; ++q) s += red[(q * nv + c / 8) * 8 + (c % 8)];
     atomicAdd(out + c, s);
   }
 }
@@ -228,8 +246,11 @@ extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, i
 }
 
 extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream) {
-  VO_CHECK_ARG(x && out && rows > 0 && C > 0 && ld >= C, "colsum: bad arguments");
-  const int rpb = 256;
+  VO_CHECK_ARG(x && out && rows > 0 && C > 0 && ld >= C && C % 8 == 0 && ld % 8 == 0 && C <= 2048,
+               "colsum: bad arguments (C %% 8 == 0, C <= 2048)");
+  // ~1024 blocks of >= 8 row passes each: enough parallelism for 256 CUs, few atomics per channel
+  const int per = 256 / (C / 8 > 0 ? C / 8 : 1);
+  const int rpb = (int)std::max<int64_t>(8 * std::max(per, 1), (rows + 1023) / 1024);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned g = (unsigned)((rows + rpb - 1) / rpb);
   if (dtype == VO_BF16)

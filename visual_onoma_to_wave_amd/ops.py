@@ -565,6 +565,9 @@ def colsum(x):
     """(..., C) -> (C,) fp32 column sums (bias gradient)."""
     _contig(x, "x")
     C = x.shape[-1]
+    if C % 8:
+        x = torch.nn.functional.pad(x, (0, 8 - C % 8)).contiguous()
+        return colsum(x)[:C]
     out = torch.zeros(C, dtype=torch.float32, device=x.device)
     _lib.check(_lib.lib().vo_colsum(_ptr(x), x.numel() // C, C, C, vo_dtype(x), _ptr(out), _stream(x)), "vo_colsum")
     return out
