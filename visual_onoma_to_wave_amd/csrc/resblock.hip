@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   constexpr int NC = C / 32;              // 32-channel planes
   constexpr int NI = C / (16 * WC);       // co tiles per wave
   constexpr int R1 = WT * 16 * NJ;        // c1 rows per tile
-  constexpr int SHW = NI == 4 ? 4 : 3;    // log2(4 * NI): weight-row swizzle
+  constexpr int SHW = NI >= 8 ? 5 : (NI == 4 ? 4 : 3);  // log2(4 * NI): weight-row swizzle
   constexpr int VPR = NC * 4;             // 16-byte vectors per activation row
   constexpr int MAXW = ((R1 + 64) * VPR + NT - 1) / NT;  // window vectors per thread, halo <= 64
   constexpr int TAPV = C * VPR;           // 16-byte vectors per weight tap (C co x C ci)
@@ -213,18 +213,15 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     store_group(0);
   }
 
-  // ---- input window staging geometry (row-major vectors: consecutive lanes, consecutive 16 B)
-  int xr[MAXW], xl[MAXW], xg[MAXW];
-  // (IP: recomputed at each use from tid -- a few VALU ops instead of 3 * MAXW live VGPRs)
-  auto win_geom = [&](int s) {
-    const int v = tid + s * NT;
-    const int r = v / VPR, rem = v - r * VPR;
-    xr[s] = r < win_rows ? r : 0x40000000;
-    xg[s] = rem * 8;
-    xl[s] = (rem >> 2) * win_rows * 32 + rb_off(r, rem & 3, 2);
-  };
-#pragma unroll
-  for (int s = 0; s < MAXW; ++s) win_geom(s);
+  // ---- input window staging geometry (row-major vectors: consecutive lanes, consecutive 16 B).
+  // NT is a multiple of VPR, so slot s of a thread is row r0 + s * RSTEP, same 16-byte column:
+  // one base row / column / LDS offset per thread, the slots are compile-time offsets (adding
+  // RSTEP rows keeps the XOR swizzle bit: RSTEP is a multiple of 8)
+  static_assert(NT % VPR == 0 && (NT / VPR) % 8 == 0, "window slot stride must keep the swizzle");
+  constexpr int RSTEP = NT / VPR;
+  const int xr0 = tid / VPR, xrem = tid - xr0 * VPR;
+  const int xg0 = xrem * 8;
+  const int xl0 = (xrem >> 2) * win_rows * 32 + rb_off(xr0, xrem & 3, 2);
   // Global loads are unconditional (clamped rows, zeroed when written to LDS): a load under a
   // divergent branch gets an immediate vmcnt(0) from the compiler and the prefetch is lost.
   u32x4 xw[MAXW];
@@ -235,22 +232,21 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     const bf16_t* base = a.x + (int64_t)b * T * C;
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
-      if constexpr (IP) win_geom(s);
-      const int t = R0 + xr[s];
-      xw_ok[s] = t >= 0 && t < T;
+      const int t = R0 + xr0 + s * RSTEP;
+      xw_ok[s] = t >= 0 && t < T && xr0 + s * RSTEP < win_rows;
       if constexpr ((ABL & 2) != 0)
         xw[s] = u32x4{(unsigned)t, 0u, 0u, 0u};
       else
-        xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg[s]);
+        xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg0);
     }
   };
   auto store_win = [&]() {
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
-      if constexpr (IP) win_geom(s);
       const u32x4 v = lrelu8(xw[s], slope);
       // idle slots (rows past the window) write the spare row after the bias table
-      *reinterpret_cast<u32x4*>(xr[s] < win_rows ? win + xl[s] : spare) = xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(xr0 + s * RSTEP < win_rows ? win + xl0 + s * RSTEP * 32 : spare) =
+          xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
     }
   };
 
@@ -540,6 +536,9 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
     if (cfg == 2) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
     if (cfg == 3) return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
+    // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
+    // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
+    // SIMD (12 waves, 2 x 6) 15 % slower.
     if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
     return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
   }
