@@ -531,8 +531,10 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
       case 1: {  // C = 256: 256 x 256 tile, 8 waves of 64 co x 128 rows (each weight tap feeds
                  // twice the rows of the 128 x 128 tile: 0.095/0.151/0.208 -> 0.077/0.125/0.172 ms
                  // for k = 3/7/11 at B = 32, bit-identical).  conv_cfg 1 = the 128 x 128 tile.
+        // s_setprio(1) around each MFMA cluster: +1-3 % (0.1667 -> 0.1654 ms at k = 11); conv_cfg 2 = without
         if (vo_tune_get("conv_cfg") == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
-        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
+        if (vo_tune_get("conv_cfg") == 2) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
+        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
       }
       case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);
       case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 4, 3>(d, st);
