@@ -140,7 +140,10 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   // slot p of a group holds (tap t, plane pl, row co, chunk q' = q ^ swz(co)).
   constexpr int GLN = GL ? (TG * TAPV) / (64 * NW) : 1;  // DMA instructions per wave per group
   static_assert(!GL || (TG * TAPV) % (64 * NW) == 0, "glds: group must split into whole wave-KiB");
-  int gl_src[GLN];
+  // per-lane source: tap within the group (gl_t) and 32-bit element offset within a tap (gl_off);
+  // the group's tap base is wave-uniform (SGPRs), the LDS destination too (m0 from an SGPR)
+  int gl_t[GLN], gl_off[GLN];
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   if constexpr (GL) {
 #pragma unroll
     for (int s = 0; s < GLN; ++s) {
@@ -148,7 +151,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       const int t = p / TAPV, vv = p - t * TAPV;
       const int pl = vv / (C * 4), rem = vv - pl * C * 4;
       const int co = rem >> 2, q = (rem & 3) ^ ((co >> (SHW - 1)) & 2);
-      gl_src[s] = t * C * C + co * C + pl * 32 + q * 8;
+      gl_t[s] = t;
+      gl_off[s] = co * C + pl * 32 + q * 8;
     }
   }
   auto load_group = [&](int gi, int buf) {  // gi in [0, 2*NG): conv gi / NG, taps (gi % NG) * TG + t
@@ -159,12 +163,13 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       if constexpr ((ABL & 1) != 0) return;
       typedef __attribute__((address_space(3))) void lds_void;
       typedef const __attribute__((address_space(1))) void g_void;
+      const bf16_t* Wk = W + k0 * (C * C);  // uniform
 #pragma unroll
       for (int s = 0; s < GLN; ++s) {
         // taps past K (last group, K % TG != 0) re-read tap K - 1; their MFMAs are skipped
-        const int kk = min(k0 + gl_src[s] / (C * C), K - 1);
-        const bf16_t* src = W + (int64_t)kk * C * C + (gl_src[s] % (C * C));
-        bf16_t* dst = wls + buf * TG * TAPE + (s * NW + wave) * 64 * 8;
+        const int dt = TG == 1 ? 0 : min(gl_t[s], K - 1 - k0);
+        const bf16_t* src = Wk + (dt * (C * C) + gl_off[s]);
+        bf16_t* dst = wls + buf * TG * TAPE + (s * NW + wave_u) * 64 * 8;
         __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
       }
       return;
