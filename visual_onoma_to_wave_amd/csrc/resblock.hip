@@ -77,8 +77,8 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
 // streamed weight tap feeds twice the MFMAs.  Costs two barriers per tile and a window store
 // after P2 instead of during it.
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false>
-__global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
+          bool IP = false, bool HP = false>
+__global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {  // >= 2 waves per SIMD
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
   constexpr int NC = C / 32;              // 32-channel planes
@@ -103,7 +103,9 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);  // [NC][win_rows][32]
   bf16_t* t1 = IP ? win : win + NC * win_rows * 32;   // [NC][T1R][32]
   bf16_t* wls = IP ? win + NC * max(win_rows, T1R) * 32 : t1 + NC * T1R * 32;  // RES: [2][K] taps; else [2 bufs][TG] taps
-  float* sbias = reinterpret_cast<float*>(wls + (RES ? 2 * K : 2 * TG) * TAPE);  // [b1 | b2]
+  static_assert(!HP || (GL && TG == 1 && !RES && NC % 2 == 0), "half-tap groups: LDS-DMA streaming, one tap");
+  constexpr int GE = HP ? TAPE / 2 : TG * TAPE;  // LDS elements per streamed group buffer
+  float* sbias = reinterpret_cast<float*>(wls + (RES ? 2 * K * TAPE : 2 * GE));  // [b1 | b2]
   bf16_t* spare = reinterpret_cast<bf16_t*>(sbias + 2 * C);  // 16 B sink for idle staging slots
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -119,7 +121,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   if (tile >= tile_end) return;
 
   // ---- weights
-  const int NG = (K + TG - 1) / TG;  // streamed groups per phase
+  const int NG = HP ? 2 * K : (K + TG - 1) / TG;  // streamed groups per phase (HP: half taps)
   int wg_g[GV], wg_l[GV], wg_t[GV];
 #pragma unroll
   for (int s = 0; s < GV; ++s) {
@@ -138,8 +140,9 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
   // instruction, lane-linear in LDS): no VGPR staging and no ds_write (the ablation without
   // weight stores ran 25-30 % faster).  The XOR swizzle moves to the source address: LDS
   // slot p of a group holds (tap t, plane pl, row co, chunk q' = q ^ swz(co)).
-  constexpr int GLN = GL ? (TG * TAPV) / (64 * NW) : 1;  // DMA instructions per wave per group
-  static_assert(!GL || (TG * TAPV) % (64 * NW) == 0, "glds: group must split into whole wave-KiB");
+  constexpr int GVEC = HP ? TAPV / 2 : TG * TAPV;     // 16-byte vectors per streamed group
+  constexpr int GLN = GL ? GVEC / (64 * NW) : 1;  // DMA instructions per wave per group
+  static_assert(!GL || GVEC % (64 * NW) == 0, "glds: group must split into whole wave-KiB");
   // per-lane source: tap within the group (gl_t) and 32-bit element offset within a tap (gl_off);
   // the group's tap base is wave-uniform (SGPRs), the LDS destination too (m0 from an SGPR)
   int gl_t[GLN], gl_off[GLN];
@@ -148,8 +151,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 #pragma unroll
     for (int s = 0; s < GLN; ++s) {
       const int p = (s * NW + wave) * 64 + lane;
-      const int t = p / TAPV, vv = p - t * TAPV;
-      const int pl = vv / (C * 4), rem = vv - pl * C * 4;
+      const int t = HP ? 0 : p / TAPV, vv = p - t * TAPV;
+      const int pl = vv / (C * 4), rem = vv - pl * C * 4;  // HP: plane within the half tap
       const int co = rem >> 2, q = (rem & 3) ^ ((co >> (SHW - 1)) & 2);
       gl_t[s] = t;
       gl_off[s] = co * C + pl * 32 + q * 8;
@@ -163,13 +166,15 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
       if constexpr ((ABL & 1) != 0) return;
       typedef __attribute__((address_space(3))) void lds_void;
       typedef const __attribute__((address_space(1))) void g_void;
-      const bf16_t* Wk = W + k0 * (C * C);  // uniform
+      // HP: group gi is half (gi & 1) of tap gi / 2 -- planes [half * NC/2, (half + 1) * NC/2)
+      const bf16_t* Wk = HP ? W + ((gi - ph * NG) >> 1) * (C * C) + ((gi - ph * NG) & 1) * (NC / 2) * 32
+                            : W + k0 * (C * C);  // uniform
 #pragma unroll
       for (int s = 0; s < GLN; ++s) {
         // taps past K (last group, K % TG != 0) re-read tap K - 1; their MFMAs are skipped
         const int dt = TG == 1 ? 0 : min(gl_t[s], K - 1 - k0);
         const bf16_t* src = Wk + (dt * (C * C) + gl_off[s]);
-        bf16_t* dst = wls + buf * TG * TAPE + (s * NW + wave_u) * 64 * 8;
+        bf16_t* dst = wls + buf * GE + (s * NW + wave_u) * 64 * 8;
         __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
       }
       return;
@@ -310,8 +315,8 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     };
     // IP keeps the window prefetch live through P2, so its residual rows are fetched one
     // group (a tap: >= 1k MFMA cycles) before the epilogue instead of a whole tile ahead
+    if constexpr (!IP) load_res();  // IP: one group before the epilogue; HP: in the epilogue
     if constexpr (!IP) {
-      load_res();
       load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
     }
 
@@ -370,21 +375,25 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
         const int gi = ph * NG + g;
         const bool more = has_next || gi + 1 < 2 * NG;
         if constexpr (IP) {  // next window: fetched at P2 start, stored after P2 (registers
-          if (gi == NG) load_win(has_next ? tile + 1 : tile);  // are not live during P1)
-          if (gi + 1 == 2 * NG) load_res();
+          if (!HP && gi == NG) load_win(has_next ? tile + 1 : tile);  // are not live during P1;
+                                                                      // HP: fetched after P2)
+          if (!HP && gi + 1 == 2 * NG) load_res();
         }
         load_group(gi + 1 == 2 * NG ? 0 : gi + 1, (gcount + 1) & 1);  // unconditional; stored only if needed
-        const bf16_t* wb = wls + (gcount & 1) * TG * TAPE;
+        const bf16_t* wb = wls + (gcount & 1) * GE;
         const bf16_t* src = ph ? t1 : win;
         const int plane = ph ? T1R * 32 : win_rows * 32;
         const int step = ph ? 1 : dil;
         // software-pipelined over the group's TG x NC (tap, plane) steps: the fragments of step
         // st + 1 are read from LDS before the MFMAs of step st (two named register sets)
-        constexpr int S = TG * NC;
+        constexpr int S = HP ? NC / 2 : TG * NC;
         if constexpr (!SB) {  // plain steps: hipcc schedules the reads (fewer live fragments)
 #pragma unroll
           for (int st = 0; st < S; ++st) {
-            if (TG == 1 || g * TG + st / NC < K) {
+            if constexpr (HP) {  // half tap g & 1 of tap g >> 1: planes (g & 1) * S + st
+              const int c = (g & 1) * S + st;
+              tap(wb + st * C * 32, src + c * plane, brow0 + (g >> 1) * step);
+            } else if (TG == 1 || g * TG + st / NC < K) {
               const int t = st / NC, c = st - t * NC;
               tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + (g * TG + t) * step);
             }
@@ -433,6 +442,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
+    if constexpr (HP) load_res();
     if constexpr (IP) {  // IP: the MRF accumulator rows are read here (registers are short)
       if (a.acc) {
 #pragma unroll
@@ -465,6 +475,9 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
     }
     if constexpr (RES) __syncthreads();
     if constexpr (IP) {  // P2's T1 reads ended at the last group barrier
+      if constexpr (HP) {  // two workgroups per CU: the other one covers this load's latency
+        if (has_next) load_win(tile + 1);
+      }
       if (has_next) store_win();
       __syncthreads();
     }
@@ -472,7 +485,7 @@ __global__ void __launch_bounds__(WC * WT * 64) mrf_pair_kernel(PairArgs a) {
 }
 
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false>
+          bool IP = false, bool HP = false>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -480,7 +493,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
   const int BT = R1 - 2 * h2;
   a.tiles_per_b = (a.T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
-  const size_t wtaps = RES ? 2 * (size_t)a.K : 2 * (size_t)TG;
+  const size_t wtaps = RES ? 2 * (size_t)a.K : (HP ? 1 : 2 * (size_t)TG);  // HP: two half-tap buffers
   const size_t act_rows = IP ? std::max<size_t>(R1 + 2 * h1, R1 + 16) : (size_t)(R1 + 2 * h1) + (R1 + 16);
   const size_t lds = (act_rows + wtaps * C) * (C / 32) * 32 * sizeof(bf16_t) +
                      2 * C * sizeof(float) + 16;
@@ -488,7 +501,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP, HP>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -541,6 +554,9 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
     if (cfg == 2) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
     if (cfg == 3) return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
+    // two 4-wave workgroups per CU (79 KB LDS each: 128-row in-place tiles, half-tap weight
+    // buffers), 64 x 64-row wave tiles: one workgroup's epilogue overlaps the other's MFMAs
+    if (cfg == 4) return pair_launch<128, 2, 2, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
     // SIMD (12 waves, 2 x 6) 15 % slower.
