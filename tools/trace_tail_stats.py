@@ -14,8 +14,11 @@ from collections import defaultdict
 def main(path, marker="stft_mel_kernel", occ=6, steps=3):
     occ, steps = int(occ), int(steps)
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-    start = idx[-occ] if len(idx) >= occ else 0
+    if marker.startswith("FRACTION:"):  # the last fraction of all dispatches (steady-state steps)
+        start = int(len(rows) * (1.0 - float(marker.split(":")[1])))
+    else:
+        idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+        start = idx[-occ] if len(idx) >= occ else 0
     tail = rows[start:]
     agg = defaultdict(lambda: [0, 0.0])
     for r in tail:
