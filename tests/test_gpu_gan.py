@@ -305,3 +305,23 @@ def test_convtranspose_wgrad_vs_torch(Ci, Co, u, T, dt, tol):
     got = ops.conv1d_wgrad(x.transpose(1, 2).contiguous().cuda().to(dt), gy.transpose(1, 2).contiguous().cuda().to(dt),
                            K, S=u, pad=p, pre_a=0.1, transposed=True)
     assert rel_l2(got.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
+    (2, 1000, 128, 128, 41, 2, 4, 20), (2, 777, 128, 256, 41, 2, 16, 20), (3, 300, 256, 512, 41, 4, 16, 20),
+    (2, 64, 1024, 1024, 41, 1, 16, 20), (4, 2731, 32, 128, 5, 3, 1, 2), (6, 100, 512, 1024, 5, 3, 1, 2),
+    (2, 13, 128, 256, 41, 4, 16, 20)])
+def test_strided_grouped_dgrad_vs_torch(B, T, Ci, Co, K, s, g, pad, dt, tol):
+    """gan_ops._dgrad (per-phase grouped convs over dY) against torch's conv1d input gradient."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    gen = torch.Generator().manual_seed(T + Co + s)
+    x = torch.randn(B, T, Ci, generator=gen).to(dt)
+    w = torch.randn(Co, Ci // g, K, generator=gen) / (Ci // g * K) ** 0.5
+    T_out = (T + 2 * pad - K) // s + 1
+    gy = torch.randn(B, T_out, Co, generator=gen).to(dt).float()
+    ref = torch.nn.grad.conv1d_input((B, Ci, T), w, gy.transpose(1, 2), stride=s, padding=pad, groups=g)
+    spec = G.ConvSpec(K=K, pad=pad, stride=s, groups=g)
+    got = G._dgrad(gy.cuda().to(dt), w.cuda(), spec, x.cuda(), dt)
+    assert got.shape == (B, T, Ci)
+    assert rel_l2(got.float().cpu(), ref.transpose(1, 2)) < tol

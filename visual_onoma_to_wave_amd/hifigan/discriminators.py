@@ -95,10 +95,10 @@ class DiscriminatorP(_DiscBase):
         specs, post = self._specs()
         fmap = []
         for m, sp in zip(self.convs, specs):
-            x = G.conv(x, effective_weight(m)[..., 0], m.bias, sp, cdt)
+            x = G.conv(x, effective_weight(m)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, effective_weight(m)[..., 0], m.bias, post, cdt)
+        y = G.conv(x, effective_weight(m)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap
@@ -145,10 +145,10 @@ class DiscriminatorS(_DiscBase):
         for m, (ci, co, k, s, g, p) in zip(self.convs, self.cfg):
             sp = G.ConvSpec(K=k, pad=p, stride=s, groups=g, post="lrelu", post_slope=LRELU_SLOPE,
                             ci_pad=8 if ci == 1 else None)
-            x = G.conv(x, effective_weight(m), m.bias, sp, cdt)
+            x = G.conv(x, effective_weight(m), m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, effective_weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt)
+        y = G.conv(x, effective_weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap

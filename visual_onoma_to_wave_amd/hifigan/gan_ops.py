@@ -12,13 +12,16 @@ Backward, per op:
   * loss gradients: ``vo_gan_reduce_grad``;
   * weight / bias gradients of dense convs (generator, MPD, conv_post): ``vo_conv1d_wgrad``
     (MFMA over transposed LDS reads) and ``vo_colsum``;
-  * the grouped MSD convs' weight gradients, the input gradient of strided / grouped
-    discriminator convs and the mel-loss STFT: PyTorch-ROCm (MIOpen ``convolution_backward``,
-    ``torch.stft``) -- the fallback SURVEY.md 8(b) sanctions for training backward.
+  * input gradient of strided / grouped discriminator convs: the conv kernel once per stride
+    phase (taps of the phase reversed, channel roles swapped, rows interleaved) -- ``_dgrad``;
+  * the grouped MSD convs' weight gradients and the mel-loss STFT: PyTorch-ROCm (MIOpen
+    ``convolution_backward``, ``torch.stft``) -- the fallback SURVEY.md 8(b) sanctions.
 """
 
 from dataclasses import dataclass
 from typing import Optional, Tuple
+
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -73,8 +76,34 @@ def out_len(spec, T_in):
     return (T_in + 2 * spec.pad - spec.dil * (spec.K - 1) - 1) // spec.stride + 1
 
 
-def _conv_fwd(x, w, b, res1, res2, spec, cdt):
-    wp = _pack(w, spec, cdt)
+_PACKS = weakref.WeakKeyDictionary()  # module -> {(spec, dtype, kind...): (versions, packed weight)}
+
+
+def weight_key(m):
+    """Cache key of a conv module's effective weight: the module and its parameters' version
+    counters (bumped by every optimizer step / load_state_dict).  None (no caching) for
+    spectral-normed convs, whose weight moves with each training-mode power iteration."""
+    if hasattr(m, "weight_g"):
+        return (m, m.weight_v._version, m.weight_g._version)
+    if hasattr(m, "weight_orig"):
+        return None
+    return (m, m.weight._version)
+
+
+def _cached(wkey, tag, build):
+    if wkey is None:
+        return build()
+    per = _PACKS.setdefault(wkey[0], {})
+    hit = per.get(tag)
+    if hit is not None and hit[0] == wkey[1:]:
+        return hit[1]
+    val = build()
+    per[tag] = (wkey[1:], val)
+    return val
+
+
+def _conv_fwd(x, w, b, res1, res2, spec, cdt, wkey=None):
+    wp = _cached(wkey, (spec, cdt, "fwd"), lambda: _pack(w, spec, cdt))
     if spec.transposed is not None:
         s, p = spec.transposed
         cout = w.shape[1]
@@ -89,6 +118,52 @@ def _conv_fwd(x, w, b, res1, res2, spec, cdt):
                       pre_slope=spec.pre_slope or 0.0, post_act=_POST[spec.post], post_slope=spec.post_slope,
                       res1=res1, res2=res2, out_scale=spec.out_scale, out_dtype=x.dtype, compute_dtype=cdt,
                       stride=spec.stride, groups=spec.groups)
+
+
+def _dgrad(gz, w, spec, x, cdt, wkey=None):
+    """Input gradient of a strided and/or grouped conv (dil 1) on the HIP conv kernel, by phase:
+    input row i = S m + r receives taps k = k_r + S j (k_r = (r + pad) mod S) from output rows
+    m + c_r - j, so each residue r is a stride-1 grouped conv over dY with those taps reversed and
+    the channel roles swapped, written to rows r, r + S, ... of dX (row-strided output view)."""
+    S, K, pad, g = spec.stride, spec.K, spec.pad, spec.groups
+    if spec.dil != 1:
+        raise NotImplementedError("strided / grouped input gradient with dilation")
+    Co, cig, _ = w.shape
+    cog, Ci = Co // g, cig * g
+    # dgrad conv weight (Ci, Co / g, K): per group the (cog x cig) blocks transposed
+    ci_out = x.shape[-1]  # >= Ci (1-channel inputs padded to 8)
+    wt_box = []
+
+    def wt_get():
+        if not wt_box:
+            wt = w.detach().float().reshape(g, cog, cig, K).transpose(1, 2).reshape(Ci, cog, K)
+            if ci_out > Ci:
+                wt = torch.cat([wt, wt.new_zeros((ci_out - Ci, cog, K))])
+            wt_box.append(wt)
+        return wt_box[0]
+    gzp = _pad_channels(gz.to(cdt))
+    co_in = gzp.shape[-1]  # >= Co (Co = 1 padded to 8); extra channels multiply zero weights
+    B, T_in = x.shape[0], x.shape[1]
+    out = torch.empty((B, T_in, ci_out), dtype=x.dtype, device=x.device)
+    for r in range(S):
+        k_r = (r + pad) % S
+        taps = list(range(k_r, K, S))
+        rows = (T_in - r + S - 1) // S
+        if rows <= 0:
+            continue
+        view = out[:, r::S]
+        if not taps:
+            view.zero_()
+            continue
+        J = len(taps)
+        c_r = (r + pad - k_r) // S
+        def build(taps=taps):
+            wsel = wt_get()[:, :, taps[::-1]].contiguous()  # tap t <- k_r + S (J - 1 - t)
+            return ops.pack_grouped_weight(wsel, cdt, groups=g if ci_out == Ci else 1, ci_pad=co_in)
+        wp = _cached(wkey, (spec, cdt, "dgrad", r, ci_out, co_in), build)
+        ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,
+                   groups=g if ci_out == Ci else 1)
+    return out
 
 
 def _pad_channels(t, mult=8):
@@ -107,11 +182,11 @@ class ConvFn(torch.autograd.Function):
     """y = (post(conv(pre(x), w) + b) + res1) * out_scale + res2, channels-last."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res1, res2, spec, cdt):
+    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None):
         if spec.post is not None and (res1 is not None or res2 is not None):
             raise ValueError("ConvFn: post-activation with residual inputs is not differentiable here")
-        y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt)
-        ctx.spec, ctx.cdt = spec, cdt
+        y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt, wkey)
+        ctx.spec, ctx.cdt, ctx.wkey = spec, cdt, wkey
         ctx.has = (res1 is not None, res2 is not None)
         ctx.save_for_backward(x, w, y if spec.post is not None else None)
         return y
@@ -141,6 +216,11 @@ class ConvFn(torch.autograd.Function):
             ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
                             pad=(spec.K - 1) * spec.dil - spec.pad, T_out=x.shape[1], out_dtype=x.dtype,
                             compute_dtype=cdt)
+            need_x = False
+        elif need_x and spec.transposed is None and spec.dil == 1:
+            ga = _dgrad(gz, w, spec, x, cdt, ctx.wkey)
+            if ga.shape[-1] != ci:
+                ga = ga[..., :ci]
             need_x = False
         elif need_x and spec.transposed is not None:
             s, p = spec.transposed
@@ -191,11 +271,12 @@ class ConvFn(torch.autograd.Function):
             gw = None
         if not ctx.needs_input_grad[2]:
             gb = None
-        return gx, gw, gb, g_res1, g_res2, None, None
+        return gx, gw, gb, g_res1, g_res2, None, None, None
 
 
-def conv(x, w, b, spec, cdt, res1=None, res2=None):
-    return ConvFn.apply(x, w, b, res1, res2, spec, cdt)
+def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None):
+    """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged."""
+    return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey)
 
 
 class PeriodFoldFn(torch.autograd.Function):

@@ -179,11 +179,12 @@ class Generator(HipModule):
         def wgt(m):
             return torch._weight_norm(m.weight_v, m.weight_g, 0) if hasattr(m, "weight_g") else m.weight
 
-        x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, G.ConvSpec(K=7, pad=3), dt)
+        x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, G.ConvSpec(K=7, pad=3), dt,
+                   wkey=G.weight_key(self.conv_pre))
         for i, (u, k) in enumerate(zip(self.h.upsample_rates, self.h.upsample_kernel_sizes)):
             m = self.ups[i]
             x = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=k, pad=(k - u) // 2, pre_slope=LRELU_SLOPE,
-                                                     transposed=(u, (k - u) // 2)), dt)
+                                                     transposed=(u, (k - u) // 2)), dt, wkey=G.weight_key(m))
             xs = None
             for j in range(self.num_kernels):
                 rb = self.resblocks[i * self.num_kernels + j]
@@ -192,14 +193,17 @@ class Generator(HipModule):
                 for n, (d, c1, c2) in enumerate(zip(rb.dilation, rb.convs1, rb.convs2)):
                     t = G.conv(cur, wgt(c1), c1.bias, G.ConvSpec(K=kk, pad=get_padding(kk, d), dil=d,
                                                                  pre_slope=LRELU_SLOPE, post="lrelu",
-                                                                 post_slope=LRELU_SLOPE), dt)
+                                                                 post_slope=LRELU_SLOPE), dt,
+                               wkey=G.weight_key(c1))
                     last = n == len(rb.dilation) - 1
                     sp = G.ConvSpec(K=kk, pad=get_padding(kk, 1), out_scale=1.0 / self.num_kernels if last else 1.0)
-                    cur = G.conv(t, wgt(c2), c2.bias, sp, dt, res1=cur, res2=xs if last else None)
+                    cur = G.conv(t, wgt(c2), c2.bias, sp, dt, res1=cur, res2=xs if last else None,
+                                 wkey=G.weight_key(c2))
                 xs = cur
             x = xs
         m = self.conv_post
-        y = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=7, pad=3, pre_slope=0.01, post="tanh", co_pad=4), dt)
+        y = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=7, pad=3, pre_slope=0.01, post="tanh", co_pad=4), dt,
+                   wkey=G.weight_key(m))
         return y[..., 0].float()
 
     def forward(self, x):

@@ -81,7 +81,14 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
         out = torch.empty(shape, dtype=out_dtype, device=x.device)
     if out.dim() == 2:
         out = out.unsqueeze(0)
-    _contig(out, "out")
+    if transposed is None and not out.is_contiguous():
+        # row-strided output view (phase-interleaved rows of a strided conv's input gradient):
+        # rows ldy elements apart, channels contiguous; no residuals on such views
+        if out.stride(2) != 1 or out.shape[2] != Co or res1 is not None or res2 is not None:
+            raise ValueError("conv1d: a non-contiguous out must be a row-strided (B, T, Co) view")
+        ldy = out.stride(1)
+    else:
+        _contig(out, "out")
     if res1 is not None and (res1.shape != out.shape or res1.dtype != out.dtype):
         raise ValueError("conv1d: res1 must match the output")
     if res2 is not None and (res2.shape != out.shape or res2.dtype != out.dtype):
