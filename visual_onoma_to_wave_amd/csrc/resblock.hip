@@ -77,7 +77,7 @@ __device__ __forceinline__ void unpack8(u32x4 u, float (&f)[8]) {
 // streamed weight tap feeds twice the MFMAs.  Costs two barriers per tile and a window store
 // after P2 instead of during it.
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false, bool HP = false>
+          bool IP = false, bool HP = false, bool LATE = HP>
 __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {  // >= 2 waves per SIMD
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -104,6 +104,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
   bf16_t* t1 = IP ? win : win + NC * win_rows * 32;   // [NC][T1R][32]
   bf16_t* wls = IP ? win + NC * max(win_rows, T1R) * 32 : t1 + NC * T1R * 32;  // RES: [2][K] taps; else [2 bufs][TG] taps
   static_assert(!HP || (GL && TG == 1 && !RES && NC % 2 == 0), "half-tap groups: LDS-DMA streaming, one tap");
+  static_assert(!(RES && IP) || LATE, "resident weights in place: the next window is fetched after P2");
   constexpr int GE = HP ? TAPE / 2 : TG * TAPE;  // LDS elements per streamed group buffer
   float* sbias = reinterpret_cast<float*>(wls + (RES ? 2 * K * TAPE : 2 * GE));  // [b1 | b2]
   bf16_t* spare = reinterpret_cast<bf16_t*>(sbias + 2 * C);  // 16 B sink for idle staging slots
@@ -363,9 +364,15 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     if constexpr (RES) {
       for (int c = 0; c < NC; ++c)
         for (int k = 0; k < K; ++k) tap(wls + k * TAPE + c * C * 32, win + c * win_rows * 32, brow0 + k * dil);
-      p1_epilogue();
-      __syncthreads();
-      if (has_next) store_win();
+      if constexpr (IP) {  // T1 overwrites the window: every wave must be past its P1 reads
+        __syncthreads();
+        p1_epilogue();
+        __syncthreads();
+      } else {
+        p1_epilogue();
+        __syncthreads();
+        if (has_next) store_win();
+      }
       const bf16_t* wb = wls + K * TAPE;
       for (int c = 0; c < NC; ++c)
         for (int k = 0; k < K; ++k) tap(wb + k * TAPE + c * C * 32, t1 + c * T1R * 32, brow0 + k);
@@ -375,9 +382,9 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
         const int gi = ph * NG + g;
         const bool more = has_next || gi + 1 < 2 * NG;
         if constexpr (IP) {  // next window: fetched at P2 start, stored after P2 (registers
-          if (!HP && gi == NG) load_win(has_next ? tile + 1 : tile);  // are not live during P1;
-                                                                      // HP: fetched after P2)
-          if (!HP && gi + 1 == 2 * NG) load_res();
+          if (!LATE && gi == NG) load_win(has_next ? tile + 1 : tile);  // are not live during P1;
+                                                                        // LATE: fetched after P2)
+          if (!LATE && gi + 1 == 2 * NG) load_res();
         }
         load_group(gi + 1 == 2 * NG ? 0 : gi + 1, (gcount + 1) & 1);  // unconditional; stored only if needed
         const bf16_t* wb = wls + (gcount & 1) * GE;
@@ -442,7 +449,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
-    if constexpr (HP) load_res();
+    if constexpr (LATE) load_res();
     if constexpr (IP) {  // IP: the MRF accumulator rows are read here (registers are short)
       if (a.acc) {
 #pragma unroll
@@ -475,7 +482,8 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     }
     if constexpr (RES) __syncthreads();
     if constexpr (IP) {  // P2's T1 reads ended at the last group barrier
-      if constexpr (HP) {  // two workgroups per CU: the other one covers this load's latency
+      if constexpr (LATE) {  // no window registers live in P2 (HP: the other workgroup of the CU
+                             // covers this load's latency)
         if (has_next) load_win(tile + 1);
       }
       if (has_next) store_win();
@@ -485,7 +493,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
 }
 
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false, bool HP = false>
+          bool IP = false, bool HP = false, bool LATE = HP>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -501,7 +509,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP, HP>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP, HP, LATE>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -542,8 +550,15 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   const int cfg = vo_tune_get("pair_cfg");
   if (C == 32) {
     if (cfg == 3) return pair_launch<32, 1, 4, 8, true, 1>(a, B, st);
-    const bool small = cfg == 0 ? K <= 7 : cfg == 1;
-    return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
+    if (cfg == 4) return pair_launch<32, 1, 8, 8, true, 1, 0, 0, false, false, true, false, true>(a, B, st);
+    if (cfg == 6) return pair_launch<32, 1, 8, 6, true, 1, 0, 0, false, false, true, false, true>(a, B, st);
+    if (cfg == 1 || cfg == 2 || cfg == 9) {  // the previous tilings (9: k <= 7 -> 256 rows, else 512)
+      const bool small = cfg == 9 ? K <= 7 : cfg == 1;
+      return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
+    }
+    // 512-row in-place tiles, window / residual fetched after P2: k = 11 -13 %, k = 7 -3 %
+    // (k = 3 is HBM-bound at ~5 TB/s either way; tools/ab_sb.py pair32 9 5)
+    return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true>(a, B, st);
   }
   if (C == 128) {
     // 2 x 4 waves of 64 channels (2 waves/SIMD), weights by LDS-DMA.  k = 3: 128-row tiles;
@@ -557,16 +572,34 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // two 4-wave workgroups per CU (79 KB LDS each: 128-row in-place tiles, half-tap weight
     // buffers), 64 x 64-row wave tiles: one workgroup's epilogue overlaps the other's MFMAs
     if (cfg == 4) return pair_launch<128, 2, 2, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
+    // one 8-wave workgroup per CU with half-tap buffers: 256- / 384-row in-place tiles halve the
+    // weight stream per MFMA of the 192-row kernel (384 rows spill)
+    if (cfg == 6) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
+    if (cfg == 7) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
     // SIMD (12 waves, 2 x 6) 15 % slower.
-    if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
-    return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
+    if (cfg == 9) {  // the previous defaults
+      if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
+      return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
+    }
+    // 256-row in-place tiles, window / residual fetched after P2 (no window registers live in
+    // the MFMA loop): k = 3 with half-tap buffers (-10 %), k >= 7 with whole taps (-4..6 %)
+    // against the 128 / 192-row kernels (tools/ab_sb.py pair 9 6 7)
+    if (K <= 3) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
+    return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
   }
   // C = 64: k = 3 -> both convs resident in LDS; k >= 7 -> 2-tap groups, register staged.
+  // pair_cfg 3 / 4 / 5: 512-row IP + LDS-DMA / 384-row IP + LDS-DMA / 512-row IP (the default)
   // pair_cfg 1 = LDS-DMA weights + pinned fragment pipeline: 7 % faster alone (tools/ab_sb.py)
   // but 15 % slower inside the bench step with the MRF accumulator (tools/bench_ab.sh)
+  if (cfg == 3) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
+  if (cfg == 4) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
+  if (cfg == 5) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
   if (K <= 3 && cfg != 2) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
   if (cfg == 1) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, true, true>(a, B, st);
-  return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);
+  if (cfg == 9) return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);  // the previous default
+  // k >= 7: 512-row in-place tiles, window / residual fetched after P2: -5 % against the
+  // 384-row kernel with T1 beside the window (tools/ab_sb.py pair64 9 5)
+  return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
 }
