@@ -579,6 +579,11 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
     // SIMD (12 waves, 2 x 6) 15 % slower.
+    // timing ablations (garbage results): no window / residual loads -- 0.67 -> 0.56 ms at
+    // k = 11, 0.30 -> 0.21 at k = 3: the chip-wide burst of window loads after P2 (17 MB at
+    // once); fetching the window during the last P2 group instead was 11-20 % slower
+    if (cfg == 16) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, true>(a, B, st);
+    if (cfg == 17) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, false, true>(a, B, st);
     if (cfg == 9) {  // the previous defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
