@@ -278,11 +278,12 @@ def main():
         tag, d = max(ks.items(), key=lambda kv: kv[1]["total_ms"])
         achieved = d["flops_per_launch"] / (d["avg_ms"] * 1e-3) / 1e12
         peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
-        traffic = None
+        pmc = {}  # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_round.sh)
         tf = os.path.join(REPO, "profiles", "traffic_r01.json")
         if os.path.exists(tf):
             with open(tf) as f:
-                traffic = json.load(f).get(tag, {}).get("hbm_bytes_per_launch")
+                pmc = {k: v.get("hbm_bytes_per_launch") for k, v in json.load(f).items()}
+        traffic = pmc.get(tag)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": f"{' + '.join(d['kernels'])} (HiFi-GAN MRF stage {tag[-1]})",
@@ -292,7 +293,11 @@ def main():
                 "all_stages": {k: {"kernel": " + ".join(v["kernels"]), "avg_ms": round(v["avg_ms"], 4),
                                    "launches": v["launches"],
                                    "tflops": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12, 1),
-                                   "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1)}
+                                   "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1),
+                                   # measured HBM bytes (PMC) over this run's launch time: the
+                                   # north star's "HBM roofline on the MRF" for the narrow stages
+                                   "hbm_frac_pmc": (round(pmc[k] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)
+                                                    if pmc.get(k) else None)}
                                for k, v in sorted(ks.items())}}
 
     cpu = None

@@ -65,18 +65,21 @@ def run(kind, C, T, cfgs, key):
         print(line, flush=True)
 
 
-def run_gen(cfgs):
-    """decoder / PostNet / upsampler shapes through the generic bf16 path (gen_cfg)"""
-    B, T = 32, 512
+def run_gen(cfgs, dt=torch.bfloat16, T=512):
+    """decoder / PostNet / upsampler shapes through the generic bf16 path (gen_cfg); with
+    dt=float32, T=12: the glyph encoder / variance predictor shapes"""
+    B = 32
     shapes = [(256, 1024, 9, 1), (1024, 256, 1, 1), (256, 768, 1, 1), (256, 256, 1, 1), (512, 512, 5, 1),
-              (80, 512, 5, 1)]
+              (80, 512, 5, 1)] if T > 16 else [(256, 1024, 9, 1), (1024, 256, 1, 1), (256, 768, 1, 1),
+                                                 (256, 256, 1, 1), (256, 256, 3, 1)]
     for Ci, Co, k, d in shapes:
         torch.manual_seed(k)
-        x = torch.randn(B, T, Ci, device="cuda").to(torch.bfloat16)
-        w = ops.pack_conv_weight(torch.randn(Co, Ci, k, device="cuda") / (Ci * k) ** 0.5, torch.bfloat16)
+        x = torch.randn(B, T, Ci, device="cuda").to(dt)
+        w = ops.pack_conv_weight(torch.randn(Co, Ci, k, device="cuda") / (Ci * k) ** 0.5, dt)
         b = torch.randn(Co, device="cuda") * 0.1
-        y = torch.empty(B, T, Co, device="cuda", dtype=torch.bfloat16)
-        f = lambda: ops.conv1d(x, w, b, Co=Co, K=k, dil=d, pad=d * (k - 1) // 2, out=y)  # noqa: E731
+        y = torch.empty(B, T, Co, device="cuda", dtype=dt)
+        f = lambda: ops.conv1d(x, w, b, Co=Co, K=k, dil=d, pad=d * (k - 1) // 2, out=y,  # noqa: E731
+                               compute_dtype=dt)
         fl = 2.0 * B * T * Ci * Co * k
         errs, best, ref = {}, {}, None
         for cfg in cfgs:
@@ -108,6 +111,8 @@ def main():
         run("pair", 32, 131072, cfgs, b"pair_cfg")
     elif kind == "gen":
         run_gen(cfgs)
+    elif kind == "genf32":
+        run_gen(cfgs, torch.float32, 12)
     else:
         run("conv", 256, 4096, cfgs, b"conv_cfg")
 

@@ -463,7 +463,15 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   const int64_t rows = (int64_t)d->B * d->T_out;
   // short sequences (the glyph encoder / phoneme-level predictors run at T_src ~ 12): one
   // 16- or 32-row time tile, waves spread over output channels
-  if (d->T_out <= 16 && d->Co >= 64) return launch_cfg<TIN, TC, TOUT, 2, 1, 4, 1, 4>(d, st);  // 128 x 16
+  if (d->T_out <= 16 && d->Co >= 64) {
+    // fp32 (glyph encoder, variance predictors at B = 32, T = 12): 32 x 16 tiles, 4x the
+    // workgroups of 128 x 16: FFN w_1 66 -> 51 us, w_2 28 -> 20, predictor k3 20 -> 13
+    // (tools/ab_sb.py genf32 5 3); gen_cfg 2 = 64 x 16, 5 = 128 x 16
+    const int gc = vo_tune_get("gen_cfg");
+    if (gc == 2) return launch_cfg<TIN, TC, TOUT, 1, 1, 4, 1, 4>(d, st);  // 64 x 16
+    if (gc != 5 && sizeof(TC) == 4) return launch_cfg<TIN, TC, TOUT, 1, 1, 2, 1, 4>(d, st);  // 32 x 16
+    return launch_cfg<TIN, TC, TOUT, 2, 1, 4, 1, 4>(d, st);  // 128 x 16
+  }
   if (d->T_out <= 32 && d->Co >= 64) return launch_cfg<TIN, TC, TOUT, 2, 2, 4, 1, 4>(d, st);  // 128 x 32
   if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4, 4>(d, st);   // 32 x 256
   if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
