@@ -272,6 +272,13 @@ int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb,
 int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
                     int N, int K, int S, int dil, int pad, int pre_a, int pre_b, float slope,
                     int dtype, float* dw, void* stream);
+/* Grouped conv (groups > 1): M = C_out / groups and N = C_in / groups per group, lda >= groups*M,
+ * ldb >= groups*N; group g reads A columns [g*M, (g+1)*M), B columns [g*N, (g+1)*N) and writes
+ * dw block g of the (groups*M, N, K) grouped weight.  Replaces MIOpen's grouped weight pass of
+ * the multi-scale discriminator (HiFi-GAN V1 MSD). */
+int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
+                            int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
+                            int pre_b, float slope, int dtype, float* dw, void* stream);
 int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream);
 
 /* ------------------------------------------------------------------ training input pipeline

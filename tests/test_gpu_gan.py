@@ -291,6 +291,25 @@ def test_conv1d_wgrad_vs_torch(B, T, Ci, Co, K, dil, s, pad, pre, dt, tol):
 
 
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
+    (2, 1000, 128, 128, 41, 2, 4, 20), (2, 777, 128, 256, 41, 4, 16, 20), (3, 300, 256, 512, 41, 4, 16, 20),
+    (2, 64, 1024, 1024, 41, 1, 16, 20), (2, 13, 512, 1024, 41, 4, 16, 20), (1, 5, 64, 64, 3, 1, 2, 1)])
+def test_grouped_conv1d_wgrad_vs_torch(B, T, Ci, Co, K, s, g, pad, dt, tol):
+    """vo_conv1d_wgrad_grouped (MSD grouped strided convs) against torch's grouped weight gradient."""
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(T + Co + g)
+    x = torch.randn(B, T, Ci, generator=gen).to(dt).float()
+    T_out = (T + 2 * pad - K) // s + 1
+    gy = torch.randn(B, T_out, Co, generator=gen).to(dt).float()
+    xa = F.leaky_relu(x, 0.1)
+    ref = torch.nn.grad.conv1d_weight(xa.transpose(1, 2), (Co, Ci // g, K), gy.transpose(1, 2), stride=s,
+                                      padding=pad, groups=g)
+    got = ops.conv1d_wgrad(gy.cuda().to(dt), x.cuda().to(dt), K, S=s, pad=pad, pre_b=0.1, groups=g)
+    assert got.shape == (Co, Ci // g, K)
+    assert rel_l2(got.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("Ci,Co,u,T", [(512, 256, 8, 32), (128, 64, 2, 1000), (64, 32, 2, 7)])
 def test_convtranspose_wgrad_vs_torch(Ci, Co, u, T, dt, tol):
     """vo_conv1d_wgrad transposed form (A = lrelu(x), B = dY) against torch's ConvTranspose1d grad."""

@@ -93,6 +93,9 @@ _SIGNATURES = {
                                c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_conv1d_wgrad": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                 c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p]),
+    "vo_conv1d_wgrad_grouped": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p,
+                                        c_void_p]),
     "vo_colsum": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p]),
     "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),

@@ -67,7 +67,7 @@ static const char* const kSymbols[] = {
     "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair", "vo_stft_mel_ex",
     "vo_pack_grouped",   "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
-    "vo_conv1d_wgrad",   "vo_colsum",
+    "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -35,6 +35,8 @@ struct WgradArgs {
   int rows_per_split;
   float* dw;
 };
+// groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
+// and B columns [g N, (g+1) N) and writes its (M, N, K) block of the (groups M, N, K) weight
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
@@ -57,12 +59,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
   const int tiles_n = (p.N + WG_T - 1) / WG_T;
   const int m0 = (blockIdx.y / tiles_n) * WG_T, n0 = (blockIdx.y % tiles_n) * WG_T;
-  const int k = blockIdx.z;
+  const int k = blockIdx.z % p.K, grp = blockIdx.z / p.K;
   const int64_t rows = (int64_t)p.Bn * p.T_A;
   const int64_t r_begin = (int64_t)blockIdx.x * p.rows_per_split;
   const int64_t r_end = min(rows, r_begin + p.rows_per_split);
-  const TC* A = reinterpret_cast<const TC*>(p.a);
-  const TC* Bs = reinterpret_cast<const TC*>(p.bsrc);
+  const TC* A = reinterpret_cast<const TC*>(p.a) + (int64_t)grp * p.M;
+  const TC* Bs = reinterpret_cast<const TC*>(p.bsrc) + (int64_t)grp * p.N;
+  float* dw = p.dw + (int64_t)grp * p.M * p.N * p.K;
   constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
   constexpr int VPR = WG_T / EV;            // vectors per staged row
   constexpr int NV = WG_R * VPR / 256;      // vectors per thread per operand
@@ -178,7 +181,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
-        if (m < p.M && n < p.N) atomicAdd(p.dw + ((int64_t)m * p.N + n) * p.K + k, acc[i][j][e]);
+        if (m < p.M && n < p.N) atomicAdd(dw + ((int64_t)m * p.N + n) * p.K + k, acc[i][j][e]);
       }
 }
 
@@ -216,33 +219,42 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, in
 
 using namespace vo;
 
-extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M, int N,
-                               int K, int S, int dil, int pad, int pre_a, int pre_b, float slope, int dtype, float* dw,
-                               void* stream) {
+extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
+                                       int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
+                                       float slope, int dtype, float* dw, void* stream) {
   VO_CHECK_ARG(a && b && dw, "conv1d_wgrad: null pointer");
-  VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1, "conv1d_wgrad: bad sizes");
+  VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1 && groups >= 1, "conv1d_wgrad: bad sizes");
   const int ev = dtype == VO_BF16 ? 8 : 4;
-  VO_CHECK_ARG(M % ev == 0 && N % ev == 0 && lda % ev == 0 && ldb % ev == 0 && lda >= M && ldb >= N,
-               "conv1d_wgrad: M=%d N=%d (and leading dims) must be multiples of %d", M, N, ev);
+  VO_CHECK_ARG(M % ev == 0 && N % ev == 0 && lda % ev == 0 && ldb % ev == 0 && lda >= (int64_t)groups * M &&
+                   ldb >= (int64_t)groups * N,
+               "conv1d_wgrad: M=%d N=%d (per group, and leading dims) must be multiples of %d", M, N, ev);
   WgradArgs p;
   p.a = a; p.lda = lda; p.T_A = T_A; p.bsrc = b; p.ldb = ldb; p.T_B = T_B;
   p.M = M; p.N = N; p.K = K; p.S = S; p.dil = dil; p.pad = pad; p.Bn = B;
   p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope; p.dw = dw;
+  const int64_t zk = (int64_t)K * groups;
   const int64_t rows = (int64_t)B * T_A;
   const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
   // enough workgroups to fill 256 CUs ~4 deep, at least 4 chunks of 64 rows each
-  int64_t splits = std::max<int64_t>(1, (1024 + (int64_t)tiles * K - 1) / ((int64_t)tiles * K));
+  int64_t splits = std::max<int64_t>(1, (1024 + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
   p.rows_per_split = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
   splits = (rows + p.rows_per_split - 1) / p.rows_per_split;
-  VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && K < 65536, "conv1d_wgrad: grid too large");
+  VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)K);
+  dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)zk);
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M, int N,
+                               int K, int S, int dil, int pad, int pre_a, int pre_b, float slope, int dtype, float* dw,
+                               void* stream) {
+  return vo_conv1d_wgrad_grouped(a, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, 1, pre_a, pre_b, slope, dtype, dw,
+                                 stream);
 }
 
 extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream) {

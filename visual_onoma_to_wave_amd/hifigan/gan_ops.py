@@ -10,12 +10,13 @@ Backward, per op:
     re-packed taps-reversed / channels-swapped (as in C4); of a polyphase ConvTranspose1d:
     the strided conv kernel (dX = conv1d(dY, W, stride s, pad p));
   * loss gradients: ``vo_gan_reduce_grad``;
-  * weight / bias gradients of dense convs (generator, MPD, conv_post): ``vo_conv1d_wgrad``
-    (MFMA over transposed LDS reads) and ``vo_colsum``;
+  * weight / bias gradients of dense and grouped convs (generator, MPD, MSD, conv_post):
+    ``vo_conv1d_wgrad[_grouped]`` (MFMA over transposed LDS reads) and ``vo_colsum``;
   * input gradient of strided / grouped discriminator convs: the conv kernel once per stride
     phase (taps of the phase reversed, channel roles swapped, rows interleaved) -- ``_dgrad``;
-  * the grouped MSD convs' weight gradients and the mel-loss STFT: PyTorch-ROCm (MIOpen
-    ``convolution_backward``, ``torch.stft``) -- the fallback SURVEY.md 8(b) sanctions.
+  * the mel-loss STFT backward: PyTorch-ROCm (``torch.stft``), and MIOpen
+    ``convolution_backward`` only for layouts none of the above covers (none in HiFi-GAN V1)
+    -- the fallback SURVEY.md 8(b) sanctions.
 """
 
 from dataclasses import dataclass
@@ -229,8 +230,11 @@ class ConvFn(torch.autograd.Function):
             ga = ops.conv1d(gz.to(cdt), wc, None, Co=w.shape[0], K=spec.K, pad=p, stride=s, T_out=x.shape[1],
                             out_dtype=x.dtype, compute_dtype=cdt)
             need_x = False
-        if (need_w or need_b) and spec.groups == 1:
-            # weight / bias gradient on MFMA (vo_conv1d_wgrad, vo_colsum)
+        g = spec.groups
+        grouped_ok = g == 1 or (spec.transposed is None and x.shape[-1] == ci and (ci // g) % 8 == 0
+                                and (w.shape[0] // g) % 8 == 0)
+        if (need_w or need_b) and grouped_ok:
+            # weight / bias gradient on MFMA (vo_conv1d_wgrad[_grouped], vo_colsum)
             gzc = _pad_channels(gz.to(x.dtype))
             if need_w:
                 if spec.transposed is not None:
@@ -239,8 +243,8 @@ class ConvFn(torch.autograd.Function):
                                           transposed=True)
                     gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
                 else:
-                    dw = ops.conv1d_wgrad(gzc, _pad_channels(x), spec.K, S=spec.stride, dil=spec.dil, pad=spec.pad,
-                                          pre_b=spec.pre_slope)
+                    dw = ops.conv1d_wgrad(gzc, _pad_channels(x) if g == 1 else x, spec.K, S=spec.stride,
+                                          dil=spec.dil, pad=spec.pad, pre_b=spec.pre_slope, groups=g)
                     gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
             if need_b:
                 gb = ops.colsum(gz.contiguous())[: w.shape[1] if spec.transposed is not None else w.shape[0]]

@@ -548,23 +548,27 @@ def char_features(energy, fstats, durations, n_bins):
 
 # ----------------------------------------------------------------------------- training backward
 
-def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False):
+def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1):
     """Weight gradient on MFMA (vo_conv1d_wgrad).  Conv1d: a = dY (B, T_out, Co), b = x (B, T_in, Ci)
-    -> dW (Co, Ci, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY (B, T_up, Co)
-    -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand (None = identity)."""
+    -> dW (Co, Ci / groups, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY
+    (B, T_up, Co) -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand
+    (None = identity)."""
     _contig(a, "a")
     _contig(b, "b")
     if a.dtype != b.dtype:
         raise TypeError("conv1d_wgrad: operand dtypes differ")
     B, T_A, M = a.shape
     _, T_B, N = b.shape
-    dw = torch.zeros((M, N, K), dtype=torch.float32, device=a.device)
+    if M % groups or N % groups:
+        raise ValueError(f"conv1d_wgrad: channels {M} / {N} not divisible by groups {groups}")
+    dw = torch.zeros((M, N // groups, K), dtype=torch.float32, device=a.device)
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
-    _lib.check(_lib.lib().vo_conv1d_wgrad(_ptr(a), M, T_A, _ptr(b), N, T_B, B, M, N, K, S, dil, pad,
-                                          int(pre_a is not None), int(pre_b is not None), float(slope),
-                                          vo_dtype(a), _ptr(dw), _stream(a)), "vo_conv1d_wgrad")
+    _lib.check(_lib.lib().vo_conv1d_wgrad_grouped(_ptr(a), M, T_A, _ptr(b), N, T_B, B, M // groups, N // groups, K,
+                                                  S, dil, pad, groups, int(pre_a is not None),
+                                                  int(pre_b is not None), float(slope), vo_dtype(a), _ptr(dw),
+                                                  _stream(a)), "vo_conv1d_wgrad")
     return dw
 
 
