@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="gan mode: eager steps instead of one HIP graph")
     ap.add_argument("--mode", default="infer", choices=["infer", "train", "gan"],
                     help="infer: end-to-end synthesis (headline); train: C4 training step (DDP); "
                          "gan: C5 HiFi-GAN training step (DDP)")
@@ -118,7 +119,9 @@ def bench_gan(a, dev, rank, world, dist):
     load_into(g, hifigan_arrays())
     g = g.to(dev)
     torch.manual_seed(1234)  # identical discriminator init on every rank (broadcast anyway)
-    tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev)
+    graphed = dist is None and not a.no_graph  # one process: the whole step as a HIP graph replay
+    tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev, graphed=graphed)
+    run = tr.step_graphed if graphed else tr.step
     tr.set_compute_dtype(torch.float32 if a.precision == "fp32" else torch.bfloat16)
     B, seg = a.batch, h.segment_size
     gen = torch.Generator().manual_seed(99 + rank)
@@ -129,13 +132,13 @@ def bench_gan(a, dev, rank, world, dist):
         x = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin, h.fmax).to(dev).mel(y)
     x = x.transpose(1, 2).contiguous()  # (B, 32, 80) channels-last generator input
     for _ in range(a.warmup):
-        tr.step(x, y)
+        run(x, y)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        losses = tr.step(x, y)
+        losses = run(x, y)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -153,6 +156,7 @@ def bench_gan(a, dev, rank, world, dist):
             "vs_baseline": None, "dtype": "bf16" if a.precision != "fp32" else "f32",
             "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
             "losses": {k: round(float(v), 4) for k, v in losses.items()},
+            "hip_graph": graphed,
             "config": {"workload": "C5 HiFi-GAN V1 train step", "per_gpu_batch": B, "global_batch": B * world,
                        "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D)"}}))
 

@@ -263,7 +263,8 @@ int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb,
 /* ------------------------------------------------------------------ training backward
  * Weight gradient of a channels-last conv on MFMA (replaces the MIOpen weight pass of the
  * training backward):
- *   dw[(m*N + n)*K + k] += sum_{b, t < T_A} A[b, t, m] * B[b, t*S + k*dil - pad, n]
+ *   dw[(k*M + m)*N + n] += sum_{b, t < T_A} A[b, t, m] * B[b, t*S + k*dil - pad, n]
+ * (tap-major (K, M, N): the caller permutes to the (M, N, K) conv weight order)
  * (B rows outside [0, T_B) read as 0; pre_a / pre_b: leaky-ReLU(slope) applied to that operand).
  * Conv1d (Co, Ci, K): A = dY (T_out rows, M = Co), B = pre(x) (T_in rows, N = Ci).
  * ConvTranspose1d (Ci, Co, 2s): A = pre(x) (T_in, M = Ci), B = dY (T_up, N = Co), S = s, pad p.
@@ -274,7 +275,7 @@ int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int
                     int dtype, float* dw, void* stream);
 /* Grouped conv (groups > 1): M = C_out / groups and N = C_in / groups per group, lda >= groups*M,
  * ldb >= groups*N; group g reads A columns [g*M, (g+1)*M), B columns [g*N, (g+1)*N) and writes
- * dw block g of the (groups*M, N, K) grouped weight.  Replaces MIOpen's grouped weight pass of
+ * block g of dw laid out (groups, K, M, N).  Replaces MIOpen's grouped weight pass of
  * the multi-scale discriminator (HiFi-GAN V1 MSD). */
 int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
                             int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,

@@ -270,6 +270,36 @@ def test_trainer_step_bf16():
     assert not torch.equal(before, g.conv_pre.weight_v.detach())
 
 
+def test_trainer_graphed_matches_eager():
+    """HIP-graph replays of the training step (HifiGanTrainer.step_graphed) against the same
+    number of eager steps from the same initial state (fp32 compute; atomics reorder sums)."""
+    from visual_onoma_to_wave_amd import hifigan
+    h = hifigan.AttrDict(hifigan_h())
+    mel = (torch.randn(2, 32, 80, generator=torch.Generator().manual_seed(5)) - 4).cuda()
+    y = torch.tanh(torch.randn(2, 8192, generator=torch.Generator().manual_seed(6)) * 0.3).cuda()
+    finals = []
+    for graphed in (False, True):
+        torch.manual_seed(1234)
+        g = _gen("cuda")
+        tr = hifigan.HifiGanTrainer(g, h, graphed=graphed).set_compute_dtype(torch.float32)
+        if graphed:
+            for _ in range(3):  # 1 eager warm-up step + capture, then 3 replays
+                losses = tr.step_graphed(mel, y, warmup=1)
+        else:
+            for _ in range(4):
+                losses = tr.step(mel, y)
+        torch.cuda.synchronize()
+        finals.append(({k: float(v) for k, v in losses.items()},
+                       torch.cat([p.detach().flatten().cpu() for p in g.parameters()]),
+                       torch.cat([p.detach().flatten().cpu() for p in tr.mpd.parameters()])))
+    (le, ge, de), (lg, gg, dg) = finals
+    for k in le:
+        assert abs(le[k] - lg[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, le[k], lg[k])
+    # one AdamW step moves a weight by ~lr = 2e-4 (~4e-3 of its size): a replay that read a stale
+    # packed weight or input would differ at that scale; atomics reordering leaves ~1e-5
+    assert rel_l2(gg, ge) < 1e-4 and rel_l2(dg, de) < 1e-4
+
+
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,T,Ci,Co,K,dil,s,pad,pre", [
     (2, 1000, 32, 32, 11, 5, 1, 25, 0.1), (3, 517, 256, 256, 3, 1, 1, 1, 0.1), (2, 300, 80, 512, 7, 1, 1, 3, None),

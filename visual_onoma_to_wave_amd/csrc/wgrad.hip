@@ -2,7 +2,9 @@
 // (training paths C4 / C5): replaces the MIOpen ``convolution_backward`` weight pass that
 // SURVEY.md 8(b) allowed as the initial fallback.
 //
-//   dW[(m * N + n) * K + k] += sum_{b, t < T_A} A[b, t, m] * B[b, t * S + k * dil - pad, n]
+//   dW[(k * M + m) * N + n] += sum_{b, t < T_A} A[b, t, m] * B[b, t * S + k * dil - pad, n]
+// (tap-major: a wave's atomics cover 4 runs of 16 consecutive floats; in the conv weight's own
+// (m, n, k) order every lane hit its own cache line and the atomics took 70-85 % of the time)
 //
 // (rows of B outside [0, T_B) are zero; optional leaky-ReLU applied to either operand as it is
 // staged).  Conv1d (Co, Ci, K):      A = dY (rows T_out, M = Co), B = pre(x) (rows T_in, N = Ci),
@@ -34,9 +36,10 @@ struct WgradArgs {
   int pre_a, pre_b; float slope;
   int rows_per_split;
   float* dw;
+  int abl;  // timing ablations (wgrad_cfg 10 / 11): 1 = plain stores instead of atomics, 2 = no loads
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
-// and B columns [g N, (g+1) N) and writes its (M, N, K) block of the (groups M, N, K) weight
+// and B columns [g N, (g+1) N) and writes block g of the (groups, K, M, N) result
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
@@ -65,7 +68,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   const int64_t r_end = min(rows, r_begin + p.rows_per_split);
   const TC* A = reinterpret_cast<const TC*>(p.a) + (int64_t)grp * p.M;
   const TC* Bs = reinterpret_cast<const TC*>(p.bsrc) + (int64_t)grp * p.N;
-  float* dw = p.dw + (int64_t)grp * p.M * p.N * p.K;
+  float* dw = p.dw + ((int64_t)grp * p.K + k) * p.M * p.N;
   constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
   constexpr int VPR = WG_T / EV;            // vectors per staged row
   constexpr int NV = WG_R * VPR / 256;      // vectors per thread per operand
@@ -90,8 +93,12 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       const int tb = t * p.S + k * p.dil - p.pad;
       const bool bok = qok && tb >= 0 && tb < p.T_B;
       const int ma = min(m0 + c, p.M - EV), nb = min(n0 + c, p.N - EV);
-      va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + ma);
-      vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + min(max(tb, 0), p.T_B - 1)) * p.ldb + nb);
+      if (p.abl & 2) {
+        va[s] = vb[s] = u32x4_t{(unsigned)tb, (unsigned)ma, 1u, 1u};
+      } else {
+        va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + ma);
+        vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + min(max(tb, 0), p.T_B - 1)) * p.ldb + nb);
+      }
       if (!qok || m0 + c >= p.M) va[s] = u32x4_t{0u, 0u, 0u, 0u};
       if (!bok || n0 + c >= p.N) vb[s] = u32x4_t{0u, 0u, 0u, 0u};
     }
@@ -172,7 +179,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
     }
   }
 
-  // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[(m N + n) K + k]
+  // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[k][m][n]
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -181,7 +188,12 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
-        if (m < p.M && n < p.N) atomicAdd(dw + ((int64_t)m * p.N + n) * p.K + k, acc[i][j][e]);
+        if (m < p.M && n < p.N) {
+          if (p.abl & 1)
+            dw[(int64_t)m * p.N + n] = acc[i][j][e];
+          else
+            atomicAdd(dw + (int64_t)m * p.N + n, acc[i][j][e]);
+        }
       }
 }
 
@@ -236,8 +248,15 @@ extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const vo
   const int64_t rows = (int64_t)B * T_A;
   const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
   // enough workgroups to fill 256 CUs ~4 deep, at least 4 chunks of 64 rows each
-  int64_t splits = std::max<int64_t>(1, (1024 + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
+  const int wc = vo_tune_get("wgrad_cfg");
+  const int64_t target = wc == 1 ? 4096 : wc == 2 ? 8192 : wc == 3 ? 16384 : 1024;
+  p.abl = wc >= 10 ? wc - 9 : 0;  // 10: no atomics, 11: no loads, 12: neither
+  int64_t splits = std::max<int64_t>(1, (target + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
+  // serial row chains of at most 64 chunks (a small tile x tap grid -- the MSD's 32 x 16 groups --
+  // otherwise leaves one workgroup walking every row)
+  const int64_t max_rows = wc == 4 ? 2048 : wc == 5 ? 8192 : wc == 6 ? (int64_t)1 << 40 : 4096;
+  splits = std::max<int64_t>(splits, (rows + max_rows - 1) / max_rows);
   p.rows_per_split = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
   splits = (rows + p.rows_per_split - 1) / p.rows_per_split;
   VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");

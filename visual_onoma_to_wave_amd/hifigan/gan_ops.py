@@ -78,6 +78,15 @@ def out_len(spec, T_in):
 
 
 _PACKS = weakref.WeakKeyDictionary()  # module -> {(spec, dtype, kind...): (versions, packed weight)}
+# Inside a HIP-graph capture only packs recorded by that capture may be reused (an eager pack
+# would be read, never rewritten, by every replay); replays change parameters without bumping
+# their version counters, so the eager cache is dropped after each (reset_pack_cache).
+_CAPTURE_PACKS = weakref.WeakKeyDictionary()
+
+
+def reset_pack_cache():
+    _PACKS.clear()
+    _CAPTURE_PACKS.clear()
 
 
 def weight_key(m):
@@ -94,7 +103,7 @@ def weight_key(m):
 def _cached(wkey, tag, build):
     if wkey is None:
         return build()
-    per = _PACKS.setdefault(wkey[0], {})
+    per = (_CAPTURE_PACKS if torch.cuda.is_current_stream_capturing() else _PACKS).setdefault(wkey[0], {})
     hit = per.get(tag)
     if hit is not None and hit[0] == wkey[1:]:
         return hit[1]
@@ -158,8 +167,10 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
             continue
         J = len(taps)
         c_r = (r + pad - k_r) // S
-        def build(taps=taps):
-            wsel = wt_get()[:, :, taps[::-1]].contiguous()  # tap t <- k_r + S (J - 1 - t)
+        def build(k_r=k_r):
+            # tap t <- k_r + S (J - 1 - t); a strided slice + flip (list indexing would copy the
+            # index list host -> device, which a HIP-graph capture refuses)
+            wsel = wt_get()[:, :, k_r::S].flip(-1).contiguous()
             return ops.pack_grouped_weight(wsel, cdt, groups=g if ci_out == Ci else 1, ci_pad=co_in)
         wp = _cached(wkey, (spec, cdt, "dgrad", r, ci_out, co_in), build)
         ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,

@@ -40,15 +40,24 @@ def _single(disc, wav, grad):
 
 
 class HifiGanTrainer:
-    def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None):
+    """``graphed=True``: ``step_graphed`` replays the whole step (both optimiser steps
+    included) as one HIP graph captured after eager warm-up steps on a side stream -- the step
+    launches ~4.6k kernels, and the eager loop is host-launch-bound.  AdamW then runs with
+    ``capturable=True``; ``end_epoch`` drops the graph so the next step re-captures with the
+    decayed learning rate."""
+
+    def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None, graphed=False):
         self.generator = generator
         device = device or next(generator.parameters()).device
         self.mpd = (mpd or MultiPeriodDiscriminator()).to(device)
         self.msd = (msd or MultiScaleDiscriminator()).to(device)
         self.h = h
-        self.optim_g = torch.optim.AdamW(generator.parameters(), h.learning_rate, betas=[h.adam_b1, h.adam_b2])
+        self.graphed = graphed
+        self._graph = None
+        self.optim_g = torch.optim.AdamW(generator.parameters(), h.learning_rate, betas=[h.adam_b1, h.adam_b2],
+                                         capturable=graphed)
         self.optim_d = torch.optim.AdamW(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
-                                         h.learning_rate, betas=[h.adam_b1, h.adam_b2])
+                                         h.learning_rate, betas=[h.adam_b1, h.adam_b2], capturable=graphed)
         self.sched_g = torch.optim.lr_scheduler.ExponentialLR(self.optim_g, gamma=h.lr_decay)
         self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
         self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,
@@ -116,6 +125,36 @@ class HifiGanTrainer:
         return dict(disc=loss_disc_all.detach(), gen=loss_gen_all.detach(), mel=loss_mel.detach(),
                     fm=loss_fm.detach(), adv=loss_adv.detach())
 
+    def step_graphed(self, x_mel_cl, y, warmup=3):
+        """``step`` as one HIP-graph replay (captured on the first call, after ``warmup`` eager
+        steps on a side stream).  Inputs are copied into the graph's static buffers; the
+        returned loss tensors are the graph's (overwritten by the next replay)."""
+        from . import gan_ops
+        if not self.graphed:
+            raise RuntimeError("HifiGanTrainer: construct with graphed=True to replay steps as a HIP graph")
+        if self.bk_g is not None:
+            raise RuntimeError("HifiGanTrainer: graphed steps are single-process (the RCCL buckets run eagerly)")
+        if self._graph is None:
+            self._x, self._y = x_mel_cl.clone(), y.clone()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self.step(self._x, self._y)
+            torch.cuda.current_stream().wait_stream(side)
+            gan_ops.reset_pack_cache()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                self._out = self.step(self._x, self._y)
+            gan_ops.reset_pack_cache()
+            self._graph = graph
+        self._x.copy_(x_mel_cl)
+        self._y.copy_(y)
+        self._graph.replay()
+        gan_ops.reset_pack_cache()
+        return self._out
+
     def end_epoch(self):
         self.sched_g.step()
         self.sched_d.step()
+        self._graph = None  # the captured AdamW step holds the old learning rate

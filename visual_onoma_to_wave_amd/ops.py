@@ -561,15 +561,16 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     _, T_B, N = b.shape
     if M % groups or N % groups:
         raise ValueError(f"conv1d_wgrad: channels {M} / {N} not divisible by groups {groups}")
-    dw = torch.zeros((M, N // groups, K), dtype=torch.float32, device=a.device)
+    mg, ng = M // groups, N // groups
+    dw = torch.zeros((groups, K, mg, ng), dtype=torch.float32, device=a.device)  # tap-major (kernel order)
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
-    _lib.check(_lib.lib().vo_conv1d_wgrad_grouped(_ptr(a), M, T_A, _ptr(b), N, T_B, B, M // groups, N // groups, K,
+    _lib.check(_lib.lib().vo_conv1d_wgrad_grouped(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K,
                                                   S, dil, pad, groups, int(pre_a is not None),
                                                   int(pre_b is not None), float(slope), vo_dtype(a), _ptr(dw),
                                                   _stream(a)), "vo_conv1d_wgrad")
-    return dw
+    return dw.permute(0, 2, 3, 1).reshape(M, ng, K)
 
 
 def colsum(x):
