@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
-    ap.add_argument("--no-graph", action="store_true", help="gan mode: eager steps instead of one HIP graph")
+    ap.add_argument("--no-graph", action="store_true", help="train / gan modes: eager steps instead of one HIP graph")
     ap.add_argument("--mode", default="infer", choices=["infer", "train", "gan"],
                     help="infer: end-to-end synthesis (headline); train: C4 training step (DDP); "
                          "gan: C5 HiFi-GAN training step (DDP)")
@@ -67,7 +67,8 @@ def bench_train(a, dev, rank, world, dist):
     m = vTTS(pc, mc, tc)
     load_into(m, vtts_arrays())
     m = m.to(dev).train().set_precision(a.precision)
-    opt = ScheduledOptim(m, tc, mc, 0)
+    graphed = dist is None and not a.no_graph  # one process: the whole step as a HIP graph replay
+    opt = ScheduledOptim(m, tc, mc, 0, capturable=graphed)
     bk = None
     if dist:
         skip = unused_on_path(m)
@@ -78,14 +79,22 @@ def bench_train(a, dev, rank, world, dist):
     batch = (None, t["audiotypes"], t["texts"], t["src_lens"], t["max_src_len"], t["mels"], t["mel_lens"],
              t["max_mel_len"], t["e_targets"], None, t["d_targets"], t["images"], None)
     loss_fn = FastSpeech2Loss()
+    if graphed:
+        from visual_onoma_to_wave_amd.train import GraphedTrainStep
+        run = GraphedTrainStep(m, opt, loss_fn)
+    else:
+        def run(bt):
+            return train_step(m, opt, loss_fn, bt, bucketer=bk)
     for _ in range(a.warmup):
-        train_step(m, opt, loss_fn, batch, bucketer=bk)
+        run(batch)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        losses = train_step(m, opt, loss_fn, batch, bucketer=bk)
+        losses = run(batch)
+        if os.environ.get("VO_BENCH_DEBUG"):
+            print("loss", [round(float(v.detach()), 4) for v in losses[:6]], file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -101,7 +110,7 @@ def bench_train(a, dev, rank, world, dist):
             "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
-            "final_loss": round(float(losses[0]), 5),
+            "final_loss": round(float(losses[0]), 5), "hip_graph": graphed,
             "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
                        "seq_len": a.mel_len, "src_len": a.src_len, "parallelism": f"dp{world} (RCCL bucketed all-reduce)"}}))
 

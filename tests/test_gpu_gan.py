@@ -283,10 +283,10 @@ def test_trainer_graphed_matches_eager():
         g = _gen("cuda")
         tr = hifigan.HifiGanTrainer(g, h, graphed=graphed).set_compute_dtype(torch.float32)
         if graphed:
-            for _ in range(3):  # 1 eager warm-up step + capture, then 3 replays
+            for _ in range(9):  # 1 eager warm-up step + capture, then 9 back-to-back replays
                 losses = tr.step_graphed(mel, y, warmup=1)
         else:
-            for _ in range(4):
+            for _ in range(10):
                 losses = tr.step(mel, y)
         torch.cuda.synchronize()
         finals.append(({k: float(v) for k, v in losses.items()},

@@ -96,3 +96,44 @@ def test_training_reduces_loss(device):
         losses = train_step(m, opt, FastSpeech2Loss(), batch)
         first = first if first is not None else float(losses[0])
     assert float(losses[0]) < 0.8 * first
+
+
+def test_graphed_train_step_matches_eager(device):
+    """train.GraphedTrainStep (HIP-graph replay with the capturable Adam and a device-tensor
+    learning rate) against the same number of eager train_step calls (fp32, dropout off).  The
+    weight-gradient atomics make two eager runs differ slightly; training amplifies that, so the
+    graphed run is held to the spread of a second eager run, not to zero."""
+    from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
+    from visual_onoma_to_wave_amd.train import GraphedTrainStep, train_step
+    pc, mc, tc = configs()
+    tc = dict(tc)
+    tc["optimizer"] = dict(tc["optimizer"], warm_up_step=10, init_lr=1e-3)  # steps that move the weights
+    batch = _batch(golden("vtts_tf"), device)
+    finals = []
+    for graphed in (False, False, True):
+        m = vTTS(pc, mc, tc)
+        load_into(m, vtts_arrays())
+        m = m.to(device).train().set_precision("fp32")
+        _no_dropout(m)
+        opt = ScheduledOptim(m, tc, mc, 0, capturable=graphed)
+        if graphed:
+            run = GraphedTrainStep(m, opt, FastSpeech2Loss(), warmup=1)
+            for _ in range(11):  # 1 eager warm-up step + capture, then 11 replays
+                losses = run(batch)
+        else:
+            for _ in range(12):
+                losses = train_step(m, opt, FastSpeech2Loss(), batch)
+        torch.cuda.synchronize()
+        assert opt.current_step == 12
+        finals.append((np.array([float(x) for x in losses]),
+                       torch.cat([p.detach().flatten().cpu() for p in m.parameters()])))
+    (l0, p0), (l1, p1), (lg, pg) = finals
+    p_noise = float((p1 - p0).norm() / p0.norm())
+    p_err = float((pg - p0).norm() / p0.norm())
+    l_noise, l_err = float(np.abs(l1 - l0).max()), float(np.abs(lg - l0).max())
+    print(f"graphed vs eager: params {p_err:.2e} (eager spread {p_noise:.2e}), losses {l_err:.2e} "
+          f"(eager spread {l_noise:.2e})")
+    # twelve Adam steps at lr up to 3e-4 move the weights by ~1e-2 of their norm and the loss
+    # 25 -> 7.5: a replay with a stale input / learning rate / packed weight differs at that scale
+    assert p_err < max(10 * p_noise, 1e-6) and p_err < 1e-3
+    assert l_err < max(10 * l_noise, 1e-4)

@@ -155,5 +155,33 @@ class LengthRegulateFn(torch.autograd.Function):
         return gx[:, :T].to(ctx.xdtype), None, None, None
 
 
+def batch_norm_train(x, bn, dims):
+    """Training-mode BatchNorm (batch statistics over ``dims``; the channel is the one dim left)
+    with the running-stat update of ``nn.BatchNorm*`` (momentum, unbiased running variance,
+    ``num_batches_tracked``).  Reductions and elementwise ops of PyTorch-ROCm on the tensor as it
+    lies -- channels-last PostNet activations need no transpose, and the single-channel VFE
+    maps reduce over all blocks (MIOpen's spatial kernels took ~200 us a call on both)."""
+    n = 1
+    for d in dims:
+        n *= x.shape[d]
+    mean = x.mean(dims, keepdim=True)
+    xc = x - mean
+    var = (xc * xc).mean(dims, keepdim=True)
+    if bn.track_running_stats and bn.running_mean is not None:
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+            m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+            bn.running_mean.mul_(1.0 - m).add_(mean.detach().flatten().to(bn.running_mean.dtype), alpha=m)
+            bn.running_var.mul_(1.0 - m).add_(var.detach().flatten().to(bn.running_var.dtype),
+                                              alpha=m * n / max(n - 1, 1))
+    shape = [1] * x.dim()
+    ch = [d for d in range(x.dim()) if d not in dims and d - x.dim() not in dims]
+    shape[ch[0]] = x.shape[ch[0]]
+    y = xc * torch.rsqrt(var + bn.eps)
+    if bn.affine:
+        y = y * bn.weight.view(shape) + bn.bias.view(shape)
+    return y
+
+
 def length_regulate(x, dur, max_len, out_dtype=None):
     return LengthRegulateFn.apply(x, dur, max_len, out_dtype or x.dtype)

@@ -18,7 +18,7 @@ import itertools
 
 import torch
 
-from ..train import GradBucketer
+from ..train import GradBucketer, graph_fence
 from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiScaleDiscriminator, discriminator_loss,
                              feature_loss, generator_loss)
 
@@ -148,13 +148,16 @@ class HifiGanTrainer:
                 self._out = self.step(self._x, self._y)
             gan_ops.reset_pack_cache()
             self._graph = graph
+        if getattr(self, "_done", None) is not None:
+            self._done.synchronize()  # train.graph_fence: replays are not launched back to back
         self._x.copy_(x_mel_cl)
         self._y.copy_(y)
         self._graph.replay()
+        self._done = graph_fence()
         gan_ops.reset_pack_cache()
         return self._out
 
     def end_epoch(self):
         self.sched_g.step()
         self.sched_d.step()
-        self._graph = None  # the captured AdamW step holds the old learning rate
+        self._graph = self._done = None  # the captured AdamW step holds the old learning rate

@@ -10,12 +10,18 @@ import torch
 
 
 class ScheduledOptim:
-    def __init__(self, model, train_config, model_config, current_step):
+    """``capturable=True`` (HIP-graph training, ``train.GraphedTrainStep``): Adam keeps its step
+    counts and the learning rate as device tensors, and the schedule writes the new rate into
+    that tensor (outside the graph) instead of replacing the Python float."""
+
+    def __init__(self, model, train_config, model_config, current_step, capturable=False):
         o = train_config["optimizer"]
         params = [p for p in model.parameters() if p.requires_grad]
         kw = dict(betas=o["betas"], eps=o["eps"], weight_decay=o["weight_decay"])
         if params and params[0].is_cuda:
             kw["fused"] = True
+        if capturable:
+            kw.update(capturable=True, lr=torch.tensor(0.0, device=params[0].device))
         self._optimizer = torch.optim.Adam(params, **kw)
         self.n_warmup_steps = o["warm_up_step"]
         self.anneal_steps = o["anneal_steps"]
@@ -45,4 +51,7 @@ class ScheduledOptim:
         self.current_step += 1
         lr = self.init_lr * self._get_lr_scale()
         for group in self._optimizer.param_groups:
-            group["lr"] = lr
+            if torch.is_tensor(group["lr"]):
+                group["lr"].fill_(lr)
+            else:
+                group["lr"] = lr

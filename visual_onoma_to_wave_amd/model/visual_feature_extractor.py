@@ -78,7 +78,13 @@ class VisualFeatureExtractor(HipModule):
         n = int((W - (self.stride // 2) * self.slice_width * 2) / self.slice_width)
         sl = images[..., : n * self.slice_width].reshape(B, C, H, n, self.slice_width)
         x = sl.permute(0, 3, 1, 2, 4).reshape(B * n, C, H, self.slice_width)
-        x = self.embedder(x)
+        for m in self.embedder:  # BatchNorm2d with batch statistics off MIOpen (1 channel)
+            if isinstance(m, nn.BatchNorm2d):
+                x = AG.batch_norm_train(x, m, (0, 2, 3))
+            elif isinstance(m, nn.ReLU):
+                x = torch.relu(x)
+            else:
+                x = m(x)
         y = AG.linear(x.reshape(1, B * n, -1).to(out_dtype), self.bridge[0].weight, self.bridge[0].bias,
                       relu=True, compute_dtype=out_dtype)
         return y.view(B, n, self.embed_dim)

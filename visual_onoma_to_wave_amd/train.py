@@ -11,8 +11,6 @@ that receive no gradient on the path (``encoder.src_word_emb`` with image input,
 ``variance_adaptor.kurt_embedding`` without kurtosis conditioning) are left out.
 """
 
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -125,6 +123,64 @@ def train_step(model, optimizer, loss_fn, batch, grad_clip=1.0, bucketer=None, u
     optimizer.step_and_update_lr()
     optimizer.zero_grad()
     return losses
+
+
+def graph_fence():
+    """Host wait for a HIP-graph replay to finish, called right after ``replay()``.  Measured
+    on this ROCm: back-to-back replays of the acoustic step without it produced NaN losses after
+    ~10 steps; an event recorded after the replay and waited on before the next one did not
+    prevent it, a stream synchronize does (graphed and eager steps then match).  Costs ~1 %."""
+    torch.cuda.current_stream().synchronize()
+    return None
+
+
+class GraphedTrainStep:
+    """``train_step`` replayed as one HIP graph (single process): forward, loss, backward, clip
+    and the Adam update are captured once after ``warmup`` eager steps on a side stream; each
+    call copies the batch into the graph's static tensors, advances the learning-rate schedule
+    (a device tensor, ``ScheduledOptim(capturable=True)``) and replays.  The acoustic step
+    launches ~1.9k kernels, so the eager loop is bound by host launch time.  Returns the
+    graph's loss tensors (overwritten by the next call)."""
+
+    def __init__(self, model, optimizer, loss_fn, grad_clip=1.0, use_image=True, warmup=3):
+        self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
+        self.grad_clip, self.use_image, self.warmup = grad_clip, use_image, warmup
+        self.graph = None
+
+    def _body(self, batch):
+        output = self.model(*(batch[1:]), self.use_image)
+        losses = self.loss_fn(batch, output)
+        losses[0].backward()
+        params = [p for p in self.model.parameters() if p.grad is not None]
+        torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
+        self.opt._optimizer.step()
+        self.opt._optimizer.zero_grad(set_to_none=True)
+        return losses
+
+    def __call__(self, batch):
+        if self.graph is None:
+            self.static = tuple(b.clone() if torch.is_tensor(b) else b for b in batch)
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(self.warmup):
+                    self.opt._update_learning_rate()
+                    self._body(self.static)
+            torch.cuda.current_stream().wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self._body(self.static)
+        if getattr(self, "done", None) is not None:
+            self.done.synchronize()  # see graph_fence
+        for s, b in zip(self.static, batch):
+            if torch.is_tensor(s):
+                s.copy_(b)
+            elif s != b:
+                raise ValueError("GraphedTrainStep: non-tensor batch entries are fixed at capture")
+        self.opt._update_learning_rate()
+        self.graph.replay()
+        self.done = graph_fence()
+        return self.out
 
 
 def init_distributed():

@@ -114,11 +114,10 @@ class PostNet(HipModule):
             last = i == n - 1
             h = AG.conv1d(h, conv.weight, conv.bias, K=k, pad=(k - 1) // 2, compute_dtype=self.compute_dtype,
                           out_dtype=torch.float32 if last else self.compute_dtype)
-            hb = F.batch_norm(h.transpose(1, 2), bn.running_mean, bn.running_var, bn.weight, bn.bias, True,
-                              bn.momentum, bn.eps)
+            hb = AG.batch_norm_train(h, bn, (0, 1))  # channels-last (B, T, C): no transposes
             if not last:
                 hb = torch.tanh(hb)
-            h = F.dropout(hb, self.dropout_p, True).transpose(1, 2).contiguous()
+            h = F.dropout(hb, self.dropout_p, True).contiguous()
         return h
 
     def forward(self, x):
