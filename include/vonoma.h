@@ -208,6 +208,19 @@ int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void*
                      const float* b2, void* y, const void* acc, int B, int T, int C, int K,
                      int dil, float slope, float out_scale, void* stream);
 
+/* Fused ResBlock1 with K = 3 (bf16, channels-last (B, T, C), C = 32 / 64 / 128): all three
+ * (c1_dil[s], c2) iterations in one launch,
+ *   x_{s+1} = x_s + c2_s(lrelu(c1_s(lrelu(x_s, slope)), slope))   (s = 0, 1; bf16-rounded)
+ *   y = (x_2 + c2_2(lrelu(c1_2(lrelu(x_2))))) * out_scale (+ acc)
+ * w1[s] / w2[s]: packed [3][C][C] bf16, b1[s] / b2[s] fp32, dil[s] in [1, 8] with
+ * sum_s (dil[s] + 1) <= 12 (HiFi-GAN V1: 1, 3, 5).  x_1, x_2 never leave the chip.  acc may
+ * alias y; y must not alias x.  Replaces a whole ResBlock.forward (scripts/hifigan/
+ * models.py:96-103) with the MRF sum of Generator.forward (models.py:155-160); results equal
+ * three vo_resblock_pair launches up to the fp32 summation order. */
+int vo_resblock3(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                 const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C,
+                 float slope, float out_scale, void* stream);
+
 /* (B, C, T) -> (B, T, ldy) with channels C..ldy-1 zero-filled; fp32 in, dtype out. */
 int vo_transpose_bct(const float* x, int B, int C, int T, void* y, int y_dtype, int ldy,
                      void* stream);

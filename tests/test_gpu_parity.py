@@ -326,6 +326,54 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
     assert rel_l2(out.float().cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("C,T", [(32, 1000), (64, 777), (128, 300), (32, 5), (64, 1), (128, 13), (128, 232),
+                                 (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768)])
+@pytest.mark.parametrize("with_acc", [True, False])
+@pytest.mark.parametrize("cfg", [0, 1, 4])
+def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
+    """vo_resblock3 (a whole k = 3 ResBlock, dilations 1/3/5, in one launch) against the torch fp32
+    ResBlock at tile edges (frame 232 / 488 valid rows), T = 1, and multi-tile persistent runs;
+    and against three vo_resblock_pair launches (same bf16 intermediates up to summation order)."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(C * 7 + T)
+    B, k, dils = 2, 3, (1, 3, 5)
+    x = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+    w1 = [torch.randn(C, C, k, generator=g) / (C * k) ** 0.5 for _ in dils]
+    w2 = [torch.randn(C, C, k, generator=g) / (C * k) ** 0.5 for _ in dils]
+    b1 = [torch.randn(C, generator=g) * 0.1 for _ in dils]
+    b2 = [torch.randn(C, generator=g) * 0.1 for _ in dils]
+    acc = torch.randn(B, T, C, generator=g).to(torch.bfloat16) if with_acc else None
+    cur = x.float().transpose(1, 2)
+    for s, d in enumerate(dils):
+        t = F.leaky_relu(F.conv1d(F.leaky_relu(cur, 0.1), w1[s], b1[s], padding=d, dilation=d), 0.1)
+        cur = F.conv1d(t, w2[s], b2[s], padding=1) + cur
+    ref = (cur / 3.0).transpose(1, 2) + (acc.float() if with_acc else 0.0)
+    p1 = [ops.pack_conv_weight(w.cuda(), torch.bfloat16) for w in w1]
+    p2 = [ops.pack_conv_weight(w.cuda(), torch.bfloat16) for w in w2]
+    b1c, b2c = [b.cuda() for b in b1], [b.cuda() for b in b2]
+    xc = x.cuda()
+    out = acc.cuda().clone() if with_acc else torch.empty_like(xc)
+    from visual_onoma_to_wave_amd import _lib
+    _lib.lib().vo_tune(b"rb3_cfg", cfg)  # every rb3_cfg kernel configuration (0 = shipped)
+    try:
+        ops.resblock3(xc, p1, b1c, p2, b2c, dils, 0.1, out=out, out_scale=1.0 / 3, acc=out if with_acc else None)
+    finally:
+        _lib.lib().vo_tune(b"rb3_cfg", 0)
+    chain = xc
+    for s, d in enumerate(dils):  # the per-pair path
+        if s < 2:
+            chain = ops.resblock_pair(chain, p1[s], b1c[s], p2[s], b2c[s], k, d, 0.1)
+        else:
+            o = acc.cuda().clone() if with_acc else torch.empty_like(xc)
+            chain = ops.resblock_pair(chain, p1[s], b1c[s], p2[s], b2c[s], k, d, 0.1, out=o, out_scale=1.0 / 3,
+                                      acc=o if with_acc else None)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    assert rel_l2(out.float().cpu(), ref) < 1e-2
+    assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
+
+
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 9])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),

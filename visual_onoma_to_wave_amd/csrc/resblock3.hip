@@ -1,0 +1,389 @@
+// Fused HiFi-GAN ResBlock1 with kernel size 3: all three (c1_d, c2) iterations of one
+// ResBlock in ONE persistent launch (scripts/hifigan/models.py:96-103, dilations (1, 3, 5)),
+// with the Generator's MRF sum / num_kernels scale in the last epilogue (models.py:155-160):
+//   x1 = x  + c2_0(lrelu(c1_1(lrelu x )))          (each rounded to bf16, as between the
+//   x2 = x1 + c2_1(lrelu(c1_3(lrelu x1)))           per-pair launches of resblock.hip)
+//   y  = (x2 + c2_2(lrelu(c1_5(lrelu x2)))) * out_scale (+ acc)
+//
+// Why: at k = 3 a per-pair launch moves ~4 activation passes (window, residual, MRF
+// accumulator, output) for little MFMA work, and every CU fetches its next window at the same
+// moment (the pair kernels' timing ablation: 26 % of a k = 3 launch).  Here a tile's window is
+// fetched once for three pairs; x1 / x2 never leave the chip (bf16 in registers, lrelu'd copy
+// in LDS).  Cost: every conv is evaluated on the whole F-row frame and the valid rows shrink by
+// the halos, 1+1+3+1+5+1 = 12 per side, so a tile yields F - 24 output rows (9 % more MFMA work
+// at F = 256).
+//
+// LDS: one activation region of F + 2*HPC rows per 32-channel plane (frame row f lives at
+// region row f + HPC; the pad rows only feed frame rows whose outputs are discarded), used in
+// place: lrelu(x_s) -> (P1) -> T1 over it -> (P2) -> lrelu(x_{s+1}) over it; weights either all
+// 18 taps resident (C = 32) or streamed one tap at a time through a double buffer by LDS-DMA.
+// Accumulation order per conv: tap-major, planes inner (as the streamed pair kernels).
+
+#include <algorithm>
+
+#include "mrf_common.h"
+
+namespace vo {
+
+struct Rb3Args {
+  const bf16_t* x;
+  const bf16_t* w1[3]; const float* b1[3]; const bf16_t* w2[3]; const float* b2[3];
+  bf16_t* y; const bf16_t* acc;
+  int T, dil[3], tiles_per_b, ntiles;
+  float slope, out_scale;
+};
+
+constexpr int RB3_HPC = 8;    // region pad rows per side (dilation <= 8)
+constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six convs of (k-1)/2 * dil
+
+// Streamed weights: a group is 1 / SPLIT of a tap (NC / SPLIT planes); NBUF group buffers form
+// a ring and each group's LDS-DMA is issued NBUF - 1 groups ahead (vmcnt is in-order, so the
+// wait at a group's end leaves the younger NBUF - 2 groups in flight).
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
+__global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
+  constexpr int NW = WC * WT;
+  constexpr int NT = NW * 64;
+  constexpr int NC = C / 32;               // 32-channel planes
+  constexpr int NI = C / (16 * WC);        // co tiles per wave
+  constexpr int F = WT * 16 * NJ;          // frame rows per tile
+  constexpr int RR = F + 2 * RB3_HPC;      // region rows per plane
+  constexpr int BT = F - 2 * RB3_HALO;     // valid output rows per tile
+  constexpr int SHW = NI >= 8 ? 5 : (NI == 4 ? 4 : 3);
+  constexpr int VPR = NC * 4;              // 16-byte vectors per activation row
+  constexpr int TAPV = C * VPR;            // 16-byte vectors per weight tap
+  constexpr int TAPE = NC * C * 32;        // LDS elements per weight tap
+  constexpr int NH = NI / 2;               // 8-channel vectors per lane in epilogue layout
+  constexpr int NG = 18;                   // taps per tile: 3 stages x 2 convs x 3 taps
+  constexpr int D = NBUF - 1;              // DMA prefetch distance in groups
+  constexpr int NGR = NG * SPLIT;          // streamed groups per tile
+  constexpr int GE = TAPE / SPLIT;         // LDS elements per group buffer
+  constexpr int GPL = NC / SPLIT;          // planes per group
+  static_assert(RESW || (NC % SPLIT == 0 && (TAPV / SPLIT) % NT == 0 && NBUF >= 2),
+                "streamed groups split into whole wave-KiB DMA instructions");
+  static_assert(NT % VPR == 0 && (NT / VPR) % 8 == 0, "window slot stride must keep the swizzle");
+  constexpr int RSTEP = NT / VPR;
+  constexpr int MAXW = (RR + RSTEP - 1) / RSTEP;  // window vectors per thread
+
+  const int T = a.T;
+  const float slope = a.slope;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* reg = reinterpret_cast<bf16_t*>(smem_raw);  // [NC][RR][32]
+  bf16_t* wls = reg + NC * RR * 32;                   // RESW: [18] taps; else [2] tap buffers
+  float* sbias = reinterpret_cast<float*>(wls + (RESW ? NG * TAPE : NBUF * GE));  // [6][C]: b1_0 b2_0 b1_1 ...
+  bf16_t* spare = reinterpret_cast<bf16_t*>(sbias + 6 * C);               // sink for idle slots
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int wc = wave % WC, wt = wave / WC;
+  const int cw0 = wc * (C / WC);
+  const int n0 = cw0 + NI * 4 * lq;
+
+  const int G = gridDim.x;
+  int tile = (int)(((int64_t)blockIdx.x * a.ntiles) / G);
+  const int tile_end = (int)(((int64_t)(blockIdx.x + 1) * a.ntiles) / G);
+  if (tile >= tile_end) return;  // uniform per workgroup
+
+  for (int i = tid; i < 6 * C; i += NT) {
+    const int s = i / (2 * C), ph = (i / C) & 1, c = i % C;
+    sbias[i] = ph ? a.b2[s][c] : a.b1[s][c];
+  }
+
+  // ---- weights.  Tap g of a tile: stage g / 6, conv (g / 3) & 1, tap g % 3.
+  auto tap_src = [&](int g) -> const bf16_t* {
+    const int s = g / 6, ph = (g / 3) & 1, k = g % 3;
+    return (ph ? a.w2[s] : a.w1[s]) + k * (C * C);
+  };
+  constexpr int GLN = RESW ? 1 : TAPV / SPLIT / NT;  // DMA instructions per wave per group
+  int gl_off[GLN];
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  if constexpr (!RESW) {
+#pragma unroll
+    for (int s = 0; s < GLN; ++s) {  // LDS slot p holds (plane, co, chunk q ^ swz(co)): swizzle on the source
+      const int p = (s * NW + wave) * 64 + lane;
+      const int pl = p / (C * 4), rem = p - pl * C * 4;
+      const int co = rem >> 2, q = (rem & 3) ^ ((co >> (SHW - 1)) & 2);
+      gl_off[s] = co * C + pl * 32 + q * 8;
+    }
+  }
+  auto load_grp = [&](int h, int buf) {  // LDS-DMA of group h (planes of tap h / SPLIT) into buffer buf
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef const __attribute__((address_space(1))) void g_void;
+    const bf16_t* W = tap_src(h / SPLIT) + (h % SPLIT) * GPL * 32;
+#pragma unroll
+    for (int s = 0; s < GLN; ++s)
+      __builtin_amdgcn_global_load_lds((g_void*)(W + gl_off[s]),
+                                       (lds_void*)(wls + buf * GE + (s * NW + wave_u) * 64 * 8), 16, 0, 0);
+  };
+  if constexpr (RESW) {  // all 18 taps, once per kernel (tap loop uniform: the source is a kernel argument)
+    for (int g = 0; g < NG; ++g) {
+      const bf16_t* W = tap_src(g);
+      for (int vv = tid; vv < TAPV; vv += NT) {
+        const int co = vv / VPR, rem = vv - co * VPR;
+        *reinterpret_cast<u32x4*>(wls + g * TAPE + (rem >> 2) * C * 32 + rb_off(co, rem & 3, SHW)) =
+            *reinterpret_cast<const u32x4*>(W + vv * 8);
+      }
+    }
+  } else {
+    for (int h = 0; h < D; ++h) load_grp(h, h);
+  }
+
+  // ---- window staging: region rows [0, RR) = positions p0 - HPC + row, p0 = t0 - HALO
+  const int xr0 = tid / VPR, xrem = tid - xr0 * VPR;
+  const int xg0 = xrem * 8;
+  const int xl0 = (xrem >> 2) * RR * 32 + rb_off(xr0, xrem & 3, 2);
+  u32x4 xw[MAXW];
+  bool xw_ok[MAXW];
+  auto load_win = [&](int tl) {
+    const int b = tl / a.tiles_per_b;
+    const int R0 = (tl - b * a.tiles_per_b) * BT - RB3_HALO - RB3_HPC;
+    const bf16_t* base = a.x + (int64_t)b * T * C;
+#pragma unroll
+    for (int s = 0; s < MAXW; ++s) {
+      const int t = R0 + xr0 + s * RSTEP;
+      xw_ok[s] = t >= 0 && t < T && xr0 + s * RSTEP < RR;
+      xw[s] = *reinterpret_cast<const u32x4*>(base + (int64_t)min(max(t, 0), T - 1) * C + xg0);
+    }
+  };
+  auto store_win = [&]() {
+#pragma unroll
+    for (int s = 0; s < MAXW; ++s) {
+      const u32x4 v = lrelu8(xw[s], slope);
+      *reinterpret_cast<u32x4*>(xr0 + s * RSTEP < RR ? reg + xl0 + s * RSTEP * 32 : spare) =
+          xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  int a_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) a_off[i] = rb_off(cw0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq, SHW);
+  const int brow0 = wt * 16 * NJ + lr + RB3_HPC;  // region row of the lane's first B-fragment row
+
+  load_win(tile);
+  store_win();
+  if constexpr (!RESW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto lane_bias = [&](int which, float (&bz)[8 * NH]) {
+    const float4* bp = reinterpret_cast<const float4*>(sbias + which * C + n0);
+#pragma unroll
+    for (int u = 0; u < 2 * NH; ++u) {
+      const float4 v = bp[u];
+      bz[4 * u] = v.x; bz[4 * u + 1] = v.y; bz[4 * u + 2] = v.z; bz[4 * u + 3] = v.w;
+    }
+  };
+
+  int gcount = 0;  // streamed groups consumed (position in the buffer ring)
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / a.tiles_per_b;
+    const int p0 = (tile - b * a.tiles_per_b) * BT - RB3_HALO;  // position of frame row 0
+    const bool has_next = tile + 1 < tile_end;
+    u32x4 xres[NJ][NH];  // x_s of the lane's frame rows (bf16), the next stage's residual
+
+    for (int g = 0; g < NG; ++g) {
+      const int s = g / 6, ph = (g / 3) & 1, k = g % 3;
+      const int step = ph ? 1 : a.dil[s];
+      const int row = brow0 + (k - 1) * step;
+#pragma unroll
+      for (int part = 0; part < (RESW ? 1 : SPLIT); ++part) {
+        const bf16_t* wb;
+        if constexpr (RESW) {
+          wb = wls + g * TAPE;
+        } else {  // group D ahead (wrapping into the next tile's first groups)
+          const int h = g * SPLIT + part;
+          load_grp(h + D < NGR ? h + D : h + D - NGR, (gcount + D) % NBUF);
+          wb = wls + (gcount % NBUF) * GE;
+        }
+#pragma unroll
+        for (int cl = 0; cl < (RESW ? NC : GPL); ++cl) {
+          const int c = part * GPL + cl;
+          Frag<bf16_t> af[NI], bfr[NJ];
+#pragma unroll
+          for (int i = 0; i < NI; ++i) af[i].load(wb + cl * C * 32 + a_off[i]);
+          const int boff = c * RR * 32 + rb_off(row, lq, 2);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) bfr[j].load(reg + boff + 16 * j * 32);
+#pragma unroll
+          for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+        }
+        if constexpr (!RESW) {
+          // the next group's DMA (issued D - 1 groups ago) has landed for this wave; younger ones
+          // stay in flight; the barrier publishes it and frees this group's buffer
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * GLN) : "memory");
+          __syncthreads();
+          ++gcount;
+        }
+      }
+      if (k != 2) continue;
+      // ---- end of a conv: every wave is past its reads of the region
+      if constexpr (RESW) __syncthreads();
+      float bz[8 * NH];
+      lane_bias(2 * s + ph, bz);
+      if (ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = p0 + r;
+          const bool inside = pos >= 0 && pos < T;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
+              f[e] = inside ? fmaxf(z, z * slope) : 0.f;
+            }
+            const int ch = n0 + 8 * h;
+            store8(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2), f);
+          }
+        }
+      } else if (s < 2) {  // x_{s+1} = x_s + c2 + b2 (bf16), its lrelu'd copy over the region
+        if (s == 0) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int pos = min(max(p0 + wt * 16 * NJ + 16 * j + lr, 0), T - 1);
+            const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+            for (int h = 0; h < NH; ++h) xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = p0 + r;
+          const bool inside = pos >= 0 && pos < T;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            float xf[8];
+            unpack8(xres[j][h], xf);
+            uint32_t w[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const int e = 2 * e2;
+              w[e2] = pack_bf16x2(acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e] + xf[e],
+                                  acc[2 * h + (e + 1) / 4][j][(e + 1) & 3] + bz[8 * h + e + 1] + xf[e + 1]);
+            }
+            xres[j][h] = u32x4{w[0], w[1], w[2], w[3]};
+            const int ch = n0 + 8 * h;
+            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) =
+                inside ? lrelu8(xres[j][h], slope) : u32x4{0u, 0u, 0u, 0u};
+          }
+        }
+      } else {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = p0 + r;
+          if (r < RB3_HALO || r >= F - RB3_HALO || pos >= T) continue;
+          const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            float xf[8], af8[8], q[8];
+            unpack8(xres[j][h], xf);
+            if (a.acc) {
+              load8(a.acc + off + 8 * h, af8);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) af8[e] = 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              q[e] = (acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e] + xf[e]) * a.out_scale + af8[e];
+            store8(a.y + off + 8 * h, q);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (g + 1 < NG) __syncthreads();  // region rewritten: visible before the next conv reads it
+    }
+    // next window over the region (P2 of stage 2 ended its region reads at the last barrier)
+    load_win(has_next ? tile + 1 : tile);
+    if (has_next) store_win();
+    __syncthreads();
+  }
+}
+
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
+static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
+  constexpr int NW = WC * WT;
+  constexpr int F = WT * 16 * NJ;
+  constexpr int BT = F - 2 * RB3_HALO;
+  constexpr int RR = F + 2 * RB3_HPC;
+  a.tiles_per_b = (a.T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  const size_t wel = RESW ? 18 * (size_t)C * C : (size_t)NBUF * C * C / SPLIT;
+  const size_t lds = ((size_t)RR * C + wel) * sizeof(bf16_t) + 6 * C * sizeof(float) + 16;
+  if (lds > 160 * 1024) {
+    vo_set_error("resblock3: LDS %zu B exceeds 160 KiB", lds);
+    return VO_ERR_INVALID;
+  }
+  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF>;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NW * 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int grid = (int)std::min<int64_t>((int64_t)cus * per_cu, a.ntiles);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
+  VO_RETURN_LAUNCH();
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                            const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C,
+                            float slope, float out_scale, void* stream) {
+  VO_CHECK_ARG(x && w1 && b1 && w2 && b2 && dil && y, "resblock3: null pointer");
+  VO_CHECK_ARG(C == 32 || C == 64 || C == 128, "resblock3: C=%d unsupported (32, 64 or 128)", C);
+  VO_CHECK_ARG(B > 0 && T > 0, "resblock3: empty");
+  VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "resblock3: slope %g outside [0, 1]", slope);
+  VO_CHECK_ARG(y != x, "resblock3: y must not alias x (neighbouring tiles re-read x)");
+  VO_CHECK_ARG(acc == nullptr || acc == y || acc != x, "resblock3: acc must not alias x");
+  Rb3Args a;
+  a.x = (const bf16_t*)x;
+  int halo = 0;
+  for (int s = 0; s < 3; ++s) {
+    VO_CHECK_ARG(w1[s] && b1[s] && w2[s] && b2[s], "resblock3: null weight of stage %d", s);
+    VO_CHECK_ARG(dil[s] >= 1 && dil[s] <= RB3_HPC, "resblock3: dilation %d outside [1, %d]", dil[s], RB3_HPC);
+    a.w1[s] = (const bf16_t*)w1[s]; a.b1[s] = b1[s]; a.w2[s] = (const bf16_t*)w2[s]; a.b2[s] = b2[s];
+    a.dil[s] = dil[s];
+    halo += dil[s] + 1;
+  }
+  VO_CHECK_ARG(halo <= RB3_HALO, "resblock3: dilations (%d, %d, %d) exceed the 12-row halo", dil[0], dil[1], dil[2]);
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
+  a.T = T; a.slope = slope; a.out_scale = out_scale;
+  a.tiles_per_b = a.ntiles = 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // measured on MI355X at B = 32 (tools/ab_rb3.py, with the MRF accumulator), against three
+  // vo_resblock_pair launches: C = 128 0.84 vs 1.02 ms, C = 64 0.61 vs 0.67, C = 32 0.39 vs 0.52.
+  // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
+  // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
+  const int cfg = vo_tune_get("rb3_cfg");
+  if (C == 32) {  // 256-row frames, all weights resident: 2 workgroups (4 waves / SIMD) per CU
+    if (cfg == 1) return rb3_launch<32, 1, 8, 4, true>(a, B, st);
+    return rb3_launch<32, 1, 8, 2, true>(a, B, st);
+  }
+  if (C == 64) {
+    if (cfg == 1) return rb3_launch<64, 1, 8, 2, false>(a, B, st);
+    if (cfg == 4) return rb3_launch<64, 1, 8, 4, false, 1, 4>(a, B, st);
+    return rb3_launch<64, 1, 8, 4, false>(a, B, st);
+  }
+  if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
+  if (cfg == 4) return rb3_launch<128, 2, 4, 4, false, 2, 4>(a, B, st);
+  return rb3_launch<128, 2, 4, 4, false>(a, B, st);
+}

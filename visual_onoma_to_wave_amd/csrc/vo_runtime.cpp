@@ -22,7 +22,7 @@ extern "C" int vo_version(void) { return 1; }
 
 // experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0.
 // VO_TUNE="pair_cfg=1,conv_cfg=1" presets them for a whole process (bench A/B).
-static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg"};
+static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg", "rb3_cfg"};
 static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {0, 0, 0, 0};
 
 static void knobs_from_env() {
@@ -67,7 +67,7 @@ static const char* const kSymbols[] = {
     "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair", "vo_stft_mel_ex",
     "vo_pack_grouped",   "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
-    "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped",
+    "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -9,6 +9,7 @@ its input, the ResBlock residual / MRF sum / 1/num_kernels scale in its epilogue
 each ConvTranspose1d upsampler in its polyphase form.
 """
 
+import os
 import warnings
 
 import torch
@@ -19,6 +20,8 @@ from .. import ops
 from .._base import HipModule
 
 LRELU_SLOPE = 0.1
+# K = 3 ResBlocks as one vo_resblock3 launch (VO_RB3=0: three vo_resblock_pair launches, for A/B)
+RB3_ENABLED = os.environ.get("VO_RB3", "1") != "0"
 
 with warnings.catch_warnings():
     warnings.simplefilter("ignore")
@@ -85,6 +88,13 @@ class ResBlock(HipModule):
         packs = self._packed(x.device, self._build)
         k, C = self.kernel_size, self.channels
         cur = x
+        if (RB3_ENABLED and k == 3 and len(self.dilation) == 3 and C in self.fused_pair_channels
+                and x.dtype == self.compute_dtype == torch.bfloat16
+                and sum(d + 1 for d in self.dilation) <= 12 and max(self.dilation) <= 8):
+            # k = 3: the whole ResBlock (three pairs) in one launch; x1 / x2 stay on chip
+            (w1s, b1s), (w2s, b2s) = zip(*[p[0] for p in packs]), zip(*[p[1] for p in packs])
+            return ops.resblock3(cur, w1s, b1s, w2s, b2s, self.dilation, LRELU_SLOPE, out=out,
+                                 out_scale=out_scale, acc=accumulate, tag=tag)
         if C in self.fused_pair_channels and x.dtype == self.compute_dtype == torch.bfloat16:
             # narrow stages: one fused launch per (c1, c2) pair, the intermediate stays in LDS
             for n, (d, ((w1, b1), (w2, b2))) in enumerate(zip(self.dilation, packs)):

@@ -354,6 +354,32 @@ def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0,
     return out
 
 
+def resblock3(x, w1s, b1s, w2s, b2s, dils, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None):
+    """A whole K = 3 ResBlock1 (three (c1_d, c2) pairs) in one launch (vo_resblock3):
+    y = x_3 * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64, 128}; w1s / w2s: three packed
+    [3][C][C] bf16 weights each, b1s / b2s three fp32 biases, dils the three dilations."""
+    _contig(x, "x")
+    B, T, C = x.shape
+    if x.dtype != torch.bfloat16 or any(w.dtype != torch.bfloat16 for w in list(w1s) + list(w2s)):
+        raise TypeError("resblock3: bf16 activations and packed bf16 weights")
+    if not (len(w1s) == len(b1s) == len(w2s) == len(b2s) == len(dils) == 3):
+        raise ValueError("resblock3: three stages")
+    out = out if out is not None else torch.empty_like(x)
+    if acc is not None and (acc.shape != x.shape or acc.dtype != x.dtype):
+        raise ValueError("resblock3: acc must match x")
+    arr = lambda ts: (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ts])  # noqa: E731
+    dil = (ctypes.c_int * 3)(*[int(d) for d in dils])
+    timer = profiling.active()
+    ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
+    _lib.check(_lib.lib().vo_resblock3(_ptr(x), arr(w1s), arr(b1s), arr(w2s), arr(b2s), dil, _ptr(out), _ptr(acc),
+                                       B, T, C, float(slope), float(out_scale), _stream(x)), "vo_resblock3")
+    if ev is not None:
+        flops = 3 * 2.0 * 2.0 * B * T * C * C * 3
+        nbytes = 2.0 * x.numel() * 2 + (x.numel() * 2 if acc is not None else 0) + 6 * w1s[0].numel() * 2
+        timer.stop(tag, ev, flops, nbytes, kernel=f"mrf_rb3_kernel<C={C}, ...>")
+    return out
+
+
 # ----------------------------------------------------------------------------- mel / STFT
 
 def stft_mel(wav, window, fb, n_fft=1024, hop=256, n_mels=80, log_floor=1e-5):
