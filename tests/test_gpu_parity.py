@@ -309,10 +309,15 @@ def test_conv1d_mrf_stage0_tiles(B, T, C, K, dil, cfg):
     assert rel_l2(out.float().cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,L,lens", [(4, 512, [512, 300, 1, 77]), (2, 1000, [1000, 999]), (3, 12, [12, 7, 5])])
-@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])
-def test_attention_vs_oracle(B, L, lens, dt, tol):
-    from visual_onoma_to_wave_amd import ops
+@pytest.mark.parametrize("B,L,lens", [(4, 512, [512, 300, 1, 77]), (2, 1000, [1000, 999]), (3, 12, [12, 7, 5]),
+                                      (2, 64, [64, 63]), (2, 65, [65, 1]), (1, 1, [1]), (2, 129, [100, 129])])
+@pytest.mark.parametrize("dt,tol,cfg", [(torch.float32, F32_MOD, 0), (torch.bfloat16, 1e-2, 0),
+                                        (torch.bfloat16, 1e-2, 1)])
+def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
+    """vo_attention vs the PyTorch fp32 SDPA with key padding; bf16 for both kernels (att_cfg 0 =
+    the S^T / register-P kernel, 1 = the first version)."""
+    from visual_onoma_to_wave_amd import _lib, ops
+    _lib.lib().vo_tune(b"att_cfg", cfg)
     g = torch.Generator().manual_seed(L)
     qkv = torch.randn(B, L, 768, generator=g)
     lens_t = torch.tensor(lens, dtype=torch.int32)
@@ -322,7 +327,11 @@ def test_attention_vs_oracle(B, L, lens, dt, tol):
         s = q[..., h * 128:(h + 1) * 128] @ k[..., h * 128:(h + 1) * 128].transpose(1, 2) / 128 ** 0.5
         s = s.masked_fill(torch.arange(L)[None, None, :] >= lens_t[:, None, None], -float("inf"))
         ref[..., h * 128:(h + 1) * 128] = torch.softmax(s, -1) @ v[..., h * 128:(h + 1) * 128]
-    out = ops.attention(qkv.cuda().to(dt), lens_t.cuda(), 2)
+    try:
+        out = ops.attention(qkv.cuda().to(dt), lens_t.cuda(), 2)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().vo_tune(b"att_cfg", 0)
     assert rel_l2(out.float().cpu(), ref) < tol
 
 

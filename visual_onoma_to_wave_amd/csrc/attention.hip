@@ -163,6 +163,164 @@ __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ q
   }
 }
 
+// bf16 version 2: S^T = K Q^T instead of S = Q K^T, so a lane's accumulator column is ONE
+// query (lane & 15) over 16 keys: the running max / sum are per lane, the O^T rescale is a
+// per-lane scalar, and P^T feeds the B operand of O^T += V^T P^T straight from registers (the
+// keys of a 32-deep k-step taken in the order the accumulator holds them; the V^T operand is
+// read with the same key order by two ds_read_b64_tr_b16 per fragment from row-major V) -- no P
+// round trip through LDS, no transposed scalar V stores.  K / V tiles are double-buffered:
+// the next tile is fetched into registers while the current one is consumed (one barrier per
+// tile).
+template <int NONE = 0>
+__global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restrict__ qkv, const int32_t* __restrict__ lens,
+                                                         int L, int H, float scale, bf16_t* __restrict__ out) {
+  constexpr int P = ATT_DK + 16;  // row pitch (elements): 72 dwords = 8 mod 64 banks
+  __shared__ __attribute__((aligned(16))) bf16_t kv_lds[2][2][KT * P];  // [buf][K | V][key][dk]
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+  const int D = H * ATT_DK;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int q0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int len = min(lens ? lens[b] : L, L);
+  const int64_t row_stride = 3 * (int64_t)D;
+  const bf16_t* base = qkv + (int64_t)b * L * row_stride + h * ATT_DK;
+
+  // Q^T fragments (B operand): lane (g, lr) holds Q[q = q0 + 16 wave + lr][dk = 32 ks + 8 g + j]
+  Frag<bf16_t> qf[4];
+  const int qrow = q0 + 16 * wave + lr;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    if (qrow < L)
+      qf[ks].load(base + (int64_t)qrow * row_stride + 32 * ks + 8 * g);
+    else
+      qf[ks].zero();
+  }
+
+  // staging: 64 keys x 128 dk = 1024 16-byte vectors per matrix, 4 per thread
+  u4 kreg[4], vreg[4];
+  auto fetch = [&](int key0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int v = tid + 256 * s, kr = v >> 4, c8 = (v & 15) * 8;
+      const int key = min(key0 + kr, L - 1);  // rows past L are masked by len <= L
+      const bf16_t* rp = base + (int64_t)key * row_stride + c8;
+      kreg[s] = *reinterpret_cast<const u4*>(rp + D);
+      vreg[s] = *reinterpret_cast<const u4*>(rp + 2 * D);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int v = tid + 256 * s, kr = v >> 4, c8 = (v & 15) * 8;
+      *reinterpret_cast<u4*>(&kv_lds[buf][0][kr * P + c8]) = kreg[s];
+      *reinterpret_cast<u4*>(&kv_lds[buf][1][kr * P + c8]) = vreg[s];
+    }
+  };
+
+  f32x4 o[8];  // O^T: lane (g, lr) holds O[q = lr][d = 16 dt + 4 g + r]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int n_tiles = (len + KT - 1) / KT;
+  if (n_tiles > 0) {
+    fetch(0);
+    stash(0);
+  }
+  __syncthreads();
+  const int tq = lane >> 2 & 3, tp = lane & 3;  // transposed-read lane roles within 16 lanes
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int buf = kt & 1;
+    const int key0 = kt * KT;
+    if (kt + 1 < n_tiles) fetch(key0 + KT);
+    const bf16_t* K = kv_lds[buf][0];
+    const bf16_t* V = kv_lds[buf][1];
+    // S^T = K Q^T: 64 keys x 16 queries; s[nt] lane (g, lr): key 16 nt + 4 g + r, query lr
+    f32x4 sacc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sacc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        Frag<bf16_t> kf;
+        kf.load(K + (16 * nt + lr) * P + 32 * ks + 8 * g);
+        sacc[nt] = mfma(kf, qf[ks], sacc[nt]);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = key0 + 16 * nt + 4 * g + r;
+        const float sv = key < len ? sacc[nt][r] * scale : -INFINITY;
+        sacc[nt][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+    float sum = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = sacc[nt][r] == -INFINITY ? 0.f : __expf(sacc[nt][r] - m_new);
+        sacc[nt][r] = pv;
+        sum += pv;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l_run = l_run * alpha + sum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+    // O^T += V^T P^T over two 32-key steps; k index 8 g + j <-> key 32 ks + 4 g + j (j < 4),
+    // 32 ks + 16 + 4 g + j - 4 (j >= 4): exactly the keys this lane's sacc[2 ks], sacc[2 ks + 1] hold
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // whole-vector bit cast of packed words (per-element __bf16 inserts are mis-lowered by hipcc)
+      auto pk = [](float lo, float hi) {
+        return (unsigned)from_f32<bf16_t>(lo) | ((unsigned)from_f32<bf16_t>(hi) << 16);
+      };
+      const u4 pw = u4{pk(sacc[2 * ks][0], sacc[2 * ks][1]), pk(sacc[2 * ks][2], sacc[2 * ks][3]),
+                       pk(sacc[2 * ks + 1][0], sacc[2 * ks + 1][1]), pk(sacc[2 * ks + 1][2], sacc[2 * ks + 1][3])};
+      Frag<bf16_t> pf;
+      pf.v = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16_t* vb = V + (32 * ks + 4 * g + tq) * P + 16 * dt + 4 * tp;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)vb);
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(vb + 16 * P));
+        Frag<bf16_t> vf;
+        vf.v = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        o[dt] = mfma(vf, pf, o[dt]);
+      }
+    }
+    if (kt + 1 < n_tiles) stash(buf ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+  }
+
+  if (qrow >= L) return;
+  const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+  bf16_t* orow = out + ((int64_t)b * L + qrow) * D + h * ATT_DK;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint32_t w0 = (uint32_t)from_f32<bf16_t>(o[dt][0] * inv) | ((uint32_t)from_f32<bf16_t>(o[dt][1] * inv) << 16);
+    uint32_t w1 = (uint32_t)from_f32<bf16_t>(o[dt][2] * inv) | ((uint32_t)from_f32<bf16_t>(o[dt][3] * inv) << 16);
+    *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = make_uint2(w0, w1);
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -174,7 +332,10 @@ extern "C" int vo_attention(const void* qkv, int dtype, const int32_t* lens, int
   VO_CHECK_ARG(B > 0 && L > 0 && H > 0, "attention: empty");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)((L + 63) / 64), (unsigned)(B * H));
-  if (dtype == VO_BF16)
+  if (dtype == VO_BF16 && vo_tune_get("att_cfg") != 1)
+    hipLaunchKernelGGL(attention2_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
+                       (bf16_t*)out);
+  else if (dtype == VO_BF16)
     hipLaunchKernelGGL(attention_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
                        (bf16_t*)out);
   else if (dtype == VO_F32)

@@ -474,7 +474,14 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   }
   if (d->T_out <= 32 && d->Co >= 64) return launch_cfg<TIN, TC, TOUT, 2, 2, 4, 1, 4>(d, st);  // 128 x 32
   if (d->Co <= 32) return launch_cfg<TIN, TC, TOUT, 2, 4, 1, 4, 4>(d, st);   // 32 x 256
-  if (d->Co <= 64 || d->Co == 80) return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
+  if (d->Co <= 64 || d->Co == 80) {
+    // Co = 80 (PostNet output conv, mel_linear at B*T = 16384 rows): 64 x 128 tiles, twice the
+    // workgroups of 64 x 256 (512 -> 80 k5 36.7 -> 29.7 us; tools/probes/small_convs.py)
+    const int gc = vo_tune_get("gen_cfg");
+    if (gc == 6 || (d->Co == 80 && gc != 8)) return launch_cfg<TIN, TC, TOUT, 4, 2, 1, 4, 4>(d, st);  // 64 x 128
+    if (gc == 7) return launch_cfg<TIN, TC, TOUT, 4, 1, 1, 4, 4>(d, st);  // 64 x 64
+    return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
+  }
   if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2, 2>(d, st);  // 64 x 64
   if constexpr (sizeof(TC) == 2) {
     // decoder shapes at B*T = 16384 rows (tools/ab_sb.py gen): wide outputs (FFN w_1 k9 1024,
