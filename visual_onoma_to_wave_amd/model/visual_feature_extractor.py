@@ -55,20 +55,37 @@ class VisualFeatureExtractor(HipModule):
                 s, sh = fold_bn(m)
                 bns.append(torch.cat([s, sh]))
         lin = self.bridge[0]
-        return dict(conv=torch.stack(convs).to(device).contiguous(),
-                    bn=torch.stack(bns).to(device).contiguous(),
-                    w=ops.pack_conv_weight(lin.weight.to(device)[:, :, None], dtype),
-                    b=lin.bias.detach().float().to(device).contiguous())
+        d = dict(conv=torch.stack(convs).to(device).contiguous(),
+                 bn=torch.stack(bns).to(device).contiguous(),
+                 w=ops.pack_conv_weight(lin.weight.to(device)[:, :, None], dtype),
+                 b=lin.bias.detach().float().to(device).contiguous())
+        # the bridge is a 2448-deep reduction over only B * n rows: as one conv each workgroup
+        # walks 77 channel chunks in series (90 us at B = 32).  Split-K instead: S channel groups
+        # as a grouped conv (group g = input channels [g Ci/S, (g+1) Ci/S) -> its own E outputs),
+        # then the S partial sums are added in order (deterministic) -> 5 chunks per workgroup.
+        E, Ci = lin.weight.shape
+        S = next((s for s in (17, 16, 12, 8, 4, 2) if Ci % s == 0 and (Ci // s) % 8 == 0), 1)
+        if S > 1:
+            wg = lin.weight.detach().float().to(device).view(E, S, Ci // S).transpose(0, 1).reshape(S * E, Ci // S)
+            d.update(split=S, wsplit=ops.pack_grouped_weight(wg[:, :, None], dtype, groups=S))
+        return d
 
     def run(self, images, out_dtype=None):
         self._supported()
         p = self._packed(images.device, self._build)
         flat, n = ops.vfe_stencil(images, p["conv"], p["bn"], self.slice_width, self.compute_dtype)
         B = images.shape[0]
-        y = ops.conv1d(flat.unsqueeze(0), p["w"], p["b"], Co=self.embed_dim, K=1,
+        E = self.embed_dim
+        if p.get("split", 1) > 1 and flat.shape[0] <= 4096:
+            S = p["split"]
+            part = ops.conv1d(flat.unsqueeze(0), p["wsplit"], None, Co=S * E, K=1, groups=S,
+                              out_dtype=torch.float32, compute_dtype=self.compute_dtype)
+            y = torch.relu(part.view(-1, S, E).sum(1) + p["b"]).to(out_dtype or self.compute_dtype)
+            return y.view(B, n, E)
+        y = ops.conv1d(flat.unsqueeze(0), p["w"], p["b"], Co=E, K=1,
                        post_act=ops.ACT_RELU, out_dtype=out_dtype or self.compute_dtype,
                        compute_dtype=self.compute_dtype)
-        return y.view(B, n, self.embed_dim)
+        return y.view(B, n, E)
 
     def train_run(self, images, out_dtype):
         """Training forward (BatchNorm2d uses batch statistics, so the eval-folded stencil kernel
