@@ -296,8 +296,9 @@ def test_trainer_graphed_matches_eager():
     for k in le:
         assert abs(le[k] - lg[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, le[k], lg[k])
     # one AdamW step moves a weight by ~lr = 2e-4 (~4e-3 of its size): a replay that read a stale
-    # packed weight or input would differ at that scale; atomics reordering leaves ~1e-5
-    assert rel_l2(gg, ge) < 1e-4 and rel_l2(dg, de) < 1e-4
+    # packed weight or input would differ at that scale; atomics reordering leaves ~1e-5 on G and
+    # up to ~1e-4 on D (Adam's m / sqrt(v) amplifies reordering noise on near-zero gradients)
+    assert rel_l2(gg, ge) < 5e-4 and rel_l2(dg, de) < 5e-4, (rel_l2(gg, ge), rel_l2(dg, de))
 
 
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
