@@ -118,6 +118,17 @@ int vo_layernorm(const void* x, int x_dtype, const void* res, int res_dtype, con
                  const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
                  int y_dtype, void* stream);
 
+/* Backward of vo_layernorm (training, config C4): gh = dL/d(x + res) (the gradient of both x
+ * and res; 0 on pad rows), dgamma / dbeta (fp32, D) summed over the unmasked rows.  x / res /
+ * gh share x_dtype.  workspace: vo_layernorm_bwd_workspace_size(B, T, D) bytes (per-workgroup
+ * partial column sums, added in a fixed order: deterministic).
+ * Replaces: the autograd of nn.LayerNorm + masked_fill (scripts/transformer/SubLayers.py:55,91,
+ * scripts/transformer/Layers.py:25,28) under scripts/04_train.py:128-141. */
+int64_t vo_layernorm_bwd_workspace_size(int B, int T, int D);
+int vo_layernorm_bwd(const void* x, const void* res, int x_dtype, const void* gy, int gy_dtype,
+                     const float* gamma, const int32_t* lens, int B, int T, int D, float eps, void* gh,
+                     float* dgamma, float* dbeta, void* workspace, void* stream);
+
 /* ------------------------------------------------------------------ attention
  * Scaled dot-product attention with key padding, H heads of d_k = D/H, over the fused
  * qkv activations (B, L, 3D) (columns [q | k | v], head h at h*d_k) -> out (B, L, D)
@@ -128,6 +139,16 @@ int vo_layernorm(const void* x, int x_dtype, const void* res, int res_dtype, con
  * them: Models.py:119-124, 190-195). */
 int vo_attention(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
                  float scale, void* out, void* stream);
+
+/* Backward of vo_attention (training, config C4): dqkv (B, L, 3D) = [dQ | dK | dV] in the
+ * qkv layout, from qkv, the forward output out (B, L, D) and its gradient dout (B, L, D), all in
+ * `dtype`.  Flash-style: the row log-sum-exp is rebuilt from qkv, no L x L tensor is stored.
+ * workspace: vo_attention_bwd_workspace_size(B, L, H) bytes.  Masked keys get zero dK / dV.
+ * Replaces: the autograd of SubLayers.py:39-53 / Modules.py:14-25 under
+ * scripts/04_train.py:128-141. */
+int64_t vo_attention_bwd_workspace_size(int B, int L, int H);
+int vo_attention_bwd(const void* qkv, const void* out, const void* dout, int dtype, const int32_t* lens, int B,
+                     int L, int H, int dk, float scale, void* dqkv, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------ length regulator
  * out[b, t, :] = x[b, j, :] for cs[j-1] <= t < cs[j] (cs = inclusive cumsum of

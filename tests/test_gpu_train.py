@@ -137,3 +137,76 @@ def test_graphed_train_step_matches_eager(device):
     # 25 -> 7.5: a replay with a stale input / learning rate / packed weight differs at that scale
     assert p_err < max(10 * p_noise, 1e-6) and p_err < 1e-3
     assert l_err < max(10 * l_noise, 1e-4)
+
+
+@pytest.mark.parametrize("dt,D,with_res,with_lens", [
+    (torch.float32, 256, True, True), (torch.float32, 256, False, False), (torch.bfloat16, 256, True, True),
+    (torch.float32, 512, True, False), (torch.bfloat16, 512, False, True)])
+@pytest.mark.parametrize("B,T", [(3, 37), (32, 512), (1, 1)])
+def test_layernorm_bwd_vs_torch(B, T, D, dt, with_res, with_lens):
+    """vo_layernorm_bwd vs the fp32 autograd of LayerNorm(x + res) + pad-row masked_fill."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(B * T + D)
+    x = torch.randn(B, T, D, generator=gen).to(dt)
+    res = torch.randn(B, T, D, generator=gen).to(dt) if with_res else None
+    gy = torch.randn(B, T, D, generator=gen).to(dt)
+    g = 1.0 + 0.1 * torch.randn(D, generator=gen)
+    bta = 0.1 * torch.randn(D, generator=gen)
+    lens = torch.randint(1, T + 1, (B,), generator=gen).int() if with_lens else None
+    xi = x.float().requires_grad_(True)
+    gi, bi = g.clone().requires_grad_(True), bta.clone().requires_grad_(True)
+    h = xi + res.float() if with_res else xi
+    y = F.layer_norm(h, (D,), gi, bi, 1e-5)
+    if with_lens:
+        y = y.masked_fill((torch.arange(T)[None, :] >= lens.long()[:, None])[..., None], 0.0)
+    rx, rg, rb = torch.autograd.grad(y, (xi, gi, bi), gy.float())
+    gh, dg, db = ops.layernorm_bwd(x.cuda(), gy.cuda(), g.cuda(), res=res.cuda() if with_res else None,
+                                   lens=lens.cuda() if with_lens else None)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert gh.dtype == dt and rel_l2(gh.float().cpu(), rx) < tol
+    assert rel_l2(dg.cpu(), rg) < 1e-5 and rel_l2(db.cpu(), rb) < 1e-5
+
+
+def _torch_attention(qkv, lens, n_head):
+    """fp32 reference of vo_attention: head split of SubLayers.py:39-46, SDPA of Modules.py:14-25
+    with the key-padding mask of Models.py:104 / 187."""
+    B, L, D3 = qkv.shape
+    D = D3 // 3
+    dk = D // n_head
+    q, k, v = (t.reshape(B, L, n_head, dk).transpose(1, 2) for t in qkv.split(D, dim=-1))
+    s = q @ k.transpose(-1, -2) / dk ** 0.5
+    mask = torch.arange(L)[None, None, None, :] >= lens.long()[:, None, None, None]
+    p = torch.softmax(s.masked_fill(mask, float("-inf")), dim=-1)
+    return (p @ v).transpose(1, 2).reshape(B, L, D)
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,L,H,ragged", [(2, 12, 2, True), (4, 512, 2, True), (3, 100, 2, False),
+                                          (2, 1, 2, False), (1, 1000, 2, True), (2, 130, 1, True)])
+def test_attention_bwd_vs_torch(B, L, H, ragged, dt, tol):
+    """vo_attention_bwd (dQ | dK | dV) vs the fp32 autograd of the reference SDPA, ragged key
+    padding, L not a multiple of the 64-row tiles."""
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(B * L + H)
+    D = 128 * H
+    qkv = torch.randn(B, L, 3 * D, generator=gen).to(dt)
+    lens = torch.randint(1, L + 1, (B,), generator=gen).int() if ragged else torch.full((B,), L, dtype=torch.int32)
+    gout = torch.randn(B, L, D, generator=gen).to(dt)
+    qi = qkv.float().requires_grad_(True)
+    ref_out = _torch_attention(qi, lens, H)
+    (ref,) = torch.autograd.grad(ref_out, qi, gout.float())
+    qc, lc = qkv.cuda(), lens.cuda()
+    out = ops.attention(qc, lc, H)
+    got = ops.attention_bwd(qc, out, gout.cuda(), lc, H)
+    assert got.dtype == dt and got.shape == qkv.shape
+    got = got.float().cpu()
+    for part in range(3):  # dQ, dK, dV separately (padded keys: exactly zero)
+        sl = slice(part * D, (part + 1) * D)
+        # L = 1: softmax over one key is constant, so the reference dQ / dK are exactly 0 and
+        # ours carry the rounding of P (dP - rowsum(dO o O)); the floor scales with |dO|
+        err = float((got[..., sl] - ref[..., sl]).norm())
+        den = max(float(ref[..., sl].norm()), 1e-2 * float(gout.float().norm()))
+        assert err < tol * den, (part, err / den)
+    for bi in range(B):
+        assert torch.count_nonzero(got[bi, int(lens[bi]):, D:]) == 0

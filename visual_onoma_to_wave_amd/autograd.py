@@ -6,8 +6,11 @@ The forward of every op is the same HIP kernel the inference path runs.  Backwar
   re-packed taps-reversed / channels-swapped (``vo_pack_weight`` mode DGRAD);
 * Conv1d / Linear weight and bias gradients: HIP -- ``vo_conv1d_wgrad`` (MFMA, fragments
   read transposed from LDS) and ``vo_colsum``;
-* attention, LayerNorm and LengthRegulator backward: PyTorch-ROCm recomputation -- the
-  initial fallback SURVEY.md 8(b) sanctions for C4.
+* LayerNorm backward: HIP -- ``vo_layernorm_bwd`` (row-wise input gradient, deterministic
+  gamma / beta column sums);
+* attention backward: HIP -- ``vo_attention_bwd`` (flash-style: the row log-sum-exp is rebuilt
+  from q / k, dQ and dK / dV in two MFMA kernels, nothing of size L x L stored);
+* LengthRegulator backward: a PyTorch scatter-add over the forward's frame -> token index.
 
 All functions take and return channels-last (B, T, C) activations.
 """
@@ -46,8 +49,11 @@ class Conv1dFn(torch.autograd.Function):
                             pad=(K - 1) * dil - pad, T_out=x.shape[1], out_dtype=x.dtype, compute_dtype=cdt)
         if ctx.needs_input_grad[1]:
             if x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
-                # MFMA weight gradient over transposed LDS reads (vo_conv1d_wgrad)
-                gw = ops.conv1d_wgrad(gz.to(x.dtype).contiguous(), x.contiguous(), K, dil=dil, pad=pad).to(w.dtype)
+                # MFMA weight gradient over transposed LDS reads (vo_conv1d_wgrad), in the forward's
+                # compute dtype (an fp32 activation feeding a bf16 conv -- PostNet after its fp32
+                # BatchNorm -- was contracted in bf16 by the forward too)
+                gw = ops.conv1d_wgrad(gz.to(cdt).contiguous(), x.to(cdt).contiguous(), K, dil=dil,
+                                      pad=pad).to(w.dtype)
             else:
                 gw = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), w.shape, gz.float().transpose(1, 2),
                                                  padding=pad, dilation=dil)
@@ -64,36 +70,18 @@ def linear(x, weight, bias, relu=False, compute_dtype=torch.bfloat16, out_dtype=
     return conv1d(x, weight[:, :, None], bias, 1, 1, 0, relu, compute_dtype, out_dtype)
 
 
-def _ref_attention(qkv, lens, n_head):
-    B, L, D3 = qkv.shape
-    D = D3 // 3
-    dk = D // n_head
-    q, k, v = qkv.float().split(D, dim=-1)
-    q = q.view(B, L, n_head, dk).transpose(1, 2)
-    k = k.view(B, L, n_head, dk).transpose(1, 2)
-    v = v.view(B, L, n_head, dk).transpose(1, 2)
-    s = q @ k.transpose(-1, -2) / dk ** 0.5
-    mask = torch.arange(L, device=qkv.device)[None, None, None, :] >= lens.long()[:, None, None, None]
-    p = torch.softmax(s.masked_fill(mask, float("-inf")), dim=-1)
-    p = torch.nan_to_num(p, nan=0.0)
-    return (p @ v).transpose(1, 2).reshape(B, L, D)
-
-
 class AttentionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, lens, n_head):
-        ctx.save_for_backward(qkv, lens)
+        out = ops.attention(qkv.contiguous(), lens, n_head)
+        ctx.save_for_backward(qkv, lens, out)
         ctx.n_head = n_head
-        return ops.attention(qkv.contiguous(), lens, n_head)
+        return out
 
     @staticmethod
     def backward(ctx, go):
-        qkv, lens = ctx.saved_tensors
-        with torch.enable_grad():
-            q = qkv.detach().float().requires_grad_(True)
-            out = _ref_attention(q, lens, ctx.n_head)
-            (g,) = torch.autograd.grad(out, q, go.float())
-        return g.to(qkv.dtype), None, None
+        qkv, lens, out = ctx.saved_tensors
+        return ops.attention_bwd(qkv.contiguous(), out, go.to(qkv.dtype).contiguous(), lens, ctx.n_head), None, None
 
 
 def attention(qkv, lens, n_head):
@@ -112,22 +100,13 @@ class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, res, g, b, lens = ctx.saved_tensors
-        with torch.enable_grad():
-            xi = x.detach().float().requires_grad_(True)
-            ri = res.detach().float().requires_grad_(True) if res is not None else None
-            gi = g.detach().requires_grad_(True)
-            bi = b.detach().requires_grad_(True)
-            h = xi + ri if ri is not None else xi
-            y = F.layer_norm(h, (h.shape[-1],), gi, bi, 1e-5)
-            if lens is not None:
-                pad = torch.arange(y.shape[1], device=y.device)[None, :] >= lens.long()[:, None]
-                y = y.masked_fill(pad[..., None], 0.0)
-            ins = [t for t in (xi, ri, gi, bi) if t is not None]
-            grads = torch.autograd.grad(y, ins, gy.float())
-        gx = grads[0].to(x.dtype)
-        gr = grads[1].to(res.dtype) if res is not None else None
-        gg, gb = grads[-2], grads[-1]
-        return gx, gr, gg, gb, None
+        xr = x.contiguous()
+        rr = res.contiguous() if res is not None else None
+        if rr is not None and rr.dtype != xr.dtype:
+            rr = rr.to(xr.dtype)
+        gh, gg, gb = ops.layernorm_bwd(xr, gy.contiguous(), g.detach().float().contiguous(), res=rr, lens=lens)
+        gr = (gh if res.dtype == gh.dtype else gh.to(res.dtype)) if res is not None else None
+        return gh, gr, gg.to(g.dtype), gb.to(b.dtype), None
 
 
 def layernorm(x, res, g, b, lens=None):
@@ -180,7 +159,7 @@ def batch_norm_train(x, bn, dims):
     y = xc * torch.rsqrt(var + bn.eps)
     if bn.affine:
         y = y * bn.weight.view(shape) + bn.bias.view(shape)
-    return y
+    return y.to(x.dtype)  # stay in the activation dtype (fp32 affine params would promote bf16)
 
 
 def length_regulate(x, dur, max_len, out_dtype=None):

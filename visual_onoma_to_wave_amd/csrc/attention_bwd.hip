@@ -1,0 +1,373 @@
+// Flash-style backward of the key-padded scaled-dot-product attention (training, config C4).
+//
+// Replaces the PyTorch autograd recomputation of MultiHeadAttention's head split +
+// ScaledDotProductAttention (scripts/transformer/SubLayers.py:39-53, Modules.py:14-25) under
+// scripts/04_train.py:128-141.  With S = Q K^T * scale (keys >= len at -inf), P = softmax(S):
+//   dV = P^T dO,  dP = dO V^T,  dS = P o (dP - rowsum(dO o O)),  dQ = dS K * scale,
+//   dK = dS^T Q * scale
+// Nothing of size L x L reaches HBM.  Two kernels, no atomics:
+//   attn_bwd_dq_kernel   -- one workgroup per 64 queries of one (batch, head): pass 1 rebuilds
+//                           the row log-sum-exp over the key tiles, pass 2 forms P, dP, dS and
+//                           accumulates dQ; writes LSE and D = rowsum(dO o O) to the workspace.
+//   attn_bwd_dkdv_kernel -- one workgroup per 64 keys: loops over query tiles in transposed
+//                           form (S^T = K Q^T, dP^T = V dO^T; the key-side operands stay in
+//                           registers) and accumulates dK, dV.
+// The MFMA operand convention is the forward's (vo_common.h Frag / mfma): A = lane row lr,
+// k = lk..lk+7; B = lane column lr, k = lk..lk+7; C = lane rows 4g + r, column lr.  P / dS
+// go through a per-wave LDS tile to become A operands; the operands that need their
+// reduction index along keys / queries are staged transposed in LDS.
+// bf16 (P / dS rounded to bf16 as operands, fp32 accumulation) or fp32 (parity mode).
+
+#include "vo_common.h"
+
+namespace vo {
+
+constexpr int AB_DK = 128;
+constexpr int AB_KT = 64;  // keys per tile (dq kernel) / keys per workgroup (dkdv kernel)
+
+// stage ROWS rows of 128 channels (channel offset `col` in rows of pitch `ld` starting at `row0`)
+// row-major into dst (pitch AB_DK + 8) and, if dst_t, transposed into dst_t[c][row] (pitch TP)
+template <typename TC, int ROWS, int TP>
+__device__ __forceinline__ void ab_stage(const TC* __restrict__ src, int64_t ld, int row0, int nrows, int tid,
+                                         TC* __restrict__ dst, TC* __restrict__ dst_t) {
+  constexpr int P = AB_DK + 8;
+#pragma unroll
+  for (int s = 0; s < ROWS * 16 / 256; ++s) {
+    const int v = tid + 256 * s;
+    const int r = v >> 4, c8 = (v & 15) * 8;
+    float x[8];
+    if (row0 + r < nrows)
+      load8(src + (int64_t)(row0 + r) * ld + c8, x);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 0.f;
+    if (dst) store8(dst + r * P + c8, x);
+    if (dst_t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dst_t[(c8 + e) * TP + r] = from_f32<TC>(x[e]);
+  }
+}
+
+template <typename TC>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const TC* __restrict__ qkv, const TC* __restrict__ o,
+                                                          const TC* __restrict__ dout,
+                                                          const int32_t* __restrict__ lens, int L, int H,
+                                                          float scale, TC* __restrict__ dqkv,
+                                                          float* __restrict__ lse_ws, float* __restrict__ dd_ws) {
+  constexpr int KP = AB_DK + 8;
+  constexpr int TP = AB_KT + 8;
+  __shared__ __attribute__((aligned(16))) TC k_lds[AB_KT * KP];
+  __shared__ __attribute__((aligned(16))) TC v_lds[AB_KT * KP];
+  __shared__ __attribute__((aligned(16))) TC kt_lds[AB_DK * TP];
+  __shared__ __attribute__((aligned(16))) TC p_lds[4][16 * TP];
+  __shared__ float dd_lds[4][16];
+
+  const int D = H * AB_DK;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int q0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4, lk = g * 8;
+  const int len = lens ? min(lens[b], L) : L;
+  const int64_t rs = 3 * (int64_t)D;
+  const TC* base = qkv + (int64_t)b * L * rs;
+  const TC* kbase = base + D + h * AB_DK;
+  const TC* vbase = base + 2 * D + h * AB_DK;
+
+  // Q and dO fragments (A operands: row q, k = channel), D = rowsum(dO o O)
+  Frag<TC> qf[4], df[4];
+  float dpart = 0.f;
+  {
+    const int q = q0 + 16 * wave + lr;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (q < L) {
+        const int c = h * AB_DK + 32 * ks + lk;
+        qf[ks].load(base + (int64_t)q * rs + c);
+        df[ks].load(dout + ((int64_t)b * L + q) * D + c);
+        float ov[8], dv[8];
+        load8(o + ((int64_t)b * L + q) * D + c, ov);
+        load8(dout + ((int64_t)b * L + q) * D + c, dv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dpart += ov[e] * dv[e];
+      } else {
+        qf[ks].zero();
+        df[ks].zero();
+      }
+    }
+  }
+  dpart += __shfl_xor(dpart, 16, 64);
+  dpart += __shfl_xor(dpart, 32, 64);
+  if (g == 0) dd_lds[wave][lr] = dpart;
+
+  // pass 1: row max / sum over the key tiles -> log-sum-exp
+  const int n_tiles = (len + AB_KT - 1) / AB_KT;
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m_run[r] = -INFINITY;
+    l_run[r] = 0.f;
+  }
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int key0 = kt * AB_KT;
+    __syncthreads();
+    ab_stage<TC, AB_KT, TP>(kbase, rs, key0, L, tid, k_lds, (TC*)nullptr);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        Frag<TC> kf;
+        kf.load(k_lds + (16 * nt + lr) * KP + 32 * ks + lk);
+        s[nt] = mfma(qf[ks], kf, s[nt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float sv = (key0 + 16 * nt + lr < len) ? s[nt][r] * scale : -INFINITY;
+        s[nt][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+      const float m_new = fmaxf(m_run[r], mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) sum += (s[nt][r] == -INFINITY) ? 0.f : __expf(s[nt][r] - m_new);
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) sum += __shfl_xor(sum, o2, 64);
+      l_run[r] = l_run[r] * ((m_run[r] == -INFINITY) ? 0.f : __expf(m_run[r] - m_new)) + sum;
+      m_run[r] = m_new;
+    }
+  }
+  float lse[4], ddr[4];
+  __syncthreads();  // dd_lds visible
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lse[r] = l_run[r] > 0.f ? m_run[r] + __logf(l_run[r]) : INFINITY;  // +inf: the row has no keys -> P = 0
+    ddr[r] = dd_lds[wave][4 * g + r];
+    const int q = q0 + 16 * wave + 4 * g + r;
+    if (lr == 0 && q < L) {
+      lse_ws[(int64_t)bh * L + q] = lse[r];
+      dd_ws[(int64_t)bh * L + q] = ddr[r];
+    }
+  }
+
+  // pass 2: P, dP, dS; dQ += dS K
+  f32x4 acc[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TC* pw = p_lds[wave];
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int key0 = kt * AB_KT;
+    __syncthreads();
+    ab_stage<TC, AB_KT, TP>(kbase, rs, key0, L, tid, k_lds, kt_lds);
+    ab_stage<TC, AB_KT, TP>(vbase, rs, key0, L, tid, v_lds, (TC*)nullptr);
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        Frag<TC> kf, vf;
+        kf.load(k_lds + (16 * nt + lr) * KP + 32 * ks + lk);
+        vf.load(v_lds + (16 * nt + lr) * KP + 32 * ks + lk);
+        s[nt] = mfma(qf[ks], kf, s[nt]);
+        dp[nt] = mfma(df[ks], vf, dp[nt]);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = key0 + 16 * nt + lr < len;
+        const float p = valid ? __expf(s[nt][r] * scale - lse[r]) : 0.f;
+        pw[(4 * g + r) * TP + 16 * nt + lr] = from_f32<TC>(p * (dp[nt][r] - ddr[r]));
+      }
+    __syncthreads();
+    Frag<TC> sf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) sf[ks].load(pw + lr * TP + 32 * ks + lk);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        Frag<TC> kf;
+        kf.load(kt_lds + (16 * dt + lr) * TP + 32 * ks + lk);
+        acc[dt] = mfma(sf[ks], kf, acc[dt]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 16 * wave + 4 * g + r;
+    if (q >= L) continue;
+    TC* row = dqkv + ((int64_t)b * L + q) * rs + h * AB_DK;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) row[16 * dt + lr] = from_f32<TC>(acc[dt][r] * scale);
+  }
+}
+
+template <typename TC, int QT>
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const TC* __restrict__ qkv, const TC* __restrict__ dout,
+                                                            const int32_t* __restrict__ lens, int L, int H,
+                                                            float scale, TC* __restrict__ dqkv,
+                                                            const float* __restrict__ lse_ws,
+                                                            const float* __restrict__ dd_ws) {
+  constexpr int NT = QT / 16, KS = QT / 32;
+  constexpr int QP = AB_DK + 8;
+  constexpr int TP = QT + 8;
+  __shared__ __attribute__((aligned(16))) TC q_lds[QT * QP];
+  __shared__ __attribute__((aligned(16))) TC do_lds[QT * QP];
+  __shared__ __attribute__((aligned(16))) TC qt_lds[AB_DK * TP];
+  __shared__ __attribute__((aligned(16))) TC dot_lds[AB_DK * TP];
+  __shared__ __attribute__((aligned(16))) TC pt_lds[4][16 * TP];
+  __shared__ __attribute__((aligned(16))) TC st_lds[4][16 * TP];
+  __shared__ float lse_s[QT], dd_s[QT];
+
+  const int D = H * AB_DK;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int k0 = blockIdx.x * AB_KT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4, lk = g * 8;
+  const int len = lens ? min(lens[b], L) : L;
+  const int64_t rs = 3 * (int64_t)D;
+  const TC* base = qkv + (int64_t)b * L * rs;
+
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (k0 < len) {  // workgroup-uniform: a tile of padded keys only gets zero gradients
+    Frag<TC> kf[4], vf[4];
+    {
+      const int key = k0 + 16 * wave + lr;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (key < L) {
+          kf[ks].load(base + (int64_t)key * rs + D + h * AB_DK + 32 * ks + lk);
+          vf[ks].load(base + (int64_t)key * rs + 2 * D + h * AB_DK + 32 * ks + lk);
+        } else {
+          kf[ks].zero();
+          vf[ks].zero();
+        }
+      }
+    }
+    TC* pw = pt_lds[wave];
+    TC* sw = st_lds[wave];
+    const TC* dob = dout + (int64_t)b * L * D + h * AB_DK;
+    const int n_qt = (L + QT - 1) / QT;
+    for (int qt = 0; qt < n_qt; ++qt) {
+      const int qb = qt * QT;
+      __syncthreads();
+      ab_stage<TC, QT, TP>(base + h * AB_DK, rs, qb, L, tid, q_lds, qt_lds);
+      ab_stage<TC, QT, TP>(dob, D, qb, L, tid, do_lds, dot_lds);
+      if (tid < QT) {
+        const int q = qb + tid;
+        lse_s[tid] = q < L ? lse_ws[(int64_t)bh * L + q] : INFINITY;
+        dd_s[tid] = q < L ? dd_ws[(int64_t)bh * L + q] : 0.f;
+      }
+      __syncthreads();
+      // S^T = K Q^T, dP^T = V dO^T : lane holds [key = 4g + r][q = 16 nt + lr]
+      f32x4 st[NT], dpt[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        st[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dpt[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          Frag<TC> qf, df;
+          qf.load(q_lds + (16 * nt + lr) * QP + 32 * ks + lk);
+          df.load(do_lds + (16 * nt + lr) * QP + 32 * ks + lk);
+          st[nt] = mfma(kf[ks], qf, st[nt]);
+          dpt[nt] = mfma(vf[ks], df, dpt[nt]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int qq = 16 * nt + lr;
+        const float lq = lse_s[qq], dq = dd_s[qq];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool valid = k0 + 16 * wave + 4 * g + r < len;
+          const float p = valid ? __expf(st[nt][r] * scale - lq) : 0.f;
+          pw[(4 * g + r) * TP + qq] = from_f32<TC>(p);
+          sw[(4 * g + r) * TP + qq] = from_f32<TC>(p * (dpt[nt][r] - dq));
+        }
+      }
+      __syncthreads();
+      // dV += P^T dO, dK += dS^T Q : A = [key = lr][q = 32 ks + lk], B = [d = 16 dt + lr][q]
+      Frag<TC> pf[KS], sf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        pf[ks].load(pw + lr * TP + 32 * ks + lk);
+        sf[ks].load(sw + lr * TP + 32 * ks + lk);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          Frag<TC> a, c;
+          a.load(dot_lds + (16 * dt + lr) * TP + 32 * ks + lk);
+          c.load(qt_lds + (16 * dt + lr) * TP + 32 * ks + lk);
+          dv[dt] = mfma(pf[ks], a, dv[dt]);
+          dk[dt] = mfma(sf[ks], c, dk[dt]);
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int key = k0 + 16 * wave + 4 * g + r;
+    if (key >= L) continue;
+    TC* row = dqkv + ((int64_t)b * L + key) * rs + h * AB_DK;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      row[D + 16 * dt + lr] = from_f32<TC>(dk[dt][r] * scale);
+      row[2 * D + 16 * dt + lr] = from_f32<TC>(dv[dt][r]);
+    }
+  }
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int64_t vo_attention_bwd_workspace_size(int B, int L, int H) {
+  return 2 * (int64_t)B * H * L * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_attention_bwd(const void* qkv, const void* out, const void* dout, int dtype, const int32_t* lens,
+                                int B, int L, int H, int dk, float scale, void* dqkv, void* workspace,
+                                void* stream) {
+  VO_CHECK_ARG(qkv && out && dout && dqkv && workspace, "attention_bwd: null pointer");
+  VO_CHECK_ARG(dk == AB_DK, "attention_bwd: d_k=%d unsupported (128)", dk);
+  VO_CHECK_ARG(B > 0 && L > 0 && H > 0, "attention_bwd: empty");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* lse = (float*)workspace;
+  float* dd = lse + (int64_t)B * H * L;
+  dim3 grid((unsigned)((L + 63) / 64), (unsigned)(B * H));
+  if (dtype == VO_BF16) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)out,
+                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, lse, dd);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<bf16_t, 64>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, (const float*)lse, (const float*)dd);
+  } else if (dtype == VO_F32) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, (const float*)out,
+                       (const float*)dout, lens, L, H, scale, (float*)dqkv, lse, dd);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<float, 32>), grid, dim3(256), 0, st, (const float*)qkv,
+                       (const float*)dout, lens, L, H, scale, (float*)dqkv, (const float*)lse, (const float*)dd);
+  } else {
+    vo_set_error("attention_bwd: bad dtype");
+    return VO_ERR_INVALID;
+  }
+  VO_RETURN_LAUNCH();
+}

@@ -68,6 +68,7 @@ static const char* const kSymbols[] = {
     "vo_pack_grouped",   "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
+    "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

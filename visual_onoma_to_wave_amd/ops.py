@@ -175,6 +175,28 @@ def layernorm(x, gamma, beta, res=None, lens=None, out=None, out_dtype=None, eps
     return out
 
 
+def layernorm_bwd(x, gy, gamma, res=None, lens=None, eps=1e-5):
+    """Backward of ``layernorm``: (gh, dgamma, dbeta); gh = dL/d(x + res) in x's dtype."""
+    B, T, D = x.shape
+    _contig(x, "x")
+    _contig(gy, "gy")
+    if res is not None:
+        _contig(res, "res")
+        if res.shape != x.shape or res.dtype != x.dtype:
+            raise ValueError("layernorm_bwd: res must match x in shape and dtype")
+    if gy.shape != x.shape:
+        raise ValueError("layernorm_bwd: gy shape mismatch")
+    L = _lib.lib()
+    gh = torch.empty_like(x)
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_layernorm_bwd_workspace_size(B, T, D)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_layernorm_bwd(_ptr(x), _ptr(res), vo_dtype(x), _ptr(gy), vo_dtype(gy), _ptr(gamma), _ptr(lens),
+                                  B, T, D, eps, _ptr(gh), _ptr(dg), _ptr(db), _ptr(ws), _stream(x)),
+               "vo_layernorm_bwd")
+    return gh, dg, db
+
+
 # ----------------------------------------------------------------------------- attention
 
 def attention(qkv, lens, n_head, out=None):
@@ -188,6 +210,28 @@ def attention(qkv, lens, n_head, out=None):
     _lib.check(_lib.lib().vo_attention(_ptr(qkv), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
                                        scale, _ptr(out), _stream(qkv)), "vo_attention")
     return out
+
+
+def attention_bwd(qkv, out, dout, lens, n_head):
+    """Backward of ``attention``: dqkv (B, L, 3D) in qkv's dtype from the forward output and its
+    gradient (flash-style recomputation, vo_attention_bwd)."""
+    for t, n in ((qkv, "qkv"), (out, "out"), (dout, "dout")):
+        _contig(t, n)
+    B, L, D3 = qkv.shape
+    D = D3 // 3
+    if out.shape != (B, L, D) or dout.shape != (B, L, D):
+        raise ValueError("attention_bwd: out / dout must be (B, L, D)")
+    if out.dtype != qkv.dtype or dout.dtype != qkv.dtype:
+        raise ValueError("attention_bwd: qkv, out and dout must share a dtype")
+    dk = D // n_head
+    L_ = _lib.lib()
+    dqkv = torch.empty_like(qkv)
+    ws = torch.empty(int(L_.vo_attention_bwd_workspace_size(B, L, n_head)) // 4, dtype=torch.float32,
+                     device=qkv.device)
+    _lib.check(L_.vo_attention_bwd(_ptr(qkv), _ptr(out), _ptr(dout), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
+                                   1.0 / float(dk) ** 0.5, _ptr(dqkv), _ptr(ws), _stream(qkv)),
+               "vo_attention_bwd")
+    return dqkv
 
 
 # ----------------------------------------------------------------------------- length regulator
