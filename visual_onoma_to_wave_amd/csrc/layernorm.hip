@@ -79,22 +79,25 @@ static int ln_launch(const void* x, const void* res, const float* g, const float
 // recomputes mean / rstd from x (+ res) and writes
 //   gh = rstd * (g*gy - mean(g*gy) - xhat * mean(g*gy * xhat))      (pad rows: 0)
 // which is the gradient of both x and res.  gamma / beta gradients are column sums over the
-// unmasked rows: each workgroup (4 waves x LN_BWD_RPW rows) reduces its rows in registers, then
+// unmasked rows: each workgroup (16 waves x LN_BWD_RPW rows) reduces its rows in registers, then
 // across its waves through LDS, and writes one partial row [2][D] to the workspace; a second
-// kernel adds the partials in workgroup order (deterministic, no atomics).
+// kernel adds the partials in workgroup order (deterministic, no atomics).  A wave issues the
+// loads of all its rows before the first reduction (the row chain is latency-, not
+// bandwidth-bound at 16 rows per wave: 37 us at C2 -> see DESIGN.md).
 // Replaces the PyTorch autograd recomputation of LayerNorm backward (SubLayers.py:55,91,
 // Layers.py:25,28 under 04_train.py:128-141).  HBM-bound: reads x, res, gy, writes gh.
-constexpr int LN_BWD_RPW = 16;  // rows per wave: 64 rows per workgroup, 256 partials at C2
+constexpr int LN_BWD_RPW = 4;   // rows per wave
+constexpr int LN_BWD_NW = 16;   // waves per workgroup: 64 rows, 256 partials at C2
 
 template <typename TX, typename TG, int NPL>
-__global__ void __launch_bounds__(256) layernorm_bwd_kernel(const TX* __restrict__ x, const TX* __restrict__ res,
-                                                            const TG* __restrict__ gy,
-                                                            const float* __restrict__ gamma,
-                                                            const int32_t* __restrict__ lens, int B, int T,
-                                                            float eps, TX* __restrict__ gh,
-                                                            float* __restrict__ partial) {
+__global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restrict__ x, const TX* __restrict__ res,
+                                                             const TG* __restrict__ gy,
+                                                             const float* __restrict__ gamma,
+                                                             const int32_t* __restrict__ lens, int B, int T,
+                                                             float eps, TX* __restrict__ gh,
+                                                             float* __restrict__ partial) {
   constexpr int D = NPL * 64;
-  __shared__ float red[4][2][D];
+  __shared__ float red[LN_BWD_NW][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c0 = lane * NPL;
   const int64_t rows = (int64_t)B * T;
@@ -105,61 +108,68 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const TX* __restrict
     accg[i] = 0.f;
     accb[i] = 0.f;
   }
-  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wv) * LN_BWD_RPW;
+  const int64_t row0 = ((int64_t)blockIdx.x * LN_BWD_NW + wv) * LN_BWD_RPW;
+  float v[LN_BWD_RPW][NPL], dy[LN_BWD_RPW][NPL];
+  bool live[LN_BWD_RPW];
+#pragma unroll
+  for (int r = 0; r < LN_BWD_RPW; ++r) {
+    const int64_t row = row0 + r;
+    bool ok = row < rows;
+    if (ok && lens) {
+      const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
+      ok = t < lens[b];
+    }
+    live[r] = ok;
+    const int64_t rr = ok ? row : 0;
+#pragma unroll
+    for (int i = 0; i < NPL; i += 4) {
+      float q[4], e[4], d[4];
+      load4(x + rr * D + c0 + i, q);
+      if (res)
+        load4(res + rr * D + c0 + i, e);
+      else
+        e[0] = e[1] = e[2] = e[3] = 0.f;
+      load4(gy + rr * D + c0 + i, d);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[r][i + k] = q[k] + e[k];
+        dy[r][i + k] = ok ? d[k] : 0.f;
+      }
+    }
+  }
+#pragma unroll
   for (int r = 0; r < LN_BWD_RPW; ++r) {
     const int64_t row = row0 + r;
     if (row >= rows) break;
-    const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
     TX* gr = gh + row * D + c0;
-    if (lens && t >= lens[b]) {
-      float z[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < NPL; i += 4) store4(gr + i, z);
-      continue;
-    }
-    float v[NPL], dy[NPL];
-#pragma unroll
-    for (int i = 0; i < NPL; i += 4) {
-      float q[4];
-      load4(x + row * D + c0 + i, q);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[i + e] = q[e];
-      if (res) {
-        load4(res + row * D + c0 + i, q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[i + e] += q[e];
-      }
-      load4(gy + row * D + c0 + i, q);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dy[i + e] = q[e];
-    }
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) s += v[i];
+    for (int i = 0; i < NPL; ++i) s += v[r][i];
     const float mean = wave_sum(s) * (1.0f / D);
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
-      v[i] -= mean;
-      ss += v[i] * v[i];
+      v[r][i] -= mean;
+      ss += v[r][i] * v[r][i];
     }
     const float rstd = rsqrtf(wave_sum(ss) * (1.0f / D) + eps);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
-      v[i] *= rstd;  // xhat
-      const float gd = g[i] * dy[i];
+      v[r][i] *= rstd;  // xhat
+      const float gd = g[i] * dy[r][i];
       s1 += gd;
-      s2 += gd * v[i];
-      accg[i] += dy[i] * v[i];
-      accb[i] += dy[i];
+      s2 += gd * v[r][i];
+      accg[i] += dy[r][i] * v[r][i];
+      accb[i] += dy[r][i];
     }
     const float m1 = wave_sum(s1) * (1.0f / D), m2 = wave_sum(s2) * (1.0f / D);
+    const float sc = live[r] ? rstd : 0.f;  // pad rows: zero gradient
 #pragma unroll
     for (int i = 0; i < NPL; i += 4) {
       float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = rstd * (g[i + e] * dy[i + e] - m1 - v[i + e] * m2);
+      for (int e = 0; e < 4; ++e) o[e] = sc * (g[i + e] * dy[r][i + e] - m1 - v[r][i + e] * m2);
       store4(gr + i, o);
     }
   }
@@ -169,36 +179,41 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const TX* __restrict
     red[wv][1][c0 + i] = accb[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+  for (int c = threadIdx.x; c < 2 * D; c += 1024) {
     const int k = c / D, col = c - k * D;
-    partial[(int64_t)blockIdx.x * 2 * D + c] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < LN_BWD_NW; ++w) t += red[w][k][col];
+    partial[(int64_t)blockIdx.x * 2 * D + c] = t;
   }
 }
 
 // dgamma / dbeta: sum the per-workgroup partials [nblk][2][D] column-wise in a fixed order.
-// Workgroup = 64 columns x 4 row phases; phase s adds partials s, s + 4, ... (8 loads in flight
-// per thread), then the 4 phases are added in LDS.
-__global__ void __launch_bounds__(256) ln_partial_sum_kernel(const float* __restrict__ partial, int nblk, int D2,
-                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
+// Workgroup = 64 columns x 16 row phases; phase s adds partials s, s + 16, ... (4 loads in
+// flight per thread), then the 16 phases are added in LDS.
+__global__ void __launch_bounds__(1024) ln_partial_sum_kernel(const float* __restrict__ partial, int nblk, int D2,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
   if (c < D2) {
     int k = ph;
-    for (; k + 28 < nblk; k += 32) {
-      float v[8];
+    for (; k + 48 < nblk; k += 64) {
+      float v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = partial[(int64_t)(k + 4 * u) * D2 + c];
+      for (int u = 0; u < 4; ++u) v[u] = partial[(int64_t)(k + 16 * u) * D2 + c];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 4; ++u) s += v[u];
     }
-    for (; k < nblk; k += 4) s += partial[(int64_t)k * D2 + c];
+    for (; k < nblk; k += 16) s += partial[(int64_t)k * D2 + c];
   }
   red[ph][cl] = s;
   __syncthreads();
   if (ph == 0 && c < D2) {
-    const float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][cl];
     const int D = D2 / 2;
     if (c < D)
       dgamma[c] = t;
@@ -212,14 +227,14 @@ static int ln_bwd_launch(const void* x, const void* res, const void* gy, const f
                          int B, int T, int D, float eps, void* gh, float* dgamma, float* dbeta, float* ws,
                          hipStream_t st) {
   const int64_t rows = (int64_t)B * T;
-  const int nblk = (int)((rows + 4 * LN_BWD_RPW - 1) / (4 * LN_BWD_RPW));
+  const int nblk = (int)((rows + LN_BWD_NW * LN_BWD_RPW - 1) / (LN_BWD_NW * LN_BWD_RPW));
   if (D == 256)
-    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 4>), dim3(nblk), dim3(256), 0, st, (const TX*)x,
+    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 4>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
                        (const TX*)res, (const TG*)gy, g, lens, B, T, eps, (TX*)gh, ws);
   else
-    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 8>), dim3(nblk), dim3(256), 0, st, (const TX*)x,
+    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 8>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
                        (const TX*)res, (const TG*)gy, g, lens, B, T, eps, (TX*)gh, ws);
-  hipLaunchKernelGGL(ln_partial_sum_kernel, dim3((2 * D + 63) / 64), dim3(256), 0, st, (const float*)ws, nblk,
+  hipLaunchKernelGGL(ln_partial_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, st, (const float*)ws, nblk,
                      2 * D, dgamma, dbeta);
   VO_RETURN_LAUNCH();
 }
@@ -248,7 +263,7 @@ extern "C" int vo_layernorm(const void* x, int x_dtype, const void* res, int res
 
 extern "C" int64_t vo_layernorm_bwd_workspace_size(int B, int T, int D) {
   const int64_t rows = (int64_t)B * T;
-  return ((rows + 4 * LN_BWD_RPW - 1) / (4 * LN_BWD_RPW)) * 2 * D * (int64_t)sizeof(float);
+  return ((rows + LN_BWD_NW * LN_BWD_RPW - 1) / (LN_BWD_NW * LN_BWD_RPW)) * 2 * D * (int64_t)sizeof(float);
 }
 
 extern "C" int vo_layernorm_bwd(const void* x, const void* res, int x_dtype, const void* gy, int gy_dtype,
