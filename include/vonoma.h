@@ -159,6 +159,14 @@ int vo_attention_bwd(const void* qkv, const void* out, const void* dout, int dty
 int vo_length_regulate(const void* x, int x_dtype, const float* dur, int B, int T_src, int D,
                        int max_len, void* out, int out_dtype, int64_t* mel_len, int32_t* index,
                        void* stream);
+
+/* Backward of vo_length_regulate (training, config C4): gx[b, j, :] = sum of go[b, t, :] over
+ * the frames t in [cs[j-1], min(cs[j], max_len)) that token j was copied to (frames past the
+ * crop get no gradient), summed in frame order (deterministic).  go (B, max_len, D), gx
+ * (B, T_src, D); D % 8 == 0.  Replaces: the autograd of LengthRegulator.LR/expand + pad
+ * (scripts/model/modules.py:132-159, scripts/utils/tools.py:669-687). */
+int vo_length_regulate_bwd(const void* go, int go_dtype, const float* dur, int B, int T_src, int D, int max_len,
+                           void* gx, int gx_dtype, void* stream);
 /* mel_len only (int64 and int32 copies), so the host can size the output. */
 int vo_lr_lengths(const float* dur, int B, int T_src, int64_t* mel_len, int32_t* mel_len32,
                   void* stream);

@@ -210,3 +210,29 @@ def test_attention_bwd_vs_torch(B, L, H, ragged, dt, tol):
         assert err < tol * den, (part, err / den)
     for bi in range(B):
         assert torch.count_nonzero(got[bi, int(lens[bi]):, D:]) == 0
+
+
+@pytest.mark.parametrize("go_dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("max_len_delta", [0, 7, -5])
+def test_length_regulate_bwd_vs_torch(go_dt, max_len_delta):
+    """vo_length_regulate_bwd vs the autograd of the reference expand + pad / crop
+    (modules.py:132-159, tools.py:669-687): fractional (truncated), zero and negative
+    durations, padded and cropped outputs."""
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(7 + max_len_delta)
+    B, T, D = 3, 13, 256
+    dur = torch.rand(B, T, generator=gen) * 9.0 - 1.0  # [-1, 8): negatives and fractions
+    dur[0, 3] = 0.0
+    reps = torch.clamp(torch.trunc(dur), min=0).long()
+    max_len = int(reps.sum(1).max()) + max_len_delta
+    x = torch.randn(B, T, D, generator=gen).requires_grad_(True)
+    outs = []
+    for b in range(B):
+        e = torch.cat([x[b, j:j + 1].expand(int(reps[b, j]), D) for j in range(T)], 0)
+        e = e[:max_len] if e.shape[0] > max_len else torch.nn.functional.pad(e, (0, 0, 0, max_len - e.shape[0]))
+        outs.append(e)
+    ref_out = torch.stack(outs)
+    go = torch.randn(B, max_len, D, generator=gen).to(go_dt)
+    (ref,) = torch.autograd.grad(ref_out, x, go.float())
+    got = ops.length_regulate_bwd(go.cuda(), dur.cuda(), T, out_dtype=torch.float32).cpu()
+    assert rel_l2(got, ref) < 1e-6

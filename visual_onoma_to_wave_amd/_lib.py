@@ -85,6 +85,8 @@ _SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p]),
     "vo_length_regulate": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                    c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_length_regulate_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p]),
     "vo_lr_lengths": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_variance_head": (c_int, [ctypes.POINTER(HeadDesc), c_void_p]),
     "vo_vfe_stencil": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

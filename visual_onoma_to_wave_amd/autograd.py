@@ -10,7 +10,8 @@ The forward of every op is the same HIP kernel the inference path runs.  Backwar
   gamma / beta column sums);
 * attention backward: HIP -- ``vo_attention_bwd`` (flash-style: the row log-sum-exp is rebuilt
   from q / k, dQ and dK / dV in two MFMA kernels, nothing of size L x L stored);
-* LengthRegulator backward: a PyTorch scatter-add over the forward's frame -> token index.
+* LengthRegulator backward: HIP -- ``vo_length_regulate_bwd`` (segmented frame sums per token,
+  deterministic).
 
 All functions take and return channels-last (B, T, C) activations.
 """
@@ -116,9 +117,8 @@ def layernorm(x, res, g, b, lens=None):
 class LengthRegulateFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, dur, max_len, out_dtype):
-        out, mel_len, idx = ops.length_regulate(x.contiguous(), dur, int(max_len), out_dtype=out_dtype,
-                                                want_index=True)
-        ctx.save_for_backward(idx)
+        out, mel_len, _ = ops.length_regulate(x.contiguous(), dur, int(max_len), out_dtype=out_dtype)
+        ctx.save_for_backward(dur)
         ctx.shape = x.shape
         ctx.xdtype = x.dtype
         ctx.mark_non_differentiable(mel_len)
@@ -126,12 +126,8 @@ class LengthRegulateFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, go, _gm):
-        (idx,) = ctx.saved_tensors
-        B, T, D = ctx.shape
-        gx = torch.zeros((B, T + 1, D), dtype=torch.float32, device=go.device)
-        src = torch.where(idx >= 0, idx, torch.full_like(idx, T)).long()
-        gx.scatter_add_(1, src[..., None].expand(-1, -1, D), go.float())
-        return gx[:, :T].to(ctx.xdtype), None, None, None
+        (dur,) = ctx.saved_tensors
+        return ops.length_regulate_bwd(go.contiguous(), dur, ctx.shape[1], out_dtype=ctx.xdtype), None, None, None
 
 
 def batch_norm_train(x, bn, dims):

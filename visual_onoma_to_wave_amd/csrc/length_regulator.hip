@@ -83,6 +83,48 @@ __global__ void __launch_bounds__(256) lr_gather_kernel(const TX* __restrict__ x
   }
 }
 
+// Backward (training, C4): gx[b, j, :] = sum of go[b, t, :] over the frames token j was copied
+// to, t in [cs[j-1], min(cs[j], max_len)) -- a segmented row sum (frames of one token are
+// contiguous), added in frame order: deterministic, no atomics, no index tensor.  One workgroup
+// per (token, utterance); 256 threads = 8 frame phases x 32 threads of 8 channels (D <= 256 per
+// pass, looped for wider rows), the phases added in LDS in a fixed order.
+// Replaces the autograd of the LR concat / pad (modules.py:132-159, tools.py:669-687).
+template <typename TG, typename TX>
+__global__ void __launch_bounds__(256) lr_bwd_kernel(const TG* __restrict__ go, const float* __restrict__ dur,
+                                                     int T, int D, int max_len, TX* __restrict__ gx) {
+  __shared__ float red[8][256];
+  const int j = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, ph = tid >> 5, cl = (tid & 31) * 8;
+  int start = 0;
+  for (int i = 0; i < j; ++i) start += reps_of(dur[(int64_t)b * T + i]);
+  const int end = min(start + reps_of(dur[(int64_t)b * T + j]), max_len);
+  for (int c0 = 0; c0 < D; c0 += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c0 + cl < D)
+      for (int t = start + ph; t < end; t += 8) {
+        float v[8];
+        load8(go + ((int64_t)b * max_len + t) * D + c0 + cl, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[ph][cl + e] = acc[e];
+    __syncthreads();
+    if (ph == 0 && c0 + cl < D) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t += red[q][cl + e];
+        o[e] = t;
+      }
+      store8(gx + ((int64_t)b * T + j) * D + c0 + cl, o);
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -124,5 +166,27 @@ extern "C" int vo_length_regulate(const void* x, int x_dtype, const float* dur, 
     return VO_ERR_INVALID;
   }
 #undef VO_LR
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_length_regulate_bwd(const void* go, int go_dtype, const float* dur, int B, int T_src, int D,
+                                      int max_len, void* gx, int gx_dtype, void* stream) {
+  VO_CHECK_ARG(go && dur && gx, "length_regulate_bwd: null pointer");
+  VO_CHECK_ARG(B > 0 && T_src > 0 && max_len >= 0, "length_regulate_bwd: bad sizes");
+  VO_CHECK_ARG(D % 8 == 0 && D > 0, "length_regulate_bwd: D=%d must be a multiple of 8", D);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)T_src, (unsigned)B);
+#define VO_LRB(TG, TX)                                                                                        \
+  hipLaunchKernelGGL((lr_bwd_kernel<TG, TX>), grid, dim3(256), 0, st, (const TG*)go, dur, T_src, D, max_len, \
+                     (TX*)gx)
+  if (go_dtype == VO_BF16 && gx_dtype == VO_F32) VO_LRB(bf16_t, float);
+  else if (go_dtype == VO_F32 && gx_dtype == VO_F32) VO_LRB(float, float);
+  else if (go_dtype == VO_BF16 && gx_dtype == VO_BF16) VO_LRB(bf16_t, bf16_t);
+  else if (go_dtype == VO_F32 && gx_dtype == VO_BF16) VO_LRB(float, bf16_t);
+  else {
+    vo_set_error("length_regulate_bwd: bad dtypes");
+    return VO_ERR_INVALID;
+  }
+#undef VO_LRB
   VO_RETURN_LAUNCH();
 }

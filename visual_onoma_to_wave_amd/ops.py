@@ -261,6 +261,17 @@ def length_regulate(x, dur, max_len, out_dtype=None, want_index=False):
     return out, mel_len, index
 
 
+def length_regulate_bwd(go, dur, T_src, out_dtype=torch.float32):
+    """Backward of ``length_regulate``: go (B, max_len, D) -> gx (B, T_src, D)."""
+    _contig(go, "go")
+    dur = _contig(dur.float(), "dur")
+    B, max_len, D = go.shape
+    gx = torch.empty((B, T_src, D), dtype=out_dtype, device=go.device)
+    _lib.check(_lib.lib().vo_length_regulate_bwd(_ptr(go), vo_dtype(go), _ptr(dur), B, T_src, D, max_len, _ptr(gx),
+                                                 vo_dtype(gx), _stream(go)), "vo_length_regulate_bwd")
+    return gx
+
+
 # ----------------------------------------------------------------------------- variance heads
 
 def duration_head(h, w, b, lens, d_control=1.0, want_round=True):
