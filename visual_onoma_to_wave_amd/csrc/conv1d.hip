@@ -491,6 +491,14 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       if (d->Co >= 768 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
     }
+    // mid-width convs (PostNet 512 -> 512 k5, conv_pre 80 -> 512 k7 at 16384 rows): 128 x 256
+    // tiles (twice the rows per staged weight tap): 512 k5 67.9 -> 63.4 us, 80 k7 27.6 -> 27.0,
+    // bit-identical (tools/probes/mid_convs.py); the Co = 128 polyphase upsampler is slower with
+    // it (210 -> 234 us).  gen_cfg 9 forces it, gen_cfg 10 = 256 x 128 (no gain), gen_cfg 1 = 128 x 128.
+    const int gc = vo_tune_get("gen_cfg");
+    if (gc == 9 || (gc != 1 && gc != 10 && d->Co >= 512 && d->Co < 768 && d->Co % 128 == 0 && !d->transposed))
+      return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 4, 2>(d, st);  // 128 x 256
+    if (gc == 10) return launch_cfg<TIN, TC, TOUT, 4, 4, 4, 2, 2>(d, st);  // 256 x 128
   }
   return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }
