@@ -322,6 +322,13 @@ int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int
 int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
                             int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
                             int pre_b, float slope, int dtype, float* dw, void* stream);
+/* vo_conv1d_wgrad_grouped + the bias gradient in the same launch: db[g*M + m] += sum over all
+ * A rows of A[.., g*M + m] (the conv form, A = dY; pre_a must be 0), summed by the tap-0
+ * workgroups as they stage A.  db fp32 (groups*M), zeroed by the caller (one buffer with dw
+ * saves a fill and the separate vo_colsum launch). */
+int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
+                         int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
+                         int pre_b, float slope, int dtype, float* dw, float* db, void* stream);
 int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream);
 
 /* ------------------------------------------------------------------ training input pipeline

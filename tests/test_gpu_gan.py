@@ -375,3 +375,25 @@ def test_strided_grouped_dgrad_vs_torch(B, T, Ci, Co, K, s, g, pad, dt, tol):
     got = G._dgrad(gy.cuda().to(dt), w.cuda(), spec, x.cuda(), dt)
     assert got.shape == (B, T, Ci)
     assert rel_l2(got.float().cpu(), ref.transpose(1, 2)) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
+    (2, 1000, 32, 32, 11, 1, 1, 5), (3, 517, 256, 256, 3, 1, 1, 1), (2, 777, 128, 256, 41, 2, 16, 20),
+    (4, 100, 1024, 256, 1, 1, 1, 0), (1, 5, 64, 64, 7, 1, 1, 3), (2, 300, 80, 512, 7, 1, 1, 3)])
+def test_conv1d_wgrad_fused_bias(B, T, Ci, Co, K, s, g, pad, dt, tol):
+    """vo_conv1d_wgrad_bias: the bias gradient summed by the tap-0 workgroups equals the column
+    sums of dY (and the weight gradient is unchanged)."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(B * T + Ci + Co)
+    x = torch.randn(B, T, Ci, generator=gen).to(dt)
+    T_out = (T + 2 * pad - K) // s + 1
+    gy = torch.randn(B, T_out, Co, generator=gen).to(dt)
+    ref_w = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), (Co, Ci // g, K), gy.float().transpose(1, 2),
+                                        stride=s, padding=pad, groups=g)
+    ref_b = gy.float().sum((0, 1))
+    gw, gb = ops.conv1d_wgrad(gy.cuda(), x.cuda(), K, S=s, pad=pad, groups=g, with_bias=True)
+    assert rel_l2(gw.cpu(), ref_w) < tol
+    assert gb.shape == (Co,) and rel_l2(gb.cpu(), ref_b) < 1e-5
+    del F

@@ -106,6 +106,9 @@ _SIGNATURES = {
     "vo_conv1d_wgrad_grouped": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p,
                                         c_void_p]),
+    "vo_conv1d_wgrad_bias": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
+                                     c_void_p]),
     "vo_colsum": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p]),
     "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),

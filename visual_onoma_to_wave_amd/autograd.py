@@ -44,6 +44,7 @@ class Conv1dFn(torch.autograd.Function):
         if relu:
             gz = gz * (y > 0).to(gz.dtype)
         gx = gw = gb = None
+        want_b = has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[0]:
             wd = ops.pack_dgrad_weight(w, cdt)
             gx = ops.conv1d(gz.to(cdt) if gz.dtype != cdt else gz, wd, None, Co=w.shape[1], K=K, dil=dil,
@@ -53,12 +54,16 @@ class Conv1dFn(torch.autograd.Function):
                 # MFMA weight gradient over transposed LDS reads (vo_conv1d_wgrad), in the forward's
                 # compute dtype (an fp32 activation feeding a bf16 conv -- PostNet after its fp32
                 # BatchNorm -- was contracted in bf16 by the forward too)
-                gw = ops.conv1d_wgrad(gz.to(cdt).contiguous(), x.to(cdt).contiguous(), K, dil=dil,
-                                      pad=pad).to(w.dtype)
+                fuse_b = want_b and gz.dtype == cdt  # bias = column sums of the same dY (no cast)
+                r = ops.conv1d_wgrad(gz.to(cdt).contiguous(), x.to(cdt).contiguous(), K, dil=dil, pad=pad,
+                                     with_bias=fuse_b)
+                if fuse_b:
+                    r, gb = r
+                gw = r.to(w.dtype)
             else:
                 gw = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), w.shape, gz.float().transpose(1, 2),
                                                  padding=pad, dilation=dil)
-        if has_b and ctx.needs_input_grad[2]:
+        if want_b and gb is None:
             gb = ops.colsum(gz.contiguous())
         return gx, gw, gb, None, None, None, None, None, None
 

@@ -36,6 +36,7 @@ struct WgradArgs {
   int pre_a, pre_b; float slope;
   int rows_per_split;
   float* dw;
+  float* db;  // nullable: bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
   int abl;  // timing ablations (wgrad_cfg 10 / 11): 1 = plain stores instead of atomics, 2 = no loads
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
@@ -78,6 +79,11 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient: the workgroups of tap 0 and the first N tile see every A row of their M
+  // tile exactly once -> column sums of the staged A chunks (thread: column tid & 63, rows 16 x
+  // (tid >> 6) ..), one LDS reduction and one atomic per column at the end
+  const bool do_bias = p.db != nullptr && k == 0 && n0 == 0;  // workgroup-uniform
+  float bsum = 0.f;
 
   for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
     // ---- stage 64 rows of A (rows r0..) and of B (gathered rows of the same utterances)
@@ -127,6 +133,11 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       *reinterpret_cast<u32x4_t*>(sb + r * P + c) = y;
     }
     __syncthreads();
+    if (do_bias) {
+      const int col = tid & 63, r16 = (tid >> 6) * 16;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bsum += to_f32(sa[(r16 + i) * P + col]);
+    }
 
     // ---- two 32-row k-steps
 #pragma unroll
@@ -177,6 +188,14 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
       }
     }
+  }
+
+  if (do_bias) {
+    __shared__ float bred[4][64];
+    bred[tid >> 6][tid & 63] = bsum;
+    __syncthreads();
+    if (tid < 64 && m0 + tid < p.M)
+      atomicAdd(p.db + (int64_t)grp * p.M + m0 + tid, bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid]);
   }
 
   // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[k][m][n]
@@ -231,10 +250,11 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, in
 
 using namespace vo;
 
-extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
-                                       int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
-                                       float slope, int dtype, float* dw, void* stream) {
+extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
+                                    int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
+                                    float slope, int dtype, float* dw, float* db, void* stream) {
   VO_CHECK_ARG(a && b && dw, "conv1d_wgrad: null pointer");
+  VO_CHECK_ARG(!db || !pre_a, "conv1d_wgrad: the fused bias gradient sums A as stored (pre_a must be off)");
   VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1 && groups >= 1, "conv1d_wgrad: bad sizes");
   const int ev = dtype == VO_BF16 ? 8 : 4;
   VO_CHECK_ARG(M % ev == 0 && N % ev == 0 && lda % ev == 0 && ldb % ev == 0 && lda >= (int64_t)groups * M &&
@@ -243,7 +263,7 @@ extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const vo
   WgradArgs p;
   p.a = a; p.lda = lda; p.T_A = T_A; p.bsrc = b; p.ldb = ldb; p.T_B = T_B;
   p.M = M; p.N = N; p.K = K; p.S = S; p.dil = dil; p.pad = pad; p.Bn = B;
-  p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope; p.dw = dw;
+  p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope; p.dw = dw; p.db = db;
   const int64_t zk = (int64_t)K * groups;
   const int64_t rows = (int64_t)B * T_A;
   const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
@@ -267,6 +287,13 @@ extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const vo
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
+                                       int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
+                                       float slope, int dtype, float* dw, void* stream) {
+  return vo_conv1d_wgrad_bias(a, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, groups, pre_a, pre_b, slope, dtype,
+                              dw, nullptr, stream);
 }
 
 extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M, int N,

@@ -254,10 +254,16 @@ class ConvFn(torch.autograd.Function):
                                           transposed=True)
                     gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
                 else:
+                    # bias gradient from the same launch when dY needed no cast (column sums of gzc)
+                    fuse_b = need_b and gz.dtype == x.dtype
                     dw = ops.conv1d_wgrad(gzc, _pad_channels(x) if g == 1 else x, spec.K, S=spec.stride,
-                                          dil=spec.dil, pad=spec.pad, pre_b=spec.pre_slope, groups=g)
+                                          dil=spec.dil, pad=spec.pad, pre_b=spec.pre_slope, groups=g,
+                                          with_bias=fuse_b)
+                    if fuse_b:
+                        dw, db = dw
+                        gb = db[: w.shape[0]]
                     gw = dw[: w.shape[0], : w.shape[1]].to(w.dtype)
-            if need_b:
+            if need_b and gb is None:
                 gb = ops.colsum(gz.contiguous())[: w.shape[1] if spec.transposed is not None else w.shape[0]]
             need_w = need_b = False
         if need_x or need_w or need_b:

@@ -629,11 +629,12 @@ def char_features(energy, fstats, durations, n_bins):
 
 # ----------------------------------------------------------------------------- training backward
 
-def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1):
+def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1, with_bias=False):
     """Weight gradient on MFMA (vo_conv1d_wgrad).  Conv1d: a = dY (B, T_out, Co), b = x (B, T_in, Ci)
     -> dW (Co, Ci / groups, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY
     (B, T_up, Co) -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand
-    (None = identity)."""
+    (None = identity).  with_bias (conv form): also the bias gradient, column sums of a, from the
+    same launch (vo_conv1d_wgrad_bias) -> (dW, db)."""
     _contig(a, "a")
     _contig(b, "b")
     if a.dtype != b.dtype:
@@ -642,16 +643,22 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     _, T_B, N = b.shape
     if M % groups or N % groups:
         raise ValueError(f"conv1d_wgrad: channels {M} / {N} not divisible by groups {groups}")
+    if with_bias and (pre_a is not None or transposed):
+        raise ValueError("conv1d_wgrad: the fused bias gradient needs the conv form with a = dY as stored")
     mg, ng = M // groups, N // groups
-    dw = torch.zeros((groups, K, mg, ng), dtype=torch.float32, device=a.device)  # tap-major (kernel order)
+    n_w = groups * K * mg * ng
+    buf = torch.zeros(n_w + (M if with_bias else 0), dtype=torch.float32, device=a.device)  # one fill
+    dw = buf[:n_w].view(groups, K, mg, ng)  # tap-major (kernel order)
+    db = buf[n_w:] if with_bias else None
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
-    _lib.check(_lib.lib().vo_conv1d_wgrad_grouped(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K,
-                                                  S, dil, pad, groups, int(pre_a is not None),
-                                                  int(pre_b is not None), float(slope), vo_dtype(a), _ptr(dw),
-                                                  _stream(a)), "vo_conv1d_wgrad")
-    return dw.permute(0, 2, 3, 1).reshape(M, ng, K)
+    _lib.check(_lib.lib().vo_conv1d_wgrad_bias(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K,
+                                               S, dil, pad, groups, int(pre_a is not None),
+                                               int(pre_b is not None), float(slope), vo_dtype(a), _ptr(dw),
+                                               _ptr(db), _stream(a)), "vo_conv1d_wgrad")
+    w = dw.permute(0, 2, 3, 1).reshape(M, ng, K)
+    return (w, db) if with_bias else w
 
 
 def colsum(x):
