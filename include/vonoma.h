@@ -331,6 +331,13 @@ int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb
                          int pre_b, float slope, int dtype, float* dw, float* db, void* stream);
 int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream);
 
+/* Leaky-ReLU / ReLU backward mask: out[r, c] = g[r, c] * (ref[r, c] > 0 ? 1 : slope) over a
+ * (rows x width) view with leading dimensions (out may alias g; ref = the activation's input, or
+ * its output when slope > 0).  Replaces the elementwise autograd of F.leaky_relu / F.relu
+ * (hifigan/models.py:96-103,155-163, SubLayers.py:85-93) in the training backward. */
+int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, int64_t rows,
+                  int width, float slope, void* out, int ldo, void* stream);
+
 /* ------------------------------------------------------------------ training input pipeline
  * Glyph batch: B grayscale strips packed in px (strip b at img_off[b],
  * H rows of img_w[b] uint8 columns) -> out (B, 1, H, W_out) fp32 = pixel / 255 with each

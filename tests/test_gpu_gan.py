@@ -397,3 +397,20 @@ def test_conv1d_wgrad_fused_bias(B, T, Ci, Co, K, s, g, pad, dt, tol):
     assert rel_l2(gw.cpu(), ref_w) < tol
     assert gb.shape == (Co,) and rel_l2(gb.cpu(), ref_b) < 1e-5
     del F
+
+
+@pytest.mark.parametrize("gdt,rdt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                     (torch.float32, torch.bfloat16), (torch.bfloat16, torch.float32)])
+@pytest.mark.parametrize("slope", [0.1, 0.0])
+def test_lrelu_mask_exact(gdt, rdt, slope):
+    """vo_lrelu_mask vs the PyTorch chain it replaces, incl. a channel-sliced ref and in place."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.randn(3, 257, 40).to(gdt)
+    xw = torch.randn(3, 257, 48).to(rdt)
+    ref = xw[..., :40]
+    want = (g.float() * torch.where(ref.float() > 0, 1.0, slope)).to(gdt)
+    got = ops.lrelu_mask(g.cuda(), xw.cuda()[..., :40], slope).cpu()
+    assert torch.equal(got, want)
+    gc = g.cuda()
+    ops.lrelu_mask(gc, xw.cuda()[..., :40], slope, out=gc)
+    assert torch.equal(gc.cpu(), want)

@@ -109,6 +109,8 @@ _SIGNATURES = {
     "vo_conv1d_wgrad_bias": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
                                      c_void_p]),
+    "vo_lrelu_mask": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, ctypes.c_int64, c_int, c_float,
+                              c_void_p, c_int, c_void_p]),
     "vo_colsum": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p]),
     "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),

@@ -42,7 +42,7 @@ class Conv1dFn(torch.autograd.Function):
         K, dil, pad, relu, cdt, has_b = ctx.cfg
         gz = gy.contiguous()
         if relu:
-            gz = gz * (y > 0).to(gz.dtype)
+            gz = ops.lrelu_mask(gz, y, 0.0)
         gx = gw = gb = None
         want_b = has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[0]:

@@ -129,6 +129,23 @@ __global__ void __launch_bounds__(256) gan_reduce_grad_kernel(int kind, const TA
 
 static int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 4096); }
 
+
+// leaky-ReLU backward mask: out = g * (ref > 0 ? 1 : slope) over a (rows x width) view with
+// leading dimensions (out may alias g).  ref = the activation's input or its output (same sign
+// for slope > 0).  One launch instead of PyTorch's compare / where / cast / mul chain.
+template <typename TG, typename TR>
+__global__ void __launch_bounds__(256) lrelu_mask_kernel(const TG* __restrict__ g, int ldg, const TR* __restrict__ ref,
+                                                         int ldr, int64_t rows, int width, float slope,
+                                                         TG* __restrict__ out, int ldo) {
+  const int64_t n = rows * width;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / width;
+    const int c = (int)(i - r * width);
+    const float v = to_f32(g[r * ldg + c]);
+    out[r * ldo + c] = from_f32<TG>(to_f32(ref[r * ldr + c]) > 0.f ? v : v * slope);
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -185,7 +202,9 @@ extern "C" int vo_gan_reduce(int kind, const void* a, int lda, const void* b, in
   VO_CHECK_ARG(a && out && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce: bad arguments");
   VO_CHECK_ARG(rows > 0 && width > 0 && lda >= width && (kind != 0 || ldb >= width), "gan_reduce: bad shape");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = grid_for(rows * width);
+  // every block ends in one atomic on the same scalar: at most 512 of them (4096 same-address
+  // atomics serialised at L2 took ~34 us a call; the grid-stride loop keeps the loads coalesced)
+  const int g = std::min(grid_for(rows * width), 512);
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(gan_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
                        (const bf16_t*)b, ldb, rows, width, out);
@@ -207,5 +226,26 @@ extern "C" int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* 
   else
     hipLaunchKernelGGL(gan_reduce_grad_kernel<float>, dim3(g), dim3(256), 0, st, kind, (const float*)a, lda,
                        (const float*)b, ldb, rows, width, scale, (float*)ga, ldg);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
+                             int64_t rows, int width, float slope, void* out, int ldo, void* stream) {
+  VO_CHECK_ARG(g && ref && out, "lrelu_mask: null pointer");
+  VO_CHECK_ARG(rows > 0 && width > 0 && ldg >= width && ldr >= width && ldo >= width, "lrelu_mask: bad shape");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int gr = grid_for(rows * width);
+#define VO_LM(TG, TR)                                                                                          \
+  hipLaunchKernelGGL((lrelu_mask_kernel<TG, TR>), dim3(gr), dim3(256), 0, st, (const TG*)g, ldg, (const TR*)ref, \
+                     ldr, rows, width, slope, (TG*)out, ldo)
+  if (g_dtype == VO_BF16 && ref_dtype == VO_BF16) VO_LM(bf16_t, bf16_t);
+  else if (g_dtype == VO_F32 && ref_dtype == VO_F32) VO_LM(float, float);
+  else if (g_dtype == VO_BF16 && ref_dtype == VO_F32) VO_LM(bf16_t, float);
+  else if (g_dtype == VO_F32 && ref_dtype == VO_BF16) VO_LM(float, bf16_t);
+  else {
+    vo_set_error("lrelu_mask: bad dtypes");
+    return VO_ERR_INVALID;
+  }
+#undef VO_LM
   VO_RETURN_LAUNCH();
 }

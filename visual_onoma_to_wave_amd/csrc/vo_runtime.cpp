@@ -69,7 +69,7 @@ static const char* const kSymbols[] = {
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
     "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
-    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias",
+    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -212,7 +212,7 @@ class ConvFn(torch.autograd.Function):
         gz = gy * spec.out_scale if spec.out_scale != 1.0 else gy
         g_res1 = gz if ctx.has[0] and ctx.needs_input_grad[3] else None
         if spec.post == "lrelu":
-            gz = gz * torch.where(y > 0, 1.0, spec.post_slope).to(gz.dtype)
+            gz = ops.lrelu_mask(gz, y, spec.post_slope)
         elif spec.post == "tanh":
             yf = y.float()
             gz = (gz.float() * (1.0 - yf * yf)).to(gz.dtype)
@@ -284,7 +284,7 @@ class ConvFn(torch.autograd.Function):
                 gb = gb2
         if ga is not None:
             if spec.pre_slope is not None:
-                ga = ga * torch.where(xin > 0, 1.0, spec.pre_slope).to(ga.dtype)
+                ga = ops.lrelu_mask(ga, xin, spec.pre_slope, out=ga if ga.is_contiguous() else None)
             if ga.shape[-1] != x.shape[-1]:
                 ga = F.pad(ga, (0, x.shape[-1] - ga.shape[-1]))
             gx = ga

@@ -661,6 +661,30 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     return (w, db) if with_bias else w
 
 
+def lrelu_mask(g, ref, slope, out=None):
+    """g * (ref > 0 ? 1 : slope) (leaky-ReLU / ReLU backward); g, ref (..., C) with row-contiguous
+    last dims (ref may be a channel slice of a wider tensor).  out=g computes in place."""
+    if g.shape != ref.shape:
+        raise ValueError("lrelu_mask: g and ref shapes differ")
+    C = g.shape[-1]
+
+    def row_strided(t):  # (..., C) rows at a common stride (a channel slice of a wider tensor is fine)
+        return t.dim() >= 2 and t.stride(-1) == 1 and all(
+            t.stride(i) == t.stride(i + 1) * t.shape[i + 1] for i in range(t.dim() - 2))
+    if not row_strided(g):
+        g, out = g.contiguous(), None
+    if not row_strided(ref):
+        ref = ref.contiguous()
+    if out is not None and not row_strided(out):
+        raise ValueError("lrelu_mask: out must be row-strided (..., C)")
+    out = torch.empty(g.shape, dtype=g.dtype, device=g.device) if out is None else out
+    rows = g.numel() // C
+    ld = lambda t: t.stride(-2)  # noqa: E731
+    _lib.check(_lib.lib().vo_lrelu_mask(_ptr(g), ld(g), vo_dtype(g), _ptr(ref), ld(ref), vo_dtype(ref), rows, C,
+                                        float(slope), _ptr(out), ld(out), _stream(g)), "vo_lrelu_mask")
+    return out
+
+
 def colsum(x):
     """(..., C) -> (C,) fp32 column sums (bias gradient)."""
     _contig(x, "x")
