@@ -1,0 +1,68 @@
+"""Streaming polyphase upsampler (csrc/upsample.hip, ups2 128 -> 64 and ups3 64 -> 32, k4 s2).
+
+The HiFi-GAN ConvTranspose1d (scripts/hifigan/models.py:139-141,153-154, lrelu 0.1 in front)
+in its bf16 polyphase form runs on `ups_kernel` when the output is bf16; the generic tiled conv
+(`vo_tune("ups_cfg", 1)`) is the same arithmetic in the same order, so the two must agree
+bit for bit.  Both are checked against a plain PyTorch fp32 ConvTranspose1d (rel-L2 <= 1e-2,
+the bf16 tolerance of SURVEY.md 8(c))."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(x, w_t, bias, u, k, slope, cfg):
+    from visual_onoma_to_wave_amd import _lib, ops
+    wb = ops.pack_conv_weight(w_t, torch.bfloat16, transposed_stride=u)
+    _lib.lib().vo_tune(b"ups_cfg", cfg)
+    try:
+        pre = ops.ACT_LRELU if slope is not None else ops.ACT_NONE
+        y = ops.conv1d(x, wb, bias, Co=u * w_t.shape[1], K=2, pad=1, pre_act=pre,
+                       pre_slope=slope if slope is not None else 0.0,
+                       transposed=dict(stride=u, pad=(k - u) // 2, cout=w_t.shape[1]),
+                       out_dtype=torch.bfloat16, compute_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().vo_tune(b"ups_cfg", 0)
+    return y
+
+
+def _ref(x, w_t, bias, u, k, slope):
+    xt = x.float().transpose(1, 2)
+    if slope is not None:
+        xt = F.leaky_relu(xt, slope)
+    return F.conv_transpose1d(xt, w_t.to(torch.bfloat16).float(), bias, stride=u,
+                              padding=(k - u) // 2).transpose(1, 2)
+
+
+@pytest.mark.parametrize("Ci,Cout", [(128, 64), (64, 32)])
+@pytest.mark.parametrize("B,T", [(1, 1), (1, 15), (2, 16), (3, 17), (2, 31), (1, 33), (4, 1000), (32, 4096)])
+@pytest.mark.parametrize("slope", [0.1, None])
+def test_ups_stream_matches_generic_and_torch(device, Ci, Cout, B, T, slope):
+    u, k = 2, 4
+    g = torch.Generator().manual_seed(1234 + T + Ci)
+    x = torch.randn(B, T, Ci, generator=g).to(torch.bfloat16).to(device)
+    w_t = (torch.randn(Ci, Cout, k, generator=g) * 0.05).to(device)
+    bias = torch.randn(Cout, generator=g).to(device)
+    y = _run(x, w_t, bias, u, k, slope, 0)
+    y_gen = _run(x, w_t, bias, u, k, slope, 1)
+    assert y.shape == (B, 2 * T, Cout)
+    assert torch.equal(y, y_gen), (y.float() - y_gen.float()).abs().max().item()
+    ref = _ref(x, w_t, bias, u, k, slope)
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+def test_ups_stream_c3_size(device):
+    """C3-sized ups2 / ups3 (B = 32 x 512 frames): bit-identical to the generic path."""
+    u, k = 2, 4
+    for Ci, Cout, T in ((128, 64, 32768), (64, 32, 65536)):
+        g = torch.Generator().manual_seed(Ci)
+        x = torch.randn(32, T, Ci, generator=g).to(torch.bfloat16).to(device)
+        w_t = (torch.randn(Ci, Cout, k, generator=g) * 0.05).to(device)
+        bias = torch.randn(Cout, generator=g).to(device)
+        y = _run(x, w_t, bias, u, k, 0.1, 0)
+        y_gen = _run(x, w_t, bias, u, k, 0.1, 1)
+        assert torch.equal(y, y_gen), Ci
+        del x, y, y_gen

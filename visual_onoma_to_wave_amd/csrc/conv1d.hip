@@ -507,6 +507,8 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
 
 using namespace vo;
 
+int vo_ups_try(const vo_conv1d_desc* d, hipStream_t st, int* handled);  // upsample.hip
+
 extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d != nullptr, "conv1d: null descriptor");
   VO_CHECK_ARG(d->x && d->w && d->y, "conv1d: null tensor pointer");
@@ -530,6 +532,11 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
     VO_CHECK_ARG(d->Co % 16 == 0 || d->Co == 80 || d->Co <= 32, "conv1d: unsupported Co %d", d->Co);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(const_cast<void*>(stream));
+  if (d->transposed) {  // narrow upsamplers: the persistent streaming kernel (upsample.hip)
+    int handled = 0;
+    const int rc = vo_ups_try(d, st, &handled);
+    if (handled) return rc;
+  }
   const int xi = d->x_dtype, yo = d->y_dtype;
   if (d->stride > 1 || d->groups > 1) {  // discriminator layers
     const int g = d->groups > 1 ? d->groups : 1;
