@@ -1,4 +1,5 @@
-"""Streaming polyphase upsampler (csrc/upsample.hip, ups2 128 -> 64 and ups3 64 -> 32, k4 s2).
+"""HiFi-GAN generator tail kernels: the streaming polyphase upsampler (csrc/upsample.hip, ups2
+128 -> 64 and ups3 64 -> 32, k4 s2) and the row-partials conv_post (csrc/vocoder_glue.hip).
 
 The HiFi-GAN ConvTranspose1d (scripts/hifigan/models.py:139-141,153-154, lrelu 0.1 in front)
 in its bf16 polyphase form runs on `ups_kernel` when the output is bf16; the generic tiled conv
@@ -66,3 +67,27 @@ def test_ups_stream_c3_size(device):
         y_gen = _run(x, w_t, bias, u, k, 0.1, 1)
         assert torch.equal(y, y_gen), Ci
         del x, y, y_gen
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (1, 5), (2, 250), (3, 251), (1, 1000), (2, 131072)])
+def test_conv_post_rows_kernel(device, B, T):
+    """HiFi-GAN tail lrelu(0.01) -> Conv1d(32 -> 1, k7, pad 3) -> tanh (models.py:161-163) on
+    the row-partials kernel (bf16 input, C = 32, K = 7) against the LDS-stencil kernel
+    (`post_cfg` 1; same math, another fp32 summation order) and PyTorch fp32."""
+    from visual_onoma_to_wave_amd import _lib, ops
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(B, T, 32, generator=g).to(torch.bfloat16).to(device)
+    w = (torch.randn(1, 32, 7, generator=g) * 0.1).to(device)
+    bias = 0.05
+    w_kc = w[0].t().contiguous()
+    y = ops.conv_post(x, w_kc, bias, slope=0.01)
+    _lib.lib().vo_tune(b"post_cfg", 1)
+    try:
+        y_st = ops.conv_post(x, w_kc, bias, slope=0.01)
+    finally:
+        _lib.lib().vo_tune(b"post_cfg", 0)
+    ref = torch.tanh(F.conv1d(F.leaky_relu(x.float().transpose(1, 2), 0.01), w, torch.tensor([bias], device=device),
+                              padding=3))[:, 0]
+    assert y.shape == (B, T)
+    assert (y - y_st).abs().max().item() < 1e-5
+    assert (y - ref).abs().max().item() < 1e-5

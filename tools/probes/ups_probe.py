@@ -23,23 +23,28 @@ def t_us(fn, n=50):
     return s.elapsed_time(e) / n * 1e3
 
 
-for Ci, Cout, T in ((128, 64, 32768), (64, 32, 65536)):
-    u, k = 2, 4
-    xb = torch.randn(32, T, Ci, device="cuda").to(torch.bfloat16)
-    wb = ops.pack_conv_weight(torch.randn(Ci, Cout, k, device="cuda") * 0.05, torch.bfloat16, transposed_stride=u)
-    bb = torch.randn(Cout, device="cuda")
-    out = torch.empty(32, 2 * T, Cout, device="cuda", dtype=torch.bfloat16)
-    line = f"ConvT Ci={Ci} Cout={Cout} T={T}:"
-    ref = None
-    for c in (0, 2, 3, 1):
-        _lib.lib().vo_tune(b"ups_cfg", c)
-        f = lambda: ops.conv1d(xb, wb, bb, Co=u * Cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=0.1,  # noqa: E731
-                               transposed=dict(stride=u, pad=(k - u) // 2, cout=Cout), out=out)
-        y = f().clone()
-        ref = y if ref is None else ref
-        same = bool(torch.equal(y, ref))
-        us = t_us(f)
-        gbs = (xb.numel() + y.numel()) * 2 / us / 1e3
-        line += f" [ups_cfg {c}] {us:.1f} us {gbs:.0f} GB/s ({gbs / 8000:.2f} of 8 TB/s){'' if same else ' MISMATCH'}"
-    _lib.lib().vo_tune(b"ups_cfg", 0)
-    print(line, flush=True)
+def main():
+    for Ci, Cout, T in ((128, 64, 32768), (64, 32, 65536)):
+        u, k = 2, 4
+        xb = torch.randn(32, T, Ci, device="cuda").to(torch.bfloat16)
+        wb = ops.pack_conv_weight(torch.randn(Ci, Cout, k, device="cuda") * 0.05, torch.bfloat16, transposed_stride=u)
+        bb = torch.randn(Cout, device="cuda")
+        out = torch.empty(32, 2 * T, Cout, device="cuda", dtype=torch.bfloat16)
+        line = f"ConvT Ci={Ci} Cout={Cout} T={T}:"
+        ref = None
+        for c in (0, 2, 3, 1):
+            _lib.lib().vo_tune(b"ups_cfg", c)
+            f = lambda: ops.conv1d(xb, wb, bb, Co=u * Cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=0.1,  # noqa: E731
+                                   transposed=dict(stride=u, pad=(k - u) // 2, cout=Cout), out=out)
+            y = f().clone()
+            ref = y if ref is None else ref
+            same = bool(torch.equal(y, ref))
+            us = t_us(f)
+            gbs = (xb.numel() + y.numel()) * 2 / us / 1e3
+            line += f" [ups_cfg {c}] {us:.1f} us {gbs:.0f} GB/s ({gbs / 8000:.2f} of 8 TB/s){'' if same else ' MISMATCH'}"
+        _lib.lib().vo_tune(b"ups_cfg", 0)
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -83,6 +83,47 @@ __global__ void __launch_bounds__(256) conv_post_kernel(const TX* __restrict__ x
   y[(int64_t)b * T + t] = tanhf(acc0 + acc1);
 }
 
+// conv_post_rows_kernel (bf16, compile-time C and K; HiFi-GAN V1: 32, 7): each thread reads
+// ONE input row straight from HBM (C bf16, lrelu'd in registers) and reduces it against all K
+// taps, z[k][r] = sum_c w[k][c] x[r][c]; after one barrier output t0 + r is tanh(bias +
+// sum_k z[k][r + k]).  A row is read once (LDS traffic 2K floats per sample) instead of K
+// times from an LDS tile by every output (the stencil kernel above: K*C floats per sample).
+// 256 rows per workgroup give 256 - (K - 1) outputs.
+template <int C, int K>
+__global__ void __launch_bounds__(256) conv_post_rows_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                             float bias, int T, float slope, float* __restrict__ y) {
+  constexpr int OUT = 256 - (K - 1);
+  constexpr int PAD = (K - 1) / 2;
+  __shared__ float z[K][256];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * OUT;
+  const int r = threadIdx.x;
+  const int t = t0 - PAD + r;
+  const bool in = t >= 0 && t < T;
+  const bf16_t* src = x + ((int64_t)b * T + min(max(t, 0), T - 1)) * C;
+  float f[C];
+#pragma unroll
+  for (int c = 0; c < C; c += 8) load8(src + c, *reinterpret_cast<float(*)[8]>(f + c));
+#pragma unroll
+  for (int c = 0; c < C; ++c) f[c] = in ? fmaxf(f[c], f[c] * slope) : 0.f;  // 0 <= slope <= 1
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; c += 2) {
+      p0 = fmaf(w[k * C + c], f[c], p0);  // wave-uniform weights: scalar loads
+      p1 = fmaf(w[k * C + c + 1], f[c + 1], p1);
+    }
+    z[k][r] = p0 + p1;
+  }
+  __syncthreads();
+  if (r >= OUT || t0 + r >= T) return;
+  float acc = bias;
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc += z[k][r + k];
+  y[(int64_t)b * T + t0 + r] = tanhf(acc);
+}
+
 template <typename TY>
 __global__ void transpose_bct_kernel(const float* __restrict__ x, int C, int T, TY* __restrict__ y, int ldy) {
   __shared__ float tile[32][33];
@@ -152,6 +193,12 @@ extern "C" int vo_conv_post(const void* x, int x_dtype, const float* w, float bi
   VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "conv_post: slope %g outside [0, 1]", slope);
   VO_CHECK_ARG(B > 0 && T > 0, "conv_post: empty");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (x_dtype == VO_BF16 && C == 32 && K == 7 && vo_tune_get("post_cfg") != 1) {  // post_cfg 1: stencil kernel
+    constexpr int OUT = 256 - 6;
+    dim3 g2((unsigned)((T + OUT - 1) / OUT), (unsigned)B);
+    hipLaunchKernelGGL((conv_post_rows_kernel<32, 7>), g2, dim3(256), 0, st, (const bf16_t*)x, w, bias, T, slope, y);
+    VO_RETURN_LAUNCH();
+  }
   dim3 grid((unsigned)((T + CP_ROWS - 1) / CP_ROWS), (unsigned)B);
   const size_t lds = (size_t)(CP_ROWS + K - 1) * (C + 4) * sizeof(float);
   if (x_dtype == VO_BF16 && C == 32)
