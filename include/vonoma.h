@@ -89,8 +89,16 @@ typedef struct vo_conv1d_desc {
                          (HiFi-GAN MPD Conv2d (k,1)/(s,1) per period column, MSD Conv1d)  */
   int groups;         /* 0/1 = dense; g: grouped conv, w packed dense [K][Co][Ci] with zeros
                          outside the g diagonal blocks (MSD grouped Conv1d)              */
+  void* workspace;    /* optional caller-owned device scratch (NULL = none): when it holds
+                         vo_conv1d_workspace_size(d) bytes, fp32 convs over short sequences
+                         (T_out <= 16: glyph encoder, variance predictors) split their
+                         reduction over workgroups and add the fp32 partials in a fixed
+                         order (deterministic)                                           */
+  int64_t workspace_bytes;
 } vo_conv1d_desc;
 int vo_conv1d(const vo_conv1d_desc* d, void* stream);
+/* scratch bytes the split-reduction path of vo_conv1d wants for d (0 = it does not split d) */
+int64_t vo_conv1d_workspace_size(const vo_conv1d_desc* d);
 
 /* Weight preparation (load time).  Replaces the weight-norm fold (remove_weight_norm,
  * scripts/hifigan/models.py:105-109,167-174: w = g * v / ||v||, norm over all dims but 0)

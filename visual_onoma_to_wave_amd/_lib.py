@@ -39,6 +39,7 @@ class Conv1dDesc(ctypes.Structure):
         ("up_tout", c_int),
         ("variant", c_int),
         ("stride", c_int), ("groups", c_int),
+        ("workspace", c_void_p), ("workspace_bytes", ctypes.c_int64),
     ]
 
 
@@ -71,6 +72,7 @@ _SIGNATURES = {
     "vo_resblock3": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                              c_int, c_int, c_float, c_float, c_void_p]),
     "vo_conv1d": (c_int, [ctypes.POINTER(Conv1dDesc), c_void_p]),
+    "vo_conv1d_workspace_size": (ctypes.c_int64, [ctypes.POINTER(Conv1dDesc)]),
     "vo_pack_weight": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                c_void_p, c_int, c_void_p]),
     "vo_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,

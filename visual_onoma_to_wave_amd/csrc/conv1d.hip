@@ -46,6 +46,8 @@ struct ConvArgs {
   int transposed, up_stride, up_pad, up_cout, up_tout;
   int tiles_per_b, co_tiles, B;
   int cig, cog;  // channels per group (in / out): grouped conv = block-diagonal packed weights
+  float* partial;  // split reduction: fp32 partials [splits][B][T_out][Co] (null = off)
+  int kcs;         // 32-channel chunks per split (grid z = split)
 };
 
 template <typename T> struct Raw8;  // 8 elements of T held in registers
@@ -172,6 +174,28 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
   }
 }
 
+// split reduction, first pass: raw fp32 accumulators of this split's chunks (lane layout of
+// conv_epilogue: channels [n0, n0 + 4 NI) of each of its NJ positions)
+template <int NI, int NJ>
+__device__ __forceinline__ void conv_partial_store(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0,
+                                                   int co_blk, int wave_co0, int wave_t0, int lane) {
+  const int lr = lane & 15;
+  const int n0 = co_blk + wave_co0 + NI * 4 * (lane >> 4);
+  if (n0 >= a.Co) return;
+  float* P = a.partial + ((int64_t)blockIdx.z * a.B + b) * (int64_t)a.T_out * a.Co;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int pos = t0 + wave_t0 + 16 * j + lr;
+    if (pos >= a.T_out) continue;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (n0 + 4 * i >= a.Co) break;
+      *reinterpret_cast<float4*>(P + (int64_t)pos * a.Co + n0 + 4 * i) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+}
+
 // ROLE only names the instantiation (0 = generic, 1..4 = HiFi-GAN MRF stage 0..3), so a
 // profiler attributes the vocoder's stages to distinct kernels; the code is identical.
 // TPS = taps per pipeline step: the weight tiles of TPS taps are staged together so one
@@ -222,9 +246,14 @@ conv1d_kernel(ConvArgs a) {
   // channels [ci_lo, ci_hi) of their groups (32-aligned; the packed weights are
   // block-diagonal, so the extra channels of a partial chunk multiply zeros)
   const int co_last = min(co_blk + BCO, a.Co) - 1;
-  const int ci_lo = (co_blk / a.cog) * a.cig / KC * KC;
+  int ci_lo = (co_blk / a.cog) * a.cig / KC * KC;
   const int ci_hi = min(a.Ci, (co_last / a.cog + 1) * a.cig);
-  const int n_chunks = (ci_hi - ci_lo + KC - 1) / KC;
+  int n_chunks = (ci_hi - ci_lo + KC - 1) / KC;
+  if (a.partial) {  // split reduction: this workgroup's run of chunks
+    const int z0 = blockIdx.z * a.kcs;
+    ci_lo += z0 * KC;
+    n_chunks = min(a.kcs, n_chunks - z0);
+  }
   const int tsteps = (a.K + TPS - 1) / TPS;
   const int n_steps = n_chunks * tsteps;
   const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE;
@@ -386,10 +415,82 @@ conv1d_kernel(ConvArgs a) {
     __syncthreads();
     ++s;
   }
+  if (a.partial) {
+    conv_partial_store<NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
+    return;
+  }
   conv_epilogue<TOUT, NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
 }
 
+// split reduction, second pass: y = epilogue(sum_z partial[z] + bias) with the partials added
+// in split order; the epilogue (activation, residual, scale, accumulate) is conv_epilogue's
+__global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int splits) {
+  const int cg = a.Co / 4;
+  const int64_t rows = (int64_t)a.B * a.T_out;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * cg) return;
+  const int64_t row = idx / cg;
+  const int c = (int)(idx - row * cg) * 4;
+  const int b = (int)(row / a.T_out), t = (int)(row - (int64_t)b * a.T_out);
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < splits; ++z) {
+    const float4 p = *reinterpret_cast<const float4*>(a.partial + ((int64_t)z * rows + row) * a.Co + c);
+    v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] += a.bias ? a.bias[c + e] : 0.f;
+  if (a.post_act == VO_ACT_TANH) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+  } else {
+    const float ps = a.post_act == VO_ACT_RELU ? 0.f : (a.post_act == VO_ACT_LRELU ? a.post_slope : 1.f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * ps;
+  }
+  const int64_t off = (int64_t)b * a.ybs + (int64_t)t * a.ldy + c;
+  if (a.res1) {
+    float rr[4];
+    load4(reinterpret_cast<const float*>(a.res1) + off, rr);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += rr[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] *= a.out_scale;
+  if (a.res2) {
+    float rr[4];
+    load4(reinterpret_cast<const float*>(a.res2) + off, rr);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += rr[e];
+  }
+  store4(reinterpret_cast<float*>(a.y) + off, v);
+}
+
+// fp32 convs over short sequences (T_out <= 16 rows: glyph encoder, variance predictors at
+// T_src ~ 12) are a serial chain of (Ci / 32) * K pipeline steps per workgroup, each bound by
+// a load round trip (FFN w_1: 72 steps, 51 us for 1.8 GFLOP).  Split the chunks so a workgroup
+// runs about 4 steps; the partials are added by conv_splitk_reduce_kernel.  splitk_cfg 1 = off.
+static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
+  *splits = 1;
+  *kcs = 0;
+  if (vo_tune_get("splitk_cfg") == 1 || vo_tune_get("gen_cfg") != 0) return false;
+  if (d->compute_dtype != VO_F32 || d->x_dtype != VO_F32 || d->y_dtype != VO_F32) return false;
+  if (d->transposed || d->stride > 1 || d->groups > 1 || d->variant != 0) return false;
+  if (d->T_out > 16 || d->Co < 64 || d->Co % 4 || d->ldy % 4) return false;
+  const int n_chunks = (d->Ci + KC - 1) / KC;
+  if (n_chunks * d->K < 16) return false;
+  // ~4 steps per split (bench step 13.78 ms vs 13.85 with ~8 and 13.93 unsplit,
+  // tools/bench_splitk_ab.sh); splitk_cfg 2 = ~8
+  const int target = vo_tune_get("splitk_cfg") == 2 ? 8 : 4;
+  const int k = std::max(1, target / d->K);
+  const int s = (n_chunks + k - 1) / k;
+  if (s < 2) return false;
+  *splits = s;
+  *kcs = k;
+  return true;
+}
+
 // ------------------------------------------------------------------ host dispatch
+static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
           int PRIO = 0, int ABL = 0, int S = 1>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
@@ -422,8 +523,25 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
   auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S>
                    : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
-  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles);
+  a.partial = nullptr;
+  a.kcs = 0;
+  int splits = 1;
+  if constexpr (sizeof(TC) == 4 && S == 1) {
+    int kcs = 0;
+    if (d->workspace && splitk_plan(d, &splits, &kcs) &&
+        d->workspace_bytes >= (int64_t)splits * d->B * d->T_out * d->Co * (int64_t)sizeof(float)) {
+      a.partial = reinterpret_cast<float*>(d->workspace);
+      a.kcs = kcs;
+    } else {
+      splits = 1;
+    }
+  }
+  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles, (unsigned)splits);
   hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
+  if (a.partial) {
+    const int64_t n = (int64_t)d->B * d->T_out * (d->Co / 4);
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, splits);
+  }
   VO_RETURN_LAUNCH();
 }
 
@@ -508,6 +626,12 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
 using namespace vo;
 
 int vo_ups_try(const vo_conv1d_desc* d, hipStream_t st, int* handled);  // upsample.hip
+
+extern "C" int64_t vo_conv1d_workspace_size(const vo_conv1d_desc* d) {
+  int splits = 1, kcs = 0;
+  if (!d || !splitk_plan(d, &splits, &kcs)) return 0;
+  return (int64_t)splits * d->B * d->T_out * d->Co * (int64_t)sizeof(float);
+}
 
 extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d != nullptr, "conv1d: null descriptor");

@@ -22,7 +22,7 @@ extern "C" int vo_version(void) { return 1; }
 
 // experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0.
 // VO_TUNE="pair_cfg=1,conv_cfg=1" presets them for a whole process (bench A/B).
-static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg", "rb3_cfg", "att_cfg", "ups_cfg", "post_cfg"};
+static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg", "rb3_cfg", "att_cfg", "ups_cfg", "post_cfg", "splitk_cfg"};
 static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {};
 
 static void knobs_from_env() {
@@ -69,7 +69,7 @@ static const char* const kSymbols[] = {
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
     "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
-    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask",
+    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask", "vo_conv1d_workspace_size",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -9,6 +9,7 @@ its input, the ResBlock residual / MRF sum / 1/num_kernels scale in its epilogue
 each ConvTranspose1d upsampler in its polyphase form.
 """
 
+import contextlib
 import os
 import warnings
 
@@ -16,7 +17,7 @@ import torch
 import torch.nn as nn
 from torch.nn import Conv1d, ConvTranspose1d
 
-from .. import ops
+from .. import ops, profiling
 from .._base import HipModule
 
 LRELU_SLOPE = 0.1
@@ -167,11 +168,18 @@ class Generator(HipModule):
             x = ops.conv1d(x, w, b, Co=u * cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=LRELU_SLOPE,
                            transposed=dict(stride=u, pad=pad, cout=cout), out_dtype=dt, compute_dtype=dt)
             xs = torch.empty_like(x)
-            for j in range(self.num_kernels):
-                rb = self.resblocks[i * self.num_kernels + j]
-                rb.compute_dtype = dt
-                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
-                       stage=i if self.num_upsamples == 4 else None)
+            stage = i if self.num_upsamples == 4 else None
+            timer = profiling.active()
+            tag = f"mrf_s{i}"
+            # the stage's ResBlock launches are consecutive: one event pair for all of them
+            grp = timer.group(tag) if (stage is not None and timer is not None and timer.watching(tag)) \
+                else contextlib.nullcontext()
+            with grp:
+                for j in range(self.num_kernels):
+                    rb = self.resblocks[i * self.num_kernels + j]
+                    rb.compute_dtype = dt
+                    rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
+                           stage=stage)
             x = xs
         wk, bp = p["post"]
         return ops.conv_post(x, wk, bp, slope=0.01)

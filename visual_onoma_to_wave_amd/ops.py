@@ -108,6 +108,13 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
     d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
     d.stride, d.groups = stride, groups
+    ws = None
+    if compute_dtype == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
+        # split-reduction scratch for the short fp32 convs (stream-ordered: freed after enqueue)
+        nb = _lib.lib().vo_conv1d_workspace_size(ctypes.byref(d))
+        if nb > 0:
+            ws = torch.empty(nb // 4, dtype=torch.float32, device=x.device)
+            d.workspace, d.workspace_bytes = ws.data_ptr(), nb
     timer = profiling.active()
     ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
     _lib.check(_lib.lib().vo_conv1d(ctypes.byref(d), _stream(x)), "vo_conv1d")
