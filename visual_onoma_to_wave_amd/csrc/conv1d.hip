@@ -606,6 +606,9 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     // fused q/k/v 768) -> 256 x 256 tiles (-18 %); 1x1 convs to 256 channels -> 64 x 128
     // (twice the workgroups, -12 %).  gen_cfg 1 forces the 128 x 128 tile (A/B).
     if (vo_tune_get("gen_cfg") != 1) {
+      // 256 x 256 for the wide convs.  In isolation (tools/probes/wide_convs.py,
+      // profiles/r01j/wide_convs.txt) 256 co x 128 rows looked 11 % faster on FFN w_1, but in the
+      // bench step its 12 decoder launches took 818 us against 584 (profiles/r01k/): kept out.
       if (d->Co >= 768 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
     }
