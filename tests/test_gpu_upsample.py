@@ -55,10 +55,25 @@ def test_ups_stream_matches_generic_and_torch(device, Ci, Cout, B, T, slope):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("B,T", [(1, 1), (2, 17), (3, 100), (4, 513)])
+def test_ups_wide_matches_generic_and_torch(device, B, T):
+    """ups1 shape (256 -> 128, k16 s8): column-block kernel (upsw_kernel) vs the tiled conv."""
+    u, k, Ci, Cout = 8, 16, 256, 128
+    g = torch.Generator().manual_seed(77 + T)
+    x = torch.randn(B, T, Ci, generator=g).to(torch.bfloat16).to(device)
+    w_t = (torch.randn(Ci, Cout, k, generator=g) * 0.05).to(device)
+    bias = torch.randn(Cout, generator=g).to(device)
+    y = _run(x, w_t, bias, u, k, 0.1, 0)
+    y_gen = _run(x, w_t, bias, u, k, 0.1, 1)
+    assert y.shape == (B, 8 * T, Cout)
+    assert torch.equal(y, y_gen), (y.float() - y_gen.float()).abs().max().item()
+    ref = _ref(x, w_t, bias, u, k, 0.1)
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
 def test_ups_stream_c3_size(device):
-    """C3-sized ups2 / ups3 (B = 32 x 512 frames): bit-identical to the generic path."""
-    u, k = 2, 4
-    for Ci, Cout, T in ((128, 64, 32768), (64, 32, 65536)):
+    """C3-sized ups1 / ups2 / ups3 (B = 32 x 512 frames): bit-identical to the generic path."""
+    for Ci, Cout, T, u, k in ((128, 64, 32768, 2, 4), (64, 32, 65536, 2, 4), (256, 128, 4096, 8, 16)):
         g = torch.Generator().manual_seed(Ci)
         x = torch.randn(32, T, Ci, generator=g).to(torch.bfloat16).to(device)
         w_t = (torch.randn(Ci, Cout, k, generator=g) * 0.05).to(device)

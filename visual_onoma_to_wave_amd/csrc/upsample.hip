@@ -204,6 +204,210 @@ __global__ void __launch_bounds__(256) ups_kernel(UpsArgs a) {
   }
 }
 
+// Wide upsamplers (ups1: 256 -> 128, k16 s8: s * C_out = 1024 phase columns) do not fit one
+// LDS weight copy (1 MB).  (ups0, Ci = 512, would spill its 16 x-fragment k-steps at 2 waves
+// per SIMD: left on the tiled conv.)  upsw_kernel gives each persistent
+// workgroup one NCB-column block (128 KB of weights in LDS) and a contiguous run of input
+// steps; its 8 waves split that run.  Blocks are assigned so that the 8 column blocks of one
+// run of steps sit on the same XCD (workgroup id w -> XCD w % 8): the x rows they all read
+// stay in that XCD's L2.  Fragment layout, tap shift, order of accumulation and roundings
+// are ups_kernel's (bit-identical to the generic tiled conv).
+struct UpswArgs {
+  UpsArgs u;
+  int nc;       // total phase columns (s * C_out)
+  int ncb_n;    // column blocks = nc / NCB
+  int rgroups;  // run groups (grid = ncb_n * rgroups)
+};
+
+template <int CI, int NCB, int NJ>
+__global__ void __launch_bounds__(512) upsw_kernel(UpswArgs w) {
+  const UpsArgs& a = w.u;
+  constexpr int NI = NCB / 16;
+  constexpr int KS = CI / 32;
+  constexpr int CPR = CI / 8;
+  constexpr int SH = ups_log2(4 * NI);
+  constexpr int MB = 16 * NJ;
+  constexpr int NW = 8;
+  extern __shared__ __attribute__((aligned(16))) char upsw_smem[];
+  bf16_t* wl = reinterpret_cast<bf16_t*>(upsw_smem);            // [2][NCB][CI]
+  float* bl = reinterpret_cast<float*>(upsw_smem + 2 * NCB * CI * sizeof(bf16_t));  // [NCB]
+
+  // workgroup -> (column block, run group): ids g, g + 8, g + 16, ... share an XCD
+  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const int cblk = slot % w.ncb_n;
+  const int rgrp = (slot / w.ncb_n) * 8 + xcd;
+  if (rgrp >= w.rgroups) return;
+  const int cb = cblk * NCB;
+
+  auto key = [](int n) { return (n & 3) | (((n >> SH) & 1) << 2); };
+  for (int v = threadIdx.x; v < 2 * NCB * CPR; v += NW * 64) {
+    const int row = v / CPR, q = v % CPR;  // row = tap * NCB + n (block-local)
+    const int t = row / NCB, n = row % NCB;
+    const u32x4 u = *reinterpret_cast<const u32x4*>(a.w + ((int64_t)t * w.nc + cb + n) * CI + 8 * q);
+    *reinterpret_cast<u32x4*>(wl + row * CI + 8 * (q ^ key(n))) = u;
+  }
+  for (int v = threadIdx.x; v < NCB; v += NW * 64) {
+    const int n = cb + v;
+    bl[v] = a.bias ? a.bias[n % a.cout] : 0.f;
+  }
+
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lq = lane >> 4;
+  int a_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) a_off[i] = (NI * 4 * (lr >> 2) + 4 * i + (lr & 3)) * CI;
+  const int kq = key(NI * 4 * (lr >> 2) + (lr & 3));
+  const int nl0 = 4 * NI * lq;                 // block-local first column of this lane
+  const int phase = (cb + nl0) / a.cout;
+  const int col = cb + nl0 - phase * a.cout;
+  __syncthreads();
+
+  // this wave's contiguous run of units
+  const int workers = w.rgroups * NW;
+  const int wid = rgrp * NW + (threadIdx.x >> 6);
+  const int per = (a.units + workers - 1) / workers;
+  const int u_begin = wid * per;
+  const int u_end = min(u_begin + per, a.units);
+  if (u_begin >= u_end) return;
+
+  auto unit_pos = [&](int u, int& b, int& m0) {
+    b = u / a.nblk;
+    m0 = (u - b * a.nblk) * MB;
+  };
+  auto load_unit = [&](int u, u32x4 (&dst)[NJ][KS]) {
+    int b, m0;
+    unit_pos(min(u, u_end - 1), b, m0);
+    const bf16_t* X = a.x + (int64_t)b * a.xbs;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int rc = min(m0 + 16 * j + lr, a.T_in - 1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        dst[j][ks] = *reinterpret_cast<const u32x4*>(X + (int64_t)rc * CI + 32 * ks + 8 * lq);
+    }
+  };
+
+  u32x4 xf[NJ][KS], xn[NJ][KS], prev[KS];
+  {
+    int b, m0;
+    unit_pos(u_begin, b, m0);
+    const bf16_t* X = a.x + (int64_t)b * a.xbs + (int64_t)max(m0 - 1, 0) * CI;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u32x4 v = lrelu8(*reinterpret_cast<const u32x4*>(X + 32 * ks + 8 * lq), a.slope);
+      prev[ks] = m0 > 0 ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  load_unit(u_begin, xf);
+  for (int u = u_begin; u < u_end; ++u) {
+    asm volatile("" ::: "memory");
+    load_unit(u + 1, xn);
+    int b, m0;
+    unit_pos(u, b, m0);
+    if (m0 == 0) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) prev[ks] = u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const bool ok = m0 + 16 * j + lr < a.T_in;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const u32x4 v = lrelu8(xf[j][ks], a.slope);
+        xf[j][ks] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    f32x4 acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 bt[2][NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const u32x4 own = ror1(xf[j][ks]);
+        const u32x4 up = ror1(j == 0 ? prev[ks] : xf[j - 1][ks]);
+        bt[0][j] = __builtin_bit_cast(bf16x8, lr == 0 ? up : own);
+        bt[1][j] = __builtin_bit_cast(bf16x8, xf[j][ks]);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ch = 8 * ((4 * ks + lq) ^ kq);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + t * NCB * CI + a_off[i] + ch);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bt[t][j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    bf16_t* Y = a.y + (int64_t)b * a.ybs;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int m = m0 + 16 * j + lr;
+      const int trow = m * a.up_stride + phase - a.up_pad;
+      if (m > a.T_in || trow < 0 || trow >= a.up_tout) continue;
+      bf16_t* dst = Y + (int64_t)trow * a.cout + col;
+#pragma unroll
+      for (int h = 0; h < NI / 2; ++h) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bl + nl0 + 8 * h);
+        const float4 b1 = *reinterpret_cast<const float4*>(bl + nl0 + 8 * h + 4);
+        const f32x4 p = acc[2 * h][j], q = acc[2 * h + 1][j];
+        *reinterpret_cast<u32x4*>(dst + 8 * h) =
+            u32x4{pack_bf16x2(p[0] + b0.x, p[1] + b0.y), pack_bf16x2(p[2] + b0.z, p[3] + b0.w),
+                  pack_bf16x2(q[0] + b1.x, q[1] + b1.y), pack_bf16x2(q[2] + b1.z, q[3] + b1.w)};
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      prev[ks] = xf[NJ - 1][ks];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) xf[j][ks] = xn[j][ks];
+    }
+  }
+}
+
+template <int CI, int NCB, int NJ>
+static int launch_upsw(const vo_conv1d_desc* d, hipStream_t st) {
+  UpswArgs w;
+  UpsArgs& a = w.u;
+  a.x = reinterpret_cast<const bf16_t*>(d->x);
+  a.w = reinterpret_cast<const bf16_t*>(d->w);
+  a.bias = d->bias;
+  a.y = reinterpret_cast<bf16_t*>(d->y);
+  a.xbs = d->x_bstride; a.ybs = d->y_bstride;
+  a.T_in = d->T_in; a.up_tout = d->up_tout; a.up_stride = d->up_stride; a.up_pad = d->up_pad;
+  a.cout = d->up_cout;
+  a.nblk = (d->T_in + 1 + 16 * NJ - 1) / (16 * NJ);
+  a.units = a.nblk * d->B;
+  a.slope = d->pre_act == VO_ACT_LRELU ? d->pre_slope : (d->pre_act == VO_ACT_RELU ? 0.f : 1.f);
+  w.nc = d->Co;
+  w.ncb_n = d->Co / NCB;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  // resident workgroups only (persistent); run groups in multiples of 8 (one per XCD slot)
+  const size_t lds_b = 2 * (size_t)NCB * CI * sizeof(bf16_t) + NCB * sizeof(float);
+  int per_cu = 0;  // LDS- and register-limited resident workgroups per CU
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upsw_kernel<CI, NCB, NJ>, 512, lds_b) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int slots = std::max(1, cus * per_cu / 8);         // workgroup slots per XCD
+  const int rg_per_xcd = std::max(1, slots / w.ncb_n);
+  const int need = (a.units + 8 * 8 - 1) / (8 * 8);        // >= 8 units per wave
+  w.rgroups = std::min(8 * rg_per_xcd, std::max(1, need));
+  const int grid = 8 * w.ncb_n * ((w.rgroups + 7) / 8);
+  const size_t lds = 2 * (size_t)NCB * CI * sizeof(bf16_t) + NCB * sizeof(float);
+  hipLaunchKernelGGL((upsw_kernel<CI, NCB, NJ>), dim3((unsigned)grid), dim3(512), lds, st, w);
+  VO_RETURN_LAUNCH();
+}
+
 template <int CI, int NC, int NJ>
 static int launch_ups(const vo_conv1d_desc* d, hipStream_t st) {
   UpsArgs a;
@@ -253,6 +457,12 @@ int vo_ups_try(const vo_conv1d_desc* d, hipStream_t st, int* handled) {
     if (cfg == 2) return launch_ups<128, 128, 2>(d, st);
     if (cfg == 3) return launch_ups<128, 128, 1>(d, st);
     return launch_ups<128, 128, 4>(d, st);
+  }
+  // wide upsamplers: ups_cfg 4 forces the generic path for these alone
+  if (cfg != 4 && d->Ci == 256 && d->Co % 128 == 0 && d->up_cout % 32 == 0 && d->Co >= 256) {
+    *handled = 1;
+    if (cfg == 5) return launch_upsw<256, 64, 2>(d, st);
+    return launch_upsw<256, 128, 1>(d, st);
   }
   if (d->Ci == 64 && d->Co == 64 && d->up_cout % 16 == 0) {
     *handled = 1;
