@@ -20,7 +20,7 @@ with open(sys.argv[2], "w", newline="") as f:
     w = csv.DictWriter(f, keep)
     w.writeheader()
     for r in rows:
-        if "mrf_" in r["Kernel_Name"] or "conv1d_kernel" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in ("mrf_", "conv1d_kernel", "ups_kernel", "upsw_kernel", "conv_post_rows")):
             w.writerow({k: r[k] for k in keep})
 PY
   rm -rf "$OUT/raw_$lc"

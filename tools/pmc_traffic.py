@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of the MRF kernels from two rocprofv3 --pmc passes.
+"""Per-launch HBM traffic of the MRF kernels (and the streaming upsamplers / conv_post) from
+two rocprofv3 --pmc passes.
 
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one TCC
 pass).  Per MI355X_MICROARCH.md section HBM: both are KB; on gfx950 FETCH_SIZE reports
@@ -30,6 +31,14 @@ def load(path, counter):
         m = re.search(r"mrf_(?:pair|rb3)_kernel<(\d+),", name)  # fused pairs / blocks: stage by width
         if m and int(m.group(1)) in PAIR_STAGE:
             acc[PAIR_STAGE[int(m.group(1))]].append(float(r["Counter_Value"]))
+            continue
+        m = re.search(r"ups(w?)_kernel<(\d+),", name)  # streaming upsamplers: by input width
+        if m:
+            acc[{"128": "ups2", "64": "ups3", "256": "ups1"}.get(m.group(2), "ups_ci" + m.group(2))].append(
+                float(r["Counter_Value"]))
+            continue
+        if "conv_post_rows_kernel" in name:
+            acc["conv_post"].append(float(r["Counter_Value"]))
     return acc
 
 
