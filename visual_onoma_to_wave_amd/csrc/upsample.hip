@@ -205,8 +205,7 @@ __global__ void __launch_bounds__(256) ups_kernel(UpsArgs a) {
 }
 
 // Wide upsamplers (ups1: 256 -> 128, k16 s8: s * C_out = 1024 phase columns) do not fit one
-// LDS weight copy (1 MB).  (ups0, Ci = 512, would spill its 16 x-fragment k-steps at 2 waves
-// per SIMD: left on the tiled conv.)  upsw_kernel gives each persistent
+// LDS weight copy (1 MB).  upsw_kernel gives each persistent
 // workgroup one NCB-column block (128 KB of weights in LDS) and a contiguous run of input
 // steps; its 8 waves split that run.  Blocks are assigned so that the 8 column blocks of one
 // run of steps sit on the same XCD (workgroup id w -> XCD w % 8): the x rows they all read
@@ -219,15 +218,14 @@ struct UpswArgs {
   int rgroups;  // run groups (grid = ncb_n * rgroups)
 };
 
-template <int CI, int NCB, int NJ>
-__global__ void __launch_bounds__(512) upsw_kernel(UpswArgs w) {
+template <int CI, int NCB, int NJ, int NW>
+__global__ void __launch_bounds__(NW * 64) upsw_kernel(UpswArgs w) {
   const UpsArgs& a = w.u;
   constexpr int NI = NCB / 16;
   constexpr int KS = CI / 32;
   constexpr int CPR = CI / 8;
   constexpr int SH = ups_log2(4 * NI);
   constexpr int MB = 16 * NJ;
-  constexpr int NW = 8;
   extern __shared__ __attribute__((aligned(16))) char upsw_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(upsw_smem);            // [2][NCB][CI]
   float* bl = reinterpret_cast<float*>(upsw_smem + 2 * NCB * CI * sizeof(bf16_t));  // [NCB]
@@ -370,7 +368,7 @@ __global__ void __launch_bounds__(512) upsw_kernel(UpswArgs w) {
   }
 }
 
-template <int CI, int NCB, int NJ>
+template <int CI, int NCB, int NJ, int NW = 8>
 static int launch_upsw(const vo_conv1d_desc* d, hipStream_t st) {
   UpswArgs w;
   UpsArgs& a = w.u;
@@ -395,16 +393,16 @@ static int launch_upsw(const vo_conv1d_desc* d, hipStream_t st) {
   // resident workgroups only (persistent); run groups in multiples of 8 (one per XCD slot)
   const size_t lds_b = 2 * (size_t)NCB * CI * sizeof(bf16_t) + NCB * sizeof(float);
   int per_cu = 0;  // LDS- and register-limited resident workgroups per CU
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upsw_kernel<CI, NCB, NJ>, 512, lds_b) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, upsw_kernel<CI, NCB, NJ, NW>, NW * 64, lds_b) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   const int slots = std::max(1, cus * per_cu / 8);         // workgroup slots per XCD
   const int rg_per_xcd = std::max(1, slots / w.ncb_n);
-  const int need = (a.units + 8 * 8 - 1) / (8 * 8);        // >= 8 units per wave
+  const int need = (a.units + 8 * NW - 1) / (8 * NW);      // >= 8 units per wave
   w.rgroups = std::min(8 * rg_per_xcd, std::max(1, need));
   const int grid = 8 * w.ncb_n * ((w.rgroups + 7) / 8);
   const size_t lds = 2 * (size_t)NCB * CI * sizeof(bf16_t) + NCB * sizeof(float);
-  hipLaunchKernelGGL((upsw_kernel<CI, NCB, NJ>), dim3((unsigned)grid), dim3(512), lds, st, w);
+  hipLaunchKernelGGL((upsw_kernel<CI, NCB, NJ, NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, w);
   VO_RETURN_LAUNCH();
 }
 
@@ -464,6 +462,9 @@ int vo_ups_try(const vo_conv1d_desc* d, hipStream_t st, int* handled) {
     if (cfg == 5) return launch_upsw<256, 64, 2>(d, st);
     return launch_upsw<256, 128, 1>(d, st);
   }
+  // ups0 (512 -> 256, k16 s8) as 64-column blocks on 4-wave workgroups (one wave per SIMD; its
+  // 16 x-fragment k-steps spill at 8 waves) took 230 us against 145 on the tiled conv
+  // (profiles/r01l/ups_probe_ups0.txt): ups0 stays on the tiled conv.
   if (d->Ci == 64 && d->Co == 64 && d->up_cout % 16 == 0) {
     *handled = 1;
     if (cfg == 2) return launch_ups<64, 64, 2>(d, st);
