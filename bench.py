@@ -1,29 +1,37 @@
 #!/usr/bin/env python3
 """End-to-end visual-onomatopoeia -> 22.05 kHz waveform throughput on MI355X.
 
-One step = one batch of B synthetic rendered-glyph strips (B x 1 x 24 x 102*T_src, T_src=12)
-through the acoustic model (teacher-forced durations summing to T_mel=512 frames, predicted
-energy) and the HiFi-GAN V1 generator on its postnet mel
-(config C3 shape per utterance) -> B x 131,072 samples.  Inputs are resident in HBM
-before the timed region.  Multi-GPU: one process per GPU (torchrun), every rank
-synthesises its own batch (utterances are independent: replicas, no data-path
-collective), only the timing uses a barrier and a MAX all-reduce.
+Headline (``--mode infer``, the default): one step = one batch of B synthetic rendered-glyph
+strips (B x 1 x 24 x 102*T_src, T_src=12) through the acoustic model (teacher-forced durations
+summing to T_mel=512 frames, predicted energy) and the HiFi-GAN V1
+generator on its postnet mel (config C3 shape per utterance) -> B x 131,072 samples.  The same
+run also measures BASELINE.json's per-config lines C2 (acoustic only, B=32, mel-frames/s) and
+C3 (generator only, B=64 x 80 x 512, samples/s), each with its own roofline, under
+``configs`` of the one JSON line.  Inputs are resident in HBM before every timed region.
+Multi-GPU: one process per GPU (torchrun), every rank synthesises its own batch (utterances
+are independent: replicas, no data-path collective), only the timing uses a
+barrier and a MAX all-reduce.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--precision mixed]
+                    [--mode infer|c2|c3|train|gan] [--comm-dtype fp32|bf16]
 
 Prints ONE JSON line (rank 0) with the metric of BASELINE.json, the dominant kernel's
-roofline (HIP events on the launching stream over the timed region) and the CPU
-baseline (the oracle restatement timed on this host, bounded sample).
+roofline (HIP events on the launching stream over the timed region) and the CPU baseline
+(the oracle restatement timed on this host: BASELINE.md's C1 / C2 / C3 plan).
 """
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
-import numpy as np
-import torch
+# before the HIP runtime initialises (graphed training steps, visual_onoma_to_wave_amd/train.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 for p in (REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden")):
@@ -35,6 +43,7 @@ HOP = 256
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (no sparsity)
 F32_PEAK_TFLOPS = 157.3
+TRAFFIC_FILE = os.path.join("profiles", "traffic_r01.json")  # committed rocprofv3 PMC passes
 
 
 def parse():
@@ -42,37 +51,257 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 32; c3: 64; gan: 16)")
     ap.add_argument("--src-len", type=int, default=12)
     ap.add_argument("--mel-len", type=int, default=512)
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="infer: skip the C2 / C3 sub-measurements")
     ap.add_argument("--no-graph", action="store_true", help="train / gan modes: eager steps instead of one HIP graph")
-    ap.add_argument("--mode", default="infer", choices=["infer", "train", "gan"],
-                    help="infer: end-to-end synthesis (headline); train: C4 training step (DDP); "
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="train / gan under torchrun: gradient all-reduce dtype")
+    ap.add_argument("--mode", default="infer", choices=["infer", "c2", "c3", "train", "gan"],
+                    help="infer: end-to-end synthesis (headline, with C2 / C3 sub-lines); c2: acoustic model "
+                         "only; c3: HiFi-GAN generator only (B=64); train: C4 training step (DDP); "
                          "gan: C5 HiFi-GAN training step (DDP)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = {"c3": 64, "gan": 16}.get(a.mode, 32)  # gan: scripts/hifigan/config.json batch_size
+    return a
 
+
+# ----------------------------------------------------------------------------------- timing helpers
+
+def timed(fn, steps, dist):
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+def _pmc_traffic():
+    tf = os.path.join(REPO, TRAFFIC_FILE)
+    if not os.path.exists(tf):
+        return {}
+    with open(tf) as f:
+        return {k: v.get("hbm_bytes_per_launch") for k, v in json.load(f).items()}
+
+
+def roofline(ks, peak, label, batch=32):
+    """Dominant tagged kernel (largest total time) -> the roofline object of the bench line.
+    The committed PMC traffic was measured at B = 32 per launch; per-launch bytes scale with B."""
+    if not ks:
+        return None
+    tag, d = max(ks.items(), key=lambda kv: kv[1]["total_ms"])
+    achieved = d["flops_per_launch"] / (d["avg_ms"] * 1e-3) / 1e12
+    pmc = {k: (v * batch / 32.0 if v else v) for k, v in _pmc_traffic().items()}
+    stages = {}
+    for k, v in sorted(ks.items()):
+        stages[k] = {"kernel": " + ".join(v["kernels"]), "avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
+                     "tflops": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12, 1),
+                     "mfma_frac": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12 / peak, 3),
+                     "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1),
+                     # measured HBM bytes (committed PMC passes) over this run's launch time: the north
+                     # star's "HBM roofline on the MRF" for the narrow stages
+                     "hbm_frac_pmc": (round(pmc[k] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)
+                                      if pmc.get(k) else None)}
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": pmc.get(tag),
+            "traffic_source": (f"{TRAFFIC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes, committed; "
+                               "not measured in this run)") if pmc.get(tag) else None,
+            "kernel": f"{' + '.join(d['kernels'])} ({label(tag)})", "tag": tag,
+            "launches": d["launches"], "avg_launch_ms": round(d["avg_ms"], 4),
+            "flops_per_launch": d["flops_per_launch"], "algorithmic_bytes_per_launch": d["bytes_per_launch"],
+            "all_stages": stages}
+
+
+def _mrf_label(tag):
+    return f"HiFi-GAN MRF stage {tag[-1]}" if tag.startswith("mrf_s") else tag
+
+
+# ----------------------------------------------------------------------------------- models / inputs
+
+def build_models(device, precision, acoustic=True, vocoder=True):
+    from helpers import configs, hifigan_arrays, hifigan_h, vtts_arrays
+    from weights import load_into
+    from visual_onoma_to_wave_amd import hifigan
+    from visual_onoma_to_wave_amd.model import vTTS
+    m = g = None
+    if acoustic:
+        m = vTTS(*configs())
+        load_into(m, vtts_arrays())
+        m = m.to(device).eval().set_precision(precision)
+    if vocoder:
+        g = hifigan.Generator(hifigan.AttrDict(hifigan_h()))
+        load_into(g, hifigan_arrays())
+        g.eval()
+        g.remove_weight_norm()
+        g = g.to(device)
+        g.set_compute_dtype(torch.float32 if precision == "fp32" else torch.bfloat16)
+    return m, g
+
+
+def make_batch(seed, B, T_src, T_mel, device):
+    from visual_onoma_to_wave_amd import synth
+    b = synth.acoustic_batch(seed, B, T_src, T_mel)
+    t = {k: (torch.from_numpy(v).to(device) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+    return (t["audiotypes"], t["texts"], t["src_lens"], t["max_src_len"], t["mels"], t["mel_lens"],
+            t["max_mel_len"], None, None, t["d_targets"], t["images"], None, True)
+
+
+def make_mels(seed, B, T, device):
+    """C3 input: mel = clamp(N(-5, 2), -11.513, 2.5)."""
+    gen = torch.Generator().manual_seed(seed)
+    return (torch.randn(B, 80, T, generator=gen) * 2 - 5).clamp(-11.513, 2.5).to(device)
+
+
+# ----------------------------------------------------------------------------------- CPU baseline
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(budget_s, T_src, T_mel, B_headline):
+    """BASELINE.md's plan on the oracle (CPU fp32 restatement, parity-pinned to the reference):
+    C1 single utterance x real time, the full C2 acoustic batch, C3 at B = 4; the headline value
+    is the end-to-end rate of a B_headline batch composed from the C2 and C3 rates."""
+    from helpers import hifigan_arrays, hifigan_h, stats, vtts_arrays
+    from oracle import acoustic as A
+    from oracle import vocoder as V
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 (os.cpu_count() is the host's)
+    torch.set_num_threads(threads)
+    sd = A.complete_state_dict(vtts_arrays(), stats()["energy"])
+    gsd = V.fold_weight_norm({k: torch.from_numpy(np.array(v)) for k, v in hifigan_arrays().items()})
+    h = hifigan_h()
+    es = stats()["energy"]
+
+    def rep(fn, share):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            n += 1
+            if time.perf_counter() - t0 >= share * budget_s or n >= 20:
+                break
+        return (time.perf_counter() - t0) / n, n
+
+    with torch.no_grad():
+        c1 = make_batch(1234, 1, 4, 50, "cpu")
+        t_c1, n1 = rep(lambda: V.generator(gsd, A.vtts_forward(sd, *c1[:11], energy_stats=es)[1].transpose(1, 2), h),
+                       0.15)
+        c2 = make_batch(1234, 32, T_src, T_mel, "cpu")
+        t_c2, n2 = rep(lambda: A.vtts_forward(sd, *c2[:11], energy_stats=es), 0.35)
+        mel4 = make_mels(1234, 4, T_mel, "cpu")
+        t_c3, n3 = rep(lambda: V.generator(gsd, mel4, h), 0.5)
+    c1_samples = 50 * HOP
+    c3_rate = 4 * T_mel * HOP / t_c3
+    t_e2e = t_c2 * B_headline / 32 + B_headline * T_mel * HOP / c3_rate
+    value = B_headline * T_mel * HOP / t_e2e
+    return {"value": value, "unit": "audio samples/s", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(), "threads": threads, "cpu_model": cpu_model(),
+            "sample": (f"oracle fp32 torch-CPU, {threads} threads: C1 {n1} x (B=1, T_src=4, T_mel=50), C2 {n2} x "
+                       f"(B=32, T_src={T_src}, T_mel={T_mel}), C3 {n3} x (B=4 x 80 x {T_mel}); value = "
+                       f"B={B_headline} end to end composed from the C2 and C3 rates"),
+            "x_realtime": value / SR,
+            "c1_x_realtime": c1_samples / t_c1 / SR, "c1_ms": round(t_c1 * 1e3, 2),
+            "c2_mel_frames_per_s": 32 * T_mel / t_c2, "c2_ms": round(t_c2 * 1e3, 1),
+            "c3_samples_per_s": c3_rate, "c3_ms_b4": round(t_c3 * 1e3, 1)}
+
+
+# ----------------------------------------------------------------------------------- inference configs
+
+def measure_c2(a, dev, dist, model=None):
+    """C2: acoustic forward, B=32 synthetic glyph batch, teacher-forced T_mel=512 (mel-frames/s);
+    roofline on the decoder FFN's k=9 conv (the largest share of the 771 GFLOP batch)."""
+    from visual_onoma_to_wave_amd.profiling import KernelTimer
+    rank = int(os.environ.get("RANK", "0"))
+    if model is None:
+        model, _ = build_models(dev, a.precision, vocoder=False)
+    B = 32 if a.mode != "c2" else a.batch
+    args = make_batch(1234 + rank, B, a.src_len, a.mel_len, dev)
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            model(*args)
+        timer = KernelTimer(["dec_ffn_w1"] if not a.no_kernel_timer else [])
+        with timer:
+            elapsed, out = timed(lambda: model(*args), a.steps, dist)
+    assert torch.isfinite(out[1]).all()
+    world = dist.get_world_size() if dist else 1
+    frames = B * a.mel_len * a.steps * world
+    peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
+    return {"metric": "C2 acoustic forward mel-frames/sec (vTTS, batch 32, teacher-forced T_mel=512)",
+            "value": round(frames / elapsed, 1), "unit": "mel-frames/s", "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "per_gpu_batch": B, "tflops_step": round(771.4e9 * B / 32 / (elapsed / a.steps) / 1e12, 1),
+            "roofline": roofline(timer.summary(), peak, lambda t: "decoder FFN w_1 conv, k=9 256->1024")}
+
+
+def measure_c3(a, dev, dist, gen=None):
+    """C3: HiFi-GAN generator on B=64 x 80 x 512 mels (samples/s); roofline on the MRF stage
+    with the largest total time."""
+    from visual_onoma_to_wave_amd.profiling import KernelTimer
+    rank = int(os.environ.get("RANK", "0"))
+    if gen is None:
+        _, gen = build_models(dev, a.precision, acoustic=False)
+    B = 64 if a.mode != "c3" else a.batch
+    mel = make_mels(1234 + rank, B, a.mel_len, dev)
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            gen(mel)
+        timer = KernelTimer([f"mrf_s{i}" for i in range(4)] if not a.no_kernel_timer else [])
+        with timer:
+            elapsed, wav = timed(lambda: gen(mel), a.steps, dist)
+    assert wav.shape == (B, 1, a.mel_len * HOP) and torch.isfinite(wav).all()
+    world = dist.get_world_size() if dist else 1
+    samples = B * a.mel_len * HOP * a.steps * world
+    peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
+    return {"metric": "C3 HiFi-GAN generator audio samples/sec (batch 64 x 80-mel x 512-frame)",
+            "value": round(samples / elapsed, 1), "unit": "audio samples/s",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "per_gpu_batch": B,
+            "x_realtime": round(samples / elapsed / SR, 1),
+            "tflops_step": round(2398848.0 * B * a.mel_len * HOP / (elapsed / a.steps) / 1e12, 1),
+            "roofline": roofline(timer.summary(), peak, _mrf_label, batch=B)}
+
+
+# ----------------------------------------------------------------------------------- training configs
 
 def bench_train(a, dev, rank, world, dist):
     """C4: scripts/04_train.py step (teacher-forced forward, FastSpeech2Loss, backward with the
-    bucketed RCCL all-reduce, clip 1.0, Adam + schedule) on B utterances per GPU."""
+    bucketed RCCL all-reduce, clip 1.0, Adam + schedule) on B utterances per GPU, replayed as
+    one HIP graph (the all-reduces captured on the side-stream branch) unless --no-graph."""
     from helpers import configs, vtts_arrays
     from weights import load_into
     from visual_onoma_to_wave_amd import synth
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
-    from visual_onoma_to_wave_amd.train import GradBucketer, train_step, unused_on_path
+    from visual_onoma_to_wave_amd.train import GradBucketer, GraphedTrainStep, train_step, unused_on_path
     pc, mc, tc = configs()
     m = vTTS(pc, mc, tc)
     load_into(m, vtts_arrays())
     m = m.to(dev).train().set_precision(a.precision)
-    graphed = dist is None and not a.no_graph  # one process: the whole step as a HIP graph replay
+    graphed = not a.no_graph
     opt = ScheduledOptim(m, tc, mc, 0, capturable=graphed)
     bk = None
+    comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
     if dist:
         skip = unused_on_path(m)
-        bk = GradBucketer([p for p in m.parameters() if id(p) not in skip])
+        bk = GradBucketer([p for p in m.parameters() if id(p) not in skip], comm_dtype=comm)
         bk.broadcast_parameters(m)
     b = synth.acoustic_batch(1234 + rank, a.batch, a.src_len, a.mel_len)
     t = {k: (torch.from_numpy(v).to(dev) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
@@ -80,30 +309,15 @@ def bench_train(a, dev, rank, world, dist):
              t["max_mel_len"], t["e_targets"], None, t["d_targets"], t["images"], None)
     loss_fn = FastSpeech2Loss()
     if graphed:
-        from visual_onoma_to_wave_amd.train import GraphedTrainStep
-        run = GraphedTrainStep(m, opt, loss_fn)
+        run = GraphedTrainStep(m, opt, loss_fn, bucketer=bk)
     else:
         def run(bt):
             return train_step(m, opt, loss_fn, bt, bucketer=bk)
     for _ in range(a.warmup):
         run(batch)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        losses = run(batch)
-        if os.environ.get("VO_BENCH_DEBUG"):
-            print("loss", [round(float(v.detach()), 4) for v in losses[:6]], file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, losses = timed(lambda: run(batch), a.steps, dist)
     frames = a.batch * a.mel_len * a.steps * world
+    n_grad = sum(p.numel() for p in (bk.params if bk else []))
     if rank == 0:
         print(json.dumps({
             "metric": "C4 training mel-frames/sec (FastSpeech2 + variance loss, DDP)", "value": round(frames / elapsed, 1),
@@ -111,8 +325,10 @@ def bench_train(a, dev, rank, world, dist):
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
             "final_loss": round(float(losses[0]), 5), "hip_graph": graphed,
+            "allreduce_bytes_per_step": n_grad * (2 if comm is not None else 4) if dist else 0,
             "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
-                       "seq_len": a.mel_len, "src_len": a.src_len, "parallelism": f"dp{world} (RCCL bucketed all-reduce)"}}))
+                       "seq_len": a.mel_len, "src_len": a.src_len,
+                       "parallelism": f"dp{world} (RCCL bucketed all-reduce, {a.comm_dtype})"}}))
 
 
 def bench_gan(a, dev, rank, world, dist):
@@ -128,8 +344,9 @@ def bench_gan(a, dev, rank, world, dist):
     load_into(g, hifigan_arrays())
     g = g.to(dev)
     torch.manual_seed(1234)  # identical discriminator init on every rank (broadcast anyway)
-    graphed = dist is None and not a.no_graph  # one process: the whole step as a HIP graph replay
-    tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev, graphed=graphed)
+    graphed = not a.no_graph
+    tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev, graphed=graphed,
+                                comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None)
     run = tr.step_graphed if graphed else tr.step
     tr.set_compute_dtype(torch.float32 if a.precision == "fp32" else torch.bfloat16)
     B, seg = a.batch, h.segment_size
@@ -142,20 +359,7 @@ def bench_gan(a, dev, rank, world, dist):
     x = x.transpose(1, 2).contiguous()  # (B, 32, 80) channels-last generator input
     for _ in range(a.warmup):
         run(x, y)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        losses = run(x, y)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, losses = timed(lambda: run(x, y), a.steps, dist)
     samples = B * seg * a.steps * world
     if rank == 0:
         print(json.dumps({
@@ -167,66 +371,10 @@ def bench_gan(a, dev, rank, world, dist):
             "losses": {k: round(float(v), 4) for k, v in losses.items()},
             "hip_graph": graphed,
             "config": {"workload": "C5 HiFi-GAN V1 train step", "per_gpu_batch": B, "global_batch": B * world,
-                       "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D)"}}))
+                       "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D, {a.comm_dtype})"}}))
 
 
-def build_models(device, precision):
-    from helpers import configs, hifigan_arrays, hifigan_h, vtts_arrays
-    from weights import load_into
-    from visual_onoma_to_wave_amd import hifigan
-    from visual_onoma_to_wave_amd.model import vTTS
-    m = vTTS(*configs())
-    load_into(m, vtts_arrays())
-    m = m.to(device).eval().set_precision(precision)
-    g = hifigan.Generator(hifigan.AttrDict(hifigan_h()))
-    load_into(g, hifigan_arrays())
-    g.eval()
-    g.remove_weight_norm()
-    g = g.to(device)
-    g.set_compute_dtype(torch.float32 if precision == "fp32" else torch.bfloat16)
-    return m, g
-
-
-def make_batch(seed, B, T_src, T_mel, device):
-    from visual_onoma_to_wave_amd import synth
-    b = synth.acoustic_batch(seed, B, T_src, T_mel)
-    t = {k: (torch.from_numpy(v).to(device) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
-    return (t["audiotypes"], t["texts"], t["src_lens"], t["max_src_len"], t["mels"], t["mel_lens"],
-            t["max_mel_len"], None, None, t["d_targets"], t["images"], None, True)
-
-
-def step(model, gen, args):
-    out = model(*args)
-    return gen.run(out[1])  # postnet mel is already channels-last (B, T, 80): no transpose
-
-
-def cpu_baseline(budget_s, T_src, T_mel):
-    """The oracle (CPU fp32 restatement, parity-pinned to the reference) on a bounded
-    sample of the same workload: B=1 utterances, end-to-end, timed on this host."""
-    from helpers import hifigan_arrays, hifigan_h, stats, vtts_arrays
-    from oracle import acoustic as A
-    from oracle import vocoder as V
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    sd = A.complete_state_dict(vtts_arrays(), stats()["energy"])
-    gsd = V.fold_weight_norm({k: torch.from_numpy(np.array(v)) for k, v in hifigan_arrays().items()})
-    h = hifigan_h()
-    args = make_batch(7, 1, T_src, T_mel, "cpu")
-    n, t0 = 0, time.perf_counter()
-    with torch.no_grad():
-        while True:
-            out = A.vtts_forward(sd, *args[:11], energy_stats=stats()["energy"])
-            V.generator(gsd, out[1].transpose(1, 2), h)
-            n += 1
-            if time.perf_counter() - t0 >= budget_s or n >= 50:
-                break
-    dt = time.perf_counter() - t0
-    samples = n * T_mel * HOP
-    return {"value": samples / dt, "unit": "audio samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (1 utterance: T_src={T_src}, T_mel={T_mel} -> {T_mel * HOP} samples), "
-                      f"oracle fp32 torch-CPU, {dt:.1f} s",
-            "x_realtime": samples / dt / SR}
-
+# ----------------------------------------------------------------------------------- main
 
 def main():
     a = parse()
@@ -240,82 +388,60 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    if a.mode == "gan":
-        if a.batch == 32:
-            a.batch = 16  # scripts/hifigan/config.json batch_size
-        bench_gan(a, dev, rank, world, dist)
+    try:
+        if a.mode == "gan":
+            bench_gan(a, dev, rank, world, dist)
+        elif a.mode == "train":
+            bench_train(a, dev, rank, world, dist)
+        elif a.mode in ("c2", "c3"):
+            res = (measure_c2 if a.mode == "c2" else measure_c3)(a, dev, dist)
+            if rank == 0:
+                res.update({"n_gpus": world, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                            "scaling": "weak", "vs_baseline": None,
+                            "dtype": {"mixed": "bf16 (encoder+variance adaptor fp32)", "bf16": "bf16",
+                                      "fp32": "f32"}[a.precision] if a.mode == "c2" else
+                            ("f32" if a.precision == "fp32" else "bf16"),
+                            "data": "synthetic (deterministic random weights)",
+                            "config": {"workload": a.mode.upper(), "per_gpu_batch": a.batch,
+                                       "global_batch": a.batch * world, "seq_len": a.mel_len,
+                                       "parallelism": f"replicas x{world} (no data-path collective)"}})
+                print(json.dumps(res))
+        else:
+            infer(a, dev, rank, world, dist)
+    finally:
         if dist:
             dist.destroy_process_group()
-        return
-    if a.mode == "train":
-        bench_train(a, dev, rank, world, dist)
-        if dist:
-            dist.destroy_process_group()
-        return
 
+
+def infer(a, dev, rank, world, dist):
+    from visual_onoma_to_wave_amd.profiling import KernelTimer
     model, gen = build_models(dev, a.precision)
     args = make_batch(1234 + rank, a.batch, a.src_len, a.mel_len, dev)
+
+    def step():
+        out = model(*args)
+        return gen.run(out[1])  # postnet mel is already channels-last (B, T, 80): no transpose
+
     with torch.no_grad():
         for _ in range(a.warmup):
-            step(model, gen, args)
-        torch.cuda.synchronize()
-
-        from visual_onoma_to_wave_amd.profiling import KernelTimer
-        tags = [f"mrf_s{i}" for i in range(4)]
-        timer = KernelTimer(tags if not a.no_kernel_timer else [])
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+            step()
+        timer = KernelTimer([f"mrf_s{i}" for i in range(4)] if not a.no_kernel_timer else [])
         with timer:
-            for _ in range(a.steps):
-                wav = step(model, gen, args)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+            elapsed, wav = timed(step, a.steps, dist)
     assert wav.shape == (a.batch, a.mel_len * HOP) and torch.isfinite(wav).all()
     samples = a.batch * a.mel_len * HOP * a.steps * world
     frames = a.batch * a.mel_len * a.steps * world
     value = samples / elapsed
+    peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
+    roof = roofline(timer.summary(), peak, _mrf_label, batch=a.batch)
 
-    # dominant kernel: the MRF stage with the largest total time (HIP events, same stream)
-    roof = None
-    ks = timer.summary()
-    if ks:
-        tag, d = max(ks.items(), key=lambda kv: kv[1]["total_ms"])
-        achieved = d["flops_per_launch"] / (d["avg_ms"] * 1e-3) / 1e12
-        peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
-        pmc = {}  # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_round.sh)
-        tf = os.path.join(REPO, "profiles", "traffic_r01.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                pmc = {k: v.get("hbm_bytes_per_launch") for k, v in json.load(f).items()}
-        traffic = pmc.get(tag)
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": f"{' + '.join(d['kernels'])} (HiFi-GAN MRF stage {tag[-1]})",
-                "launches": d["launches"], "avg_launch_ms": round(d["avg_ms"], 4),
-                "flops_per_launch": d["flops_per_launch"],
-                "algorithmic_bytes_per_launch": d["bytes_per_launch"],
-                "all_stages": {k: {"kernel": " + ".join(v["kernels"]), "avg_ms": round(v["avg_ms"], 4),
-                                   "launches": v["launches"],
-                                   "tflops": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12, 1),
-                                   "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1),
-                                   # measured HBM bytes (PMC) over this run's launch time: the
-                                   # north star's "HBM roofline on the MRF" for the narrow stages
-                                   "hbm_frac_pmc": (round(pmc[k] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)
-                                                    if pmc.get(k) else None)}
-                               for k, v in sorted(ks.items())}}
+    configs = None
+    if not a.no_configs:  # BASELINE.json's per-config lines, same run, same models
+        configs = {"C2": measure_c2(a, dev, dist, model), "C3": measure_c3(a, dev, dist, gen)}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        cpu = cpu_baseline(a.cpu_seconds, a.src_len, a.mel_len)
+        cpu = cpu_baseline(a.cpu_seconds, a.src_len, a.mel_len, a.batch)
 
     if rank == 0:
         line = {
@@ -333,11 +459,10 @@ def main():
             "mel_frames_per_s": round(frames / elapsed, 1),
             "x_realtime": round(value / SR, 1),
             "roofline": roof,
+            "configs": configs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if dist:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

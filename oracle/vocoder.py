@@ -54,17 +54,23 @@ def upsample(sd, i, x, k, u):
                               padding=(k - u) // 2)
 
 
+def mrf(sd, i, x, h):
+    """Multi-receptive-field fusion of upsampling stage i: the mean of its num_kernels ResBlocks,
+    scripts/hifigan/models.py:155-160."""
+    nk = len(h["resblock_kernel_sizes"])
+    xs = None
+    for j, (rk, rd) in enumerate(zip(h["resblock_kernel_sizes"], h["resblock_dilation_sizes"])):
+        r = resblock(sd, f"resblocks.{i * nk + j}", x, rk, rd)
+        xs = r if xs is None else xs + r
+    return xs / nk
+
+
 def generator(sd, mel, h):
     """Generator.forward, scripts/hifigan/models.py:149-165 (folded weights)."""
-    nk = len(h["resblock_kernel_sizes"])
     x = F.conv1d(mel, sd["conv_pre.weight"], sd["conv_pre.bias"], padding=3)
     for i, (u, k) in enumerate(zip(h["upsample_rates"], h["upsample_kernel_sizes"])):
         x = upsample(sd, i, x, k, u)
-        xs = None
-        for j, (rk, rd) in enumerate(zip(h["resblock_kernel_sizes"], h["resblock_dilation_sizes"])):
-            r = resblock(sd, f"resblocks.{i * nk + j}", x, rk, rd)
-            xs = r if xs is None else xs + r
-        x = xs / nk
+        x = mrf(sd, i, x, h)
     x = F.leaky_relu(x)  # default slope 0.01, models.py:161
     x = F.conv1d(x, sd["conv_post.weight"], sd["conv_post.bias"], padding=3)
     return torch.tanh(x)

@@ -1,6 +1,10 @@
 import os
 import sys
 
+# before anything initialises the HIP runtime (torch.cuda.is_available() in the hooks below):
+# HIP-graph replays need the CLR's ordinary graph-launch path (visual_onoma_to_wave_amd/train.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

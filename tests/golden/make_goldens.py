@@ -240,5 +240,37 @@ def main():
     print("meta:", {k: v for k, v in meta.items() if "rows" not in k})
 
 
+def long_goldens():
+    """Multi-tile vocoder goldens (round 2): the MRF of every stage (sum of the three ResBlocks / 3,
+    hifigan/models.py:155-160) on inputs long enough to cross several 256 / 512-row tiles of the
+    fused kernels and two utterances, and the whole Generator at T = 80 mel frames (stage 3 runs
+    20,480 rows).  Activations are stored as float16 (inputs drawn fp16-exact, outputs rounded:
+    rel-L2 ~3e-4 of storage error, far below the 1e-2 bf16 tolerance they pin)."""
+    import torch
+    import hifigan
+    with open(os.path.join(REF, "scripts/hifigan/config.json")) as f:
+        h = hifigan.AttrDict(json.load(f))
+    gen = hifigan.Generator(h)
+    gspec = spec_of(gen.state_dict())
+    load_into(gen, make_state_dict(gspec, GEN_SEED, HIFIGAN_UPS_STRIDES))
+    gen.eval()
+    gen.remove_weight_norm()
+    rng = np.random.default_rng(2024)
+    with torch.no_grad():
+        for i, (C, T) in enumerate(((256, 600), (128, 1100), (64, 1100), (32, 1100))):
+            x = rng.normal(0, 1, size=(2, C, T)).astype(np.float16).astype(np.float32)
+            xt = torch.from_numpy(x)
+            y = sum(gen.resblocks[3 * i + j](xt) for j in range(3)) / 3
+            save(f"mrf_s{i}_long", x=x.astype(np.float16), out=t2n(y).astype(np.float16))
+        from visual_onoma_to_wave_amd import synth
+        mel = synth.mels(rng, 2, 80)
+        save("generator_long", mel=mel, wav=t2n(gen(torch.from_numpy(mel))))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["long"]:
+        import_reference()
+        long_goldens()
+    else:
+        main()
+        long_goldens()

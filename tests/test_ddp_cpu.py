@@ -24,38 +24,76 @@ def _model():
                                torch.nn.Tanh(), torch.nn.Linear(200, 4))
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, comm_dtype=None, set_to_none=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from visual_onoma_to_wave_amd.train import GradBucketer
     m = _model()
     # tiny buckets so several collectives are in flight during backward
-    bk = GradBucketer(m.parameters(), bucket_mb=0.05)
+    bk = GradBucketer(m.parameters(), bucket_mb=0.05, comm_dtype=comm_dtype)
     bk.broadcast_parameters(m)
     torch.manual_seed(123)
     x, y = torch.randn(8, 16), torch.randn(8, 4)
     xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
-    for _ in range(2):  # two steps: the bucket state resets between steps
-        m.zero_grad()
+    for _ in range(3):  # several steps: the bucket state resets between steps
+        m.zero_grad(set_to_none=set_to_none)
         ((m(xs) - ys) ** 2).mean().backward()
         bk.finish()
+    # the averaged gradients live in the persistent flat buckets (no per-step concatenation)
+    flat_ptrs = [(f.data_ptr(), f.data_ptr() + f.numel() * f.element_size()) for f in bk.flat]
+    assert all(any(lo <= p.grad.data_ptr() < hi for lo, hi in flat_ptrs) for p in m.parameters())
     out[rank] = [p.grad.clone() for p in m.parameters()]
     assert len(bk.buckets) >= 3
     dist.destroy_process_group()
 
 
-def test_bucketed_allreduce_matches_global_batch():
+@pytest.mark.parametrize("comm_dtype,set_to_none,tol", [(None, True, 1e-5), (None, False, 1e-5),
+                                                        (torch.bfloat16, True, 1e-2)])
+def test_bucketed_allreduce_matches_global_batch(comm_dtype, set_to_none, tol):
+    """fp32 and bf16-on-the-wire buckets; zero_grad(set_to_none=False) accumulates into the bucket
+    views in place (no gather copy)."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, comm_dtype, set_to_none), nprocs=world, join=True)
     m = _model()
     torch.manual_seed(123)
     x, y = torch.randn(8, 16), torch.randn(8, 4)
     ((m(x) - y) ** 2).mean().backward()
     for r in range(world):
         for g, p in zip(out[r], m.parameters()):
-            torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(g, p.grad, rtol=tol, atol=tol * 1e-1)
+
+
+def _init_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    from visual_onoma_to_wave_amd.train import init_distributed
+    got = init_distributed()
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    out[rank] = (got, float(t), dist.get_backend())
+    dist.destroy_process_group()
+
+
+def test_init_distributed_torchrun_env():
+    """The INTEGRATION.md recipe's first call: torchrun-style env -> (rank, world, local_rank) and a
+    working process group (gloo on a host without GPUs); without WORLD_SIZE: single process."""
+    from visual_onoma_to_wave_amd.train import init_distributed
+    saved = {k: os.environ.pop(k, None) for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    try:
+        assert init_distributed() == (0, 1, 0)
+        assert not dist.is_initialized()
+    finally:
+        for k, v in saved.items():
+            if v is not None:
+                os.environ[k] = v
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_init_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r] == ((r, world, r), 3.0, "gloo")
 
 
 def test_unused_parameters_are_identified():

@@ -271,8 +271,10 @@ def test_trainer_step_bf16():
 
 
 def test_trainer_graphed_matches_eager():
-    """HIP-graph replays of the training step (HifiGanTrainer.step_graphed) against the same
-    number of eager steps from the same initial state (fp32 compute; atomics reorder sums)."""
+    """HIP-graph replays of the training step (HifiGanTrainer.step_graphed, back to back, no host
+    wait; the warm-up steps before the capture are undone) against the same number of eager steps
+    from the same initial state, with an epoch boundary (ExponentialLR on the device-tensor
+    learning rates of the captured AdamW) in the middle (fp32 compute; atomics reorder sums)."""
     from visual_onoma_to_wave_amd import hifigan
     h = hifigan.AttrDict(hifigan_h())
     mel = (torch.randn(2, 32, 80, generator=torch.Generator().manual_seed(5)) - 4).cuda()
@@ -282,12 +284,10 @@ def test_trainer_graphed_matches_eager():
         torch.manual_seed(1234)
         g = _gen("cuda")
         tr = hifigan.HifiGanTrainer(g, h, graphed=graphed).set_compute_dtype(torch.float32)
-        if graphed:
-            for _ in range(9):  # 1 eager warm-up step + capture, then 9 back-to-back replays
-                losses = tr.step_graphed(mel, y, warmup=1)
-        else:
-            for _ in range(10):
-                losses = tr.step(mel, y)
+        for epoch in range(2):
+            for _ in range(5):
+                losses = tr.step_graphed(mel, y, warmup=2) if graphed else tr.step(mel, y)
+            tr.end_epoch()
         torch.cuda.synchronize()
         finals.append(({k: float(v) for k, v in losses.items()},
                        torch.cat([p.detach().flatten().cpu() for p in g.parameters()]),

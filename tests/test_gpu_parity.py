@@ -3,7 +3,7 @@
 Tolerances (relative L2 unless stated):
   * fp32 mode (exact-f32 MFMA; only summation order differs from oneDNN):  2e-5 per
     module, 1e-4 for whole-model outputs;
-  * bf16 kernels (bf16 operands, fp32 accumulation):  2e-2 (measured reference-vs-
+  * bf16 kernels (bf16 operands, fp32 accumulation):  1e-2 (measured reference-vs-
     reference bf16 drift is 3.4e-3 for the Generator, 4.5e-3 for vTTS, SURVEY.md 8(c));
   * integer / index results (LengthRegulator frames + mel_len, bucket indices, masks,
     d_rounded):  bit-exact.
@@ -18,7 +18,7 @@ from weights import load_into
 
 pytestmark = pytest.mark.gpu
 
-F32_MOD, F32_MODEL, BF16 = 2e-5, 1e-4, 2e-2
+F32_MOD, F32_MODEL, BF16 = 2e-5, 1e-4, 1e-2
 
 
 def cuda(a):
@@ -238,13 +238,22 @@ def test_upsamplers(gen, dt, tol):
         assert rel_l2(y.cpu().numpy().transpose(0, 2, 1), ref) < tol, i
 
 
-@pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MODEL), (torch.bfloat16, BF16)])
-def test_generator(gen, dt, tol):
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_generator(gen, dt):
+    """fp32 <= 1e-4; bf16 held to helpers.bf16_bar: max(1e-2, 1.1 x the reference's own bf16
+    autocast drift on these weights, 1.3e-2)."""
+    import numpy as _np
+    from helpers import bf16_bar, oracle_generator_bf16
+    from oracle import vocoder as V
     g = golden("generator")
     gen.set_compute_dtype(dt)
     with torch.no_grad():
         wav = gen(cuda(g["mel"]))
     assert wav.shape == g["wav"].shape
+    tol = F32_MODEL
+    if dt == torch.bfloat16:
+        gsd = V.fold_weight_norm({k: torch.from_numpy(_np.array(v)) for k, v in hifigan_arrays().items()})
+        tol = bf16_bar(g["wav"], oracle_generator_bf16(gsd, torch.from_numpy(g["mel"]), hifigan_h()))
     assert rel_l2(wav.cpu(), g["wav"]) < tol
 
 

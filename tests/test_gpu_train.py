@@ -100,9 +100,10 @@ def test_training_reduces_loss(device):
 
 def test_graphed_train_step_matches_eager(device):
     """train.GraphedTrainStep (HIP-graph replay with the capturable Adam and a device-tensor
-    learning rate) against the same number of eager train_step calls (fp32, dropout off).  The
-    weight-gradient atomics make two eager runs differ slightly; training amplifies that, so the
-    graphed run is held to the spread of a second eager run, not to zero."""
+    learning rate, replays launched back to back with no host wait) against the same number of
+    eager train_step calls (fp32, dropout off).  The warm-up steps before the capture are undone,
+    so 12 calls are 12 updates.  The weight-gradient atomics make two eager runs differ slightly;
+    training amplifies that, so the graphed run is held to the spread of a second eager run."""
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
     from visual_onoma_to_wave_amd.train import GraphedTrainStep, train_step
     pc, mc, tc = configs()
@@ -116,29 +117,67 @@ def test_graphed_train_step_matches_eager(device):
         m = m.to(device).train().set_precision("fp32")
         _no_dropout(m)
         opt = ScheduledOptim(m, tc, mc, 0, capturable=graphed)
+        per_step = []
         if graphed:
-            run = GraphedTrainStep(m, opt, FastSpeech2Loss(), warmup=1)
-            for _ in range(11):  # 1 eager warm-up step + capture, then 11 replays
+            run = GraphedTrainStep(m, opt, FastSpeech2Loss(), warmup=3)
+            for _ in range(12):
                 losses = run(batch)
+                per_step.append(losses[0].detach().clone())  # stream-ordered read, no host wait
         else:
             for _ in range(12):
                 losses = train_step(m, opt, FastSpeech2Loss(), batch)
+                per_step.append(losses[0].detach().clone())
         torch.cuda.synchronize()
         assert opt.current_step == 12
-        finals.append((np.array([float(x) for x in losses]),
+        finals.append((np.array([float(x) for x in per_step]),
                        torch.cat([p.detach().flatten().cpu() for p in m.parameters()])))
     (l0, p0), (l1, p1), (lg, pg) = finals
+    assert np.isfinite(lg).all()
     p_noise = float((p1 - p0).norm() / p0.norm())
     p_err = float((pg - p0).norm() / p0.norm())
     l_noise, l_err = float(np.abs(l1 - l0).max()), float(np.abs(lg - l0).max())
-    print(f"graphed vs eager: params {p_err:.2e} (eager spread {p_noise:.2e}), losses {l_err:.2e} "
+    print(f"graphed vs eager: params {p_err:.2e} (eager spread {p_noise:.2e}), per-step losses {l_err:.2e} "
           f"(eager spread {l_noise:.2e})")
     # twelve Adam steps at lr up to 3e-4 move the weights by ~1e-2 of their norm and the loss
-    # 25 -> 7.5: a replay with a stale input / learning rate / packed weight differs at that scale.
-    # At this size the eager runs can be bit-identical (single-split weight / bias gradients), and
-    # the capturable Adam's device-side bias correction then leaves ~3e-4 after 12 steps.
+    # 25 -> 7.5: a replay with a stale input / learning rate / packed weight, or an extra warm-up
+    # update, differs at that scale.
     assert p_err < max(10 * p_noise, 5e-4) and p_err < 1e-3
     assert l_err < max(10 * l_noise, 1e-2)
+
+
+def test_inference_after_graphed_training_uses_new_weights(device):
+    """Replays update parameters without bumping their version counters: the inference pack
+    cache must not serve weights packed before the graphed steps."""
+    from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
+    from visual_onoma_to_wave_amd.train import GraphedTrainStep
+    pc, mc, tc = configs()
+    tc = dict(tc)
+    tc["optimizer"] = dict(tc["optimizer"], warm_up_step=10, init_lr=1e-3)
+    g = golden("vtts_tf")
+    batch = _batch(g, device)
+    m = vTTS(pc, mc, tc)
+    load_into(m, vtts_arrays())
+    m = m.to(device).set_precision("fp32")
+    _no_dropout(m)
+    args = tuple(batch[1:]) + (True,)
+
+    def infer(model):
+        model.eval()
+        with torch.no_grad():
+            out = model(*args)[1].clone()
+        model.train()
+        return out
+    before = infer(m)
+    run = GraphedTrainStep(m, ScheduledOptim(m, tc, mc, 0, capturable=True), FastSpeech2Loss(), warmup=1)
+    for _ in range(3):
+        run(batch)
+    after = infer(m)
+    fresh = vTTS(pc, mc, tc).to(device).set_precision("fp32")
+    fresh.load_state_dict(m.state_dict())
+    ref = infer(fresh)
+    torch.cuda.synchronize()
+    assert rel_l2(after.cpu(), ref.cpu()) < 1e-6
+    assert rel_l2(after.cpu(), before.cpu()) > 1e-4
 
 
 @pytest.mark.parametrize("dt,D,with_res,with_lens", [

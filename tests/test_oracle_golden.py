@@ -169,3 +169,17 @@ def test_upsamplers(gsd):
 def test_generator(gsd):
     g = golden("generator")
     assert rel_l2(V.generator(gsd, t(g["mel"]), hifigan_h()), g["wav"]) < TOL
+
+
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
+def test_mrf_long(gsd, stage):
+    """Multi-tile MRF goldens (sum of the stage's three ResBlocks / 3 on T = 600 / 1100 rows,
+    B = 2): outputs stored as float16, so the bound is the storage rounding (~3e-4)."""
+    g = golden(f"mrf_s{stage}_long")
+    out = V.mrf(gsd, stage, t(g["x"]).float(), hifigan_h())
+    assert rel_l2(out, g["out"].astype(np.float32)) < 1e-3
+
+
+def test_generator_long(gsd):
+    g = golden("generator_long")
+    assert rel_l2(V.generator(gsd, t(g["mel"]), hifigan_h()), g["wav"]) < TOL

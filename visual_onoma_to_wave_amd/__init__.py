@@ -6,4 +6,12 @@ in hand-written HIP kernels for gfx950 behind the C ABI in ``include/vonoma.h``
 (``csrc/`` -> ``lib/libvonoma.so``).  See DESIGN.md.
 """
 
-__version__ = "0.1.0"
+import os as _os
+
+# HIP-graph training replays need the CLR's ordinary graph-launch path: with "packet capture"
+# (the ROCm default) replays of the training step computed wrong values on this runtime
+# (train.py, DESIGN.md section 7).  Read once when the HIP runtime initialises: effective when
+# this package is imported before the first CUDA call (an explicit user setting wins).
+_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
+__version__ = "0.2.0"

@@ -4,7 +4,8 @@ Each module keeps its parameters in the reference's checkpoint layout (same attr
 names, shapes and state-dict keys) and, on first use on a device, packs them once into
 the layout its kernels read (``[K][Co][Ci]``, BatchNorm / weight-norm folded, fused
 QKV ...).  The pack is cached per (device, compute dtype) and rebuilt only when a
-parameter's version counter moves (load_state_dict, optimizer step).
+parameter's version counter moves (load_state_dict, optimizer step) or a HIP-graph replay
+has updated the parameters (``invalidate_packs``).
 
 Precision ("compute dtype") is a per-module attribute:
   * torch.float32  -- exact-f32 MFMA everywhere (the parity mode);
@@ -17,6 +18,15 @@ hard part 1) -- and runs the decoder, PostNet and vocoder in bf16.
 import torch
 import torch.nn as nn
 
+_GENERATION = [0]
+
+
+def invalidate_packs():
+    """Drop every module's packed-weight cache.  HIP-graph replays of a training step update
+    parameters in place without bumping their version counters, so the graphed steps call this
+    after each replay (and after capture)."""
+    _GENERATION[0] += 1
+
 
 class HipModule(nn.Module):
     compute_dtype = torch.bfloat16
@@ -27,7 +37,7 @@ class HipModule(nn.Module):
 
     def _packed(self, device, builder, dtype=None):
         dtype = dtype or self.compute_dtype
-        key = (str(device), dtype, self._params_version())
+        key = (str(device), dtype, _GENERATION[0], self._params_version())
         cache = self.__dict__.setdefault("_pack_cache", {})
         hit = cache.get("key")
         if hit != key:

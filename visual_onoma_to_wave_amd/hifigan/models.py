@@ -167,22 +167,28 @@ class Generator(HipModule):
             w, b, cout, u, pad = p["ups"][i]
             x = ops.conv1d(x, w, b, Co=u * cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=LRELU_SLOPE,
                            transposed=dict(stride=u, pad=pad, cout=cout), out_dtype=dt, compute_dtype=dt)
-            xs = torch.empty_like(x)
-            stage = i if self.num_upsamples == 4 else None
-            timer = profiling.active()
-            tag = f"mrf_s{i}"
-            # the stage's ResBlock launches are consecutive: one event pair for all of them
-            grp = timer.group(tag) if (stage is not None and timer is not None and timer.watching(tag)) \
-                else contextlib.nullcontext()
-            with grp:
-                for j in range(self.num_kernels):
-                    rb = self.resblocks[i * self.num_kernels + j]
-                    rb.compute_dtype = dt
-                    rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
-                           stage=stage)
-            x = xs
+            x = self.mrf(i, x)
         wk, bp = p["post"]
         return ops.conv_post(x, wk, bp, slope=0.01)
+
+    def mrf(self, i, x):
+        """Multi-receptive-field fusion of upsampling stage i (hifigan/models.py:155-160):
+        (sum_j ResBlock_{i,j}(x)) / num_kernels on channels-last x (B, T, C) in the compute
+        dtype; the ResBlocks accumulate into one output in their epilogues."""
+        xs = torch.empty_like(x)
+        stage = i if self.num_upsamples == 4 else None
+        timer = profiling.active()
+        tag = f"mrf_s{i}"
+        # the stage's ResBlock launches are consecutive: one event pair for all of them
+        grp = timer.group(tag) if (stage is not None and timer is not None and timer.watching(tag)) \
+            else contextlib.nullcontext()
+        with grp:
+            for j in range(self.num_kernels):
+                rb = self.resblocks[i * self.num_kernels + j]
+                rb.compute_dtype = self.compute_dtype
+                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
+                       stage=stage)
+        return xs
 
     def train_forward(self, mel_cl):
         """Differentiable forward for HiFi-GAN training (config C5): mel_cl (B, T, 80)

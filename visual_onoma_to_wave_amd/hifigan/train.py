@@ -18,7 +18,8 @@ import itertools
 
 import torch
 
-from ..train import GradBucketer, graph_fence
+from .. import _base
+from ..train import GradBucketer, TrainState, _check_graph_runtime
 from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiScaleDiscriminator, discriminator_loss,
                              feature_loss, generator_loss)
 
@@ -40,13 +41,15 @@ def _single(disc, wav, grad):
 
 
 class HifiGanTrainer:
-    """``graphed=True``: ``step_graphed`` replays the whole step (both optimiser steps
-    included) as one HIP graph captured after eager warm-up steps on a side stream -- the step
-    launches ~4.6k kernels, and the eager loop is host-launch-bound.  AdamW then runs with
-    ``capturable=True``; ``end_epoch`` drops the graph so the next step re-captures with the
-    decayed learning rate."""
+    """``graphed=True``: ``step_graphed`` replays the whole step (both optimiser steps and, with
+    ``distributed=True``, both bucketed RCCL all-reduces included) as one HIP graph captured
+    after eager warm-up steps on a side stream whose effects are undone before the first replay
+    -- the step launches ~4.6k kernels, and the eager loop is host-launch-bound.  AdamW then runs
+    with ``capturable=True`` and device-tensor learning rates, so ``end_epoch``'s ExponentialLR
+    decay is written into the captured step without re-capturing."""
 
-    def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None, graphed=False):
+    def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None, graphed=False,
+                 comm_dtype=None):
         self.generator = generator
         device = device or next(generator.parameters()).device
         self.mpd = (mpd or MultiPeriodDiscriminator()).to(device)
@@ -54,18 +57,21 @@ class HifiGanTrainer:
         self.h = h
         self.graphed = graphed
         self._graph = None
-        self.optim_g = torch.optim.AdamW(generator.parameters(), h.learning_rate, betas=[h.adam_b1, h.adam_b2],
+        if graphed:
+            _check_graph_runtime()
+        lr = (lambda: torch.tensor(float(h.learning_rate), device=device)) if graphed else (lambda: h.learning_rate)
+        self.optim_g = torch.optim.AdamW(generator.parameters(), lr(), betas=[h.adam_b1, h.adam_b2],
                                          capturable=graphed)
         self.optim_d = torch.optim.AdamW(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
-                                         h.learning_rate, betas=[h.adam_b1, h.adam_b2], capturable=graphed)
+                                         lr(), betas=[h.adam_b1, h.adam_b2], capturable=graphed)
         self.sched_g = torch.optim.lr_scheduler.ExponentialLR(self.optim_g, gamma=h.lr_decay)
         self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
         self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,
                                 h.fmax_for_loss).to(device)
         self.bk_g = self.bk_d = None
         if distributed:
-            self.bk_g = GradBucketer(list(generator.parameters()))
-            self.bk_d = GradBucketer(list(self.msd.parameters()) + list(self.mpd.parameters()))
+            self.bk_g = GradBucketer(list(generator.parameters()), comm_dtype=comm_dtype)
+            self.bk_d = GradBucketer(list(self.msd.parameters()) + list(self.mpd.parameters()), comm_dtype=comm_dtype)
             self.bk_g.broadcast_parameters(generator)
             self.bk_d.broadcast_parameters(self.mpd)
             self.bk_d.broadcast_parameters(self.msd)
@@ -127,15 +133,15 @@ class HifiGanTrainer:
 
     def step_graphed(self, x_mel_cl, y, warmup=3):
         """``step`` as one HIP-graph replay (captured on the first call, after ``warmup`` eager
-        steps on a side stream).  Inputs are copied into the graph's static buffers; the
-        returned loss tensors are the graph's (overwritten by the next replay)."""
+        steps on a side stream whose updates are then undone).  Inputs are copied into the
+        graph's static buffers; the returned loss tensors are the graph's (overwritten by the next
+        replay).  No host synchronisation."""
         from . import gan_ops
         if not self.graphed:
             raise RuntimeError("HifiGanTrainer: construct with graphed=True to replay steps as a HIP graph")
-        if self.bk_g is not None:
-            raise RuntimeError("HifiGanTrainer: graphed steps are single-process (the RCCL buckets run eagerly)")
         if self._graph is None:
             self._x, self._y = x_mel_cl.clone(), y.clone()
+            snap = TrainState([self.generator, self.mpd, self.msd], [self.optim_g, self.optim_d])
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
@@ -146,18 +152,19 @@ class HifiGanTrainer:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 self._out = self.step(self._x, self._y)
+            snap.restore()
             gan_ops.reset_pack_cache()
+            _base.invalidate_packs()
             self._graph = graph
-        if getattr(self, "_done", None) is not None:
-            self._done.synchronize()  # train.graph_fence: replays are not launched back to back
         self._x.copy_(x_mel_cl)
         self._y.copy_(y)
         self._graph.replay()
-        self._done = graph_fence()
-        gan_ops.reset_pack_cache()
+        gan_ops.reset_pack_cache()  # replays move the parameters without bumping their versions
+        _base.invalidate_packs()
         return self._out
 
     def end_epoch(self):
+        """Per-epoch ExponentialLR decay (scripts/hifigan/config.json lr_decay); with graphed=True
+        the learning rates are device tensors the captured AdamW steps read."""
         self.sched_g.step()
         self.sched_d.step()
-        self._graph = self._done = None  # the captured AdamW step holds the old learning rate

@@ -16,7 +16,9 @@ class ScheduledOptim:
 
     def __init__(self, model, train_config, model_config, current_step, capturable=False):
         o = train_config["optimizer"]
-        params = [p for p in model.parameters() if p.requires_grad]
+        # every parameter, frozen ones included, as the reference does (scripts/model/optimizer.py:10):
+        # the param group then matches a reference checkpoint's optimizer state on resume
+        params = list(model.parameters())
         kw = dict(betas=o["betas"], eps=o["eps"], weight_decay=o["weight_decay"])
         if params and params[0].is_cuda:
             kw["fused"] = True

@@ -44,6 +44,10 @@ class vTTS(HipModule):
         back = torch.float32 if mode == "fp32" else torch.bfloat16
         self.precision = mode
         self.compute_dtype = back
+        # the decoder's residual stream (LengthRegulator output, LayerNorm outputs): fp32 unless
+        # everything is bf16 -- bf16 autocast of the reference keeps LayerNorm (and so the
+        # residual adds) in fp32, and a bf16 stream doubled the mixed mode's drift from fp32
+        self.stream_dtype = torch.bfloat16 if mode == "bf16" else torch.float32
         self.encoder.set_compute_dtype(front)
         self.variance_adaptor.set_compute_dtype(front)
         self.decoder.set_compute_dtype(back)
@@ -70,7 +74,7 @@ class vTTS(HipModule):
                               cls_idx=audiotypes)
         (x, e_pred, k_pred, log_d, d_rounded, mel_len, va_mask, va_l32) = self.variance_adaptor.run(
             x, src_l32, max_mel_len, e_targets, k_targets, d_targets, e_control, d_control,
-            out_dtype=self.decoder.compute_dtype)
+            out_dtype=self.stream_dtype)
         if d_targets is None:
             mel_masks, mel_l32 = va_mask, va_l32
         if mel_masks is None:

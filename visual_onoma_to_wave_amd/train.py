@@ -4,21 +4,50 @@ The reference trains with single-process ``nn.DataParallel`` (GPU0 broadcasts 14
 parameters and reduce-adds 139 MB of gradients every step, 04_train.py:75).  Here: one
 process per GPU (torchrun), parameters broadcast once, and a bucketed gradient all-reduce
 over RCCL/xGMI launched from per-parameter post-accumulate hooks, so each bucket's
-collective overlaps the rest of the backward on a separate stream.  Buckets are ~25 MB
-(about 6 for the 139 MB of fp32 gradients): large enough to run near link bandwidth on the
-7 point-to-point xGMI links, small enough that the first bucket starts early.  Parameters
-that receive no gradient on the path (``encoder.src_word_emb`` with image input,
-``variance_adaptor.kurt_embedding`` without kurtosis conditioning) are left out.
+collective overlaps the rest of the backward on a separate stream.
+
+Buckets are persistent flat buffers (~25 MB of fp32 gradients each: about 6 for the 139 MB
+of the acoustic model).  When a bucket's last gradient has been accumulated its gradients
+are gathered into the flat buffer by one multi-tensor copy on the compute stream (into a
+bf16 copy of the bucket with ``comm_dtype=torch.bfloat16``: 69 MB per step on the wire), the
+side stream all-reduces it in place (``ReduceOp.AVG`` on RCCL), and ``finish()`` points every
+``p.grad`` at its slice of the averaged bucket -- no per-step ``torch.cat`` / copy-back, no
+allocation.  Parameters that receive no gradient on the path (``encoder.src_word_emb`` with
+image input, ``variance_adaptor.kurt_embedding`` without kurtosis conditioning) are left out.
+
+The whole step -- forward, backward with the bucketed collectives, clipping and Adam -- is
+capturable as one HIP graph (``GraphedTrainStep``), on one GPU and under torchrun (the RCCL
+all-reduces are captured as graph nodes on the side-stream branch).
+
+HIP graphs and this ROCm runtime: with the CLR's graph "packet capture" launch path (on by
+default) replays of the C4 step computed wrong values -- losses read right after a replay
+were stale and the second replay produced NaN even with a host wait in between
+(tools/probes/graph_race_probe.py); the same graph launched through the ordinary node path
+(``DEBUG_CLR_GRAPH_PACKET_CAPTURE=0``) replays 30 steps back to back with no host wait and
+matches eager execution.  The package sets that variable at import (it is read when the HIP
+runtime initialises, so import this package -- or export the variable -- before the first CUDA
+call); ``GraphedTrainStep`` refuses to run when it is not in effect.
 """
+
+import os
 
 import torch
 import torch.distributed as dist
 
+from . import _base
+
+
+def packet_capture_disabled():
+    return os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+
 
 class GradBucketer:
-    """Bucketed, backward-overlapped gradient averaging across the default process group."""
+    """Bucketed, backward-overlapped gradient averaging across the default process group.
 
-    def __init__(self, params, bucket_mb=25.0, group=None):
+    ``comm_dtype``: dtype on the wire (None = the gradients' dtype, fp32; ``torch.bfloat16``
+    halves the bytes, accumulation error ~4e-3 relative per element)."""
+
+    def __init__(self, params, bucket_mb=25.0, group=None, comm_dtype=None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.params = [p for p in params if p.requires_grad]
@@ -35,35 +64,76 @@ class GradBucketer:
         if cur:
             self.buckets.append(cur)
         self.bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
-        self.flat = [None] * len(self.buckets)
-        self.pending = [0] * len(self.buckets)
-        self.works = []
-        self.side = torch.cuda.Stream() if self.params and self.params[0].is_cuda else None
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat, self.views, self.comm = [], [], []
+        for b in self.buckets:
+            dt = b[0].dtype
+            if any(p.dtype != dt for p in b):
+                raise TypeError("GradBucketer: one parameter dtype per bucket")
+            flat = torch.zeros(sum(p.numel() for p in b), dtype=dt, device=dev)
+            views, off = [], 0
+            for p in b:
+                views.append(flat[off: off + p.numel()].view_as(p))
+                off += p.numel()
+            self.flat.append(flat)
+            self.views.append(views)
+            self.comm.append(flat if comm_dtype in (None, dt) else torch.empty(flat.numel(), dtype=comm_dtype,
+                                                                               device=dev))
+        backend = dist.get_backend(group)
+        self.avg = backend == "nccl"  # RCCL averages on the wire; gloo sums, then we scale
+        self.side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self.hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
         self.reset()
 
     def reset(self):
         self.pending = [len(b) for b in self.buckets]
-        self.works = []
+        self.launched = [False] * len(self.buckets)
 
     def broadcast_parameters(self, module):
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, 0, group=self.group)
 
+    def _gather(self, i):
+        """Bucket i's gradients -> its comm buffer (one multi-tensor copy on the compute stream;
+        a parameter that got no gradient this step contributes zeros)."""
+        b, views = self.buckets[i], self.views[i]
+        src, dst = [], []
+        comm = self.comm[i]
+        tgt = views if comm is self.flat[i] else None
+        off = 0
+        for p, v in zip(b, views):
+            n = p.numel()
+            d = v if tgt is not None else comm[off: off + n].view_as(p)
+            off += n
+            g = p.grad
+            if g is None:
+                d.zero_()
+            elif g.data_ptr() != d.data_ptr():
+                src.append(g)
+                dst.append(d)
+        if src:
+            torch._foreach_copy_(dst, src)
+
     def _launch(self, i):
-        b = self.buckets[i]
-        main = torch.cuda.current_stream() if self.side is not None else None
+        self._gather(i)
+        buf = self.comm[i]
         if self.side is not None:
+            main = torch.cuda.current_stream(buf.device)
             self.side.wait_stream(main)
-            ctx = torch.cuda.stream(self.side)
+            with torch.cuda.stream(self.side):
+                self._reduce(i, buf)
         else:
-            ctx = _Null()
-        with ctx:
-            flat = torch.cat([p.grad.reshape(-1).float() for p in b])
-            flat.div_(self.world)
-            work = dist.all_reduce(flat, group=self.group, async_op=True)
-        self.flat[i] = flat
-        self.works.append((i, work))
+            self._reduce(i, buf)
+        self.launched[i] = True
+
+    def _reduce(self, i, buf):
+        if self.avg:
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(buf, group=self.group)
+            buf.div_(self.world)
+        if buf is not self.flat[i]:
+            self.flat[i].copy_(buf)
 
     def _ready(self, p):
         i = self.bucket_of[id(p)]
@@ -72,31 +142,17 @@ class GradBucketer:
             self._launch(i)
 
     def finish(self):
-        """Wait for every bucket, scatter the averaged gradients back (call after backward)."""
-        for i, n in enumerate(self.pending):
-            if n > 0:  # parameters that got no gradient this step
-                for p in self.buckets[i]:
-                    if p.grad is None:
-                        p.grad = torch.zeros_like(p)
+        """Launch the buckets that did not complete (parameters without a gradient this step),
+        join the side stream and point every ``p.grad`` at its averaged bucket slice."""
+        for i, done in enumerate(self.launched):
+            if not done:
                 self._launch(i)
-        for i, work in self.works:
-            work.wait()
-            off = 0
-            for p in self.buckets[i]:
-                n = p.numel()
-                p.grad.copy_(self.flat[i][off: off + n].view_as(p.grad))
-                off += n
         if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+        for b, views in zip(self.buckets, self.views):
+            for p, v in zip(b, views):
+                p.grad = v
         self.reset()
-
-
-class _Null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
 
 
 def unused_on_path(model):
@@ -125,53 +181,98 @@ def train_step(model, optimizer, loss_fn, batch, grad_clip=1.0, bucketer=None, u
     return losses
 
 
-def graph_fence():
-    """Host wait for a HIP-graph replay to finish, called right after ``replay()``.  Measured
-    on this ROCm: back-to-back replays of the acoustic step without it produced NaN losses after
-    ~10 steps; an event recorded after the replay and waited on before the next one did not
-    prevent it, a stream synchronize does (graphed and eager steps then match).  Costs ~1 %."""
-    torch.cuda.current_stream().synchronize()
-    return None
+class TrainState:
+    """Snapshot / restore of a model's parameters and buffers and of optimizers' state, so eager
+    warm-up steps before a HIP-graph capture leave no trace (each call of a graphed step applies
+    exactly one update).  Optimizer state tensors are restored in place (the capture records
+    their addresses); state created by the warm-up is reset to a fresh optimizer's (zeros)."""
+
+    def __init__(self, modules, optimizers):
+        self.tensors = []
+        for m in modules:
+            self.tensors += [t for t in list(m.parameters()) + list(m.buffers())]
+        self.optimizers = optimizers
+        with torch.no_grad():
+            self.saved = [t.detach().clone() for t in self.tensors]
+            self.state = [{id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                           for p, st in o.state.items()} for o in optimizers]
+
+    def restore(self):
+        with torch.no_grad():
+            for t, s in zip(self.tensors, self.saved):
+                t.copy_(s)
+            for o, saved in zip(self.optimizers, self.state):
+                for p, st in o.state.items():
+                    old = saved.get(id(p))
+                    for k, v in st.items():
+                        if not torch.is_tensor(v):
+                            if old is not None:
+                                st[k] = old[k]
+                            continue
+                        if old is not None and torch.is_tensor(old.get(k)):
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
+
+
+def _check_graph_runtime():
+    if not packet_capture_disabled():
+        raise RuntimeError(
+            "HIP-graph training needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in effect when the HIP runtime "
+            "initialises (visual_onoma_to_wave_amd sets it on import: import the package, or export the "
+            "variable, before the first CUDA call); with the CLR packet-capture launch path replays of the "
+            "training step compute wrong values (DESIGN.md section 7)")
 
 
 class GraphedTrainStep:
-    """``train_step`` replayed as one HIP graph (single process): forward, loss, backward, clip
-    and the Adam update are captured once after ``warmup`` eager steps on a side stream; each
-    call copies the batch into the graph's static tensors, advances the learning-rate schedule
-    (a device tensor, ``ScheduledOptim(capturable=True)``) and replays.  The acoustic step
-    launches ~1.9k kernels, so the eager loop is bound by host launch time.  Returns the
-    graph's loss tensors (overwritten by the next call)."""
+    """``train_step`` replayed as one HIP graph: forward, loss, backward (with ``bucketer``'s RCCL
+    all-reduces under torchrun), clip and the Adam update are captured once after ``warmup``
+    eager steps on a side stream whose effects are then undone (``TrainState``); each call copies
+    the batch into the graph's static tensors, advances the learning-rate schedule (a device
+    tensor, ``ScheduledOptim(capturable=True)``) and replays -- exactly one update per call, no
+    host synchronisation.  The acoustic step launches ~1.9k kernels, so the eager loop is bound
+    by host launch time.  Returns the graph's loss tensors (overwritten by the next call)."""
 
-    def __init__(self, model, optimizer, loss_fn, grad_clip=1.0, use_image=True, warmup=3):
+    def __init__(self, model, optimizer, loss_fn, grad_clip=1.0, use_image=True, warmup=3, bucketer=None):
+        _check_graph_runtime()
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.grad_clip, self.use_image, self.warmup = grad_clip, use_image, warmup
+        self.bucketer = bucketer
         self.graph = None
 
     def _body(self, batch):
         output = self.model(*(batch[1:]), self.use_image)
         losses = self.loss_fn(batch, output)
         losses[0].backward()
+        if self.bucketer is not None:
+            self.bucketer.finish()
         params = [p for p in self.model.parameters() if p.grad is not None]
         torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
         self.opt._optimizer.step()
         self.opt._optimizer.zero_grad(set_to_none=True)
         return losses
 
+    def _capture(self, batch):
+        self.static = tuple(b.clone() if torch.is_tensor(b) else b for b in batch)
+        snap = TrainState([self.model], [self.opt._optimizer])
+        step0 = self.opt.current_step
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                self.opt._update_learning_rate()
+                self._body(self.static)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._body(self.static)
+        snap.restore()  # the warm-up updates are undone: the first replay is the first update
+        self.opt.current_step = step0
+        _base.invalidate_packs()
+
     def __call__(self, batch):
         if self.graph is None:
-            self.static = tuple(b.clone() if torch.is_tensor(b) else b for b in batch)
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(self.warmup):
-                    self.opt._update_learning_rate()
-                    self._body(self.static)
-            torch.cuda.current_stream().wait_stream(side)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.out = self._body(self.static)
-        if getattr(self, "done", None) is not None:
-            self.done.synchronize()  # see graph_fence
+            self._capture(batch)
         for s, b in zip(self.static, batch):
             if torch.is_tensor(s):
                 s.copy_(b)
@@ -179,7 +280,7 @@ class GraphedTrainStep:
                 raise ValueError("GraphedTrainStep: non-tensor batch entries are fixed at capture")
         self.opt._update_learning_rate()
         self.graph.replay()
-        self.done = graph_fence()
+        _base.invalidate_packs()  # replays move the parameters without bumping their versions
         return self.out
 
 

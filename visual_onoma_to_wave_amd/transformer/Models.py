@@ -113,6 +113,8 @@ class Decoder(HipModule):
             get_sinusoid_encoding_table(self.max_seq_len + 1, self.d_model).unsqueeze(0),
             requires_grad=False)
         self.layer_stack = _fft_stack(config, "decoder", t["decoder_layer"])
+        for layer in self.layer_stack:  # bench.py's C2 roofline: the decoder FFN's k = 9 conv
+            layer.pos_ffn.timer_tag = "dec_ffn_w1"
 
     def run(self, x, mask, lens):
         """x (B, T, D) compute dtype (consumed in place for the PE add) -> (out, mask)."""

@@ -48,13 +48,16 @@ class MultiHeadAttention(HipModule):
         )
 
     def run(self, x, lens, mask_rows=False):
-        """x (B, L, D) in the compute dtype; lens (B,) int32 -> LN(fc(attn) + x) (pad rows
-        zeroed when mask_rows, as FFTBlock.masked_fill does)."""
+        """x (B, L, D) residual stream (the compute dtype, or fp32 under bf16 compute: the
+        decoder of the "mixed" precision keeps its residual stream and LayerNorm outputs in fp32,
+        as bf16 autocast of the reference does); lens (B,) int32 -> LN(fc(attn) + x) (pad rows
+        zeroed when mask_rows, as FFTBlock.masked_fill does), in x's dtype."""
         p = self._packed(x.device, self._build)
         D = x.shape[-1]
-        qkv = ops.conv1d(x, p["wqkv"], p["bqkv"], Co=3 * D, K=1, compute_dtype=self.compute_dtype)
+        cd = self.compute_dtype
+        qkv = ops.conv1d(x, p["wqkv"], p["bqkv"], Co=3 * D, K=1, compute_dtype=cd, out_dtype=cd)
         att, _ = self.attention(qkv, lens, self.n_head)
-        y = ops.conv1d(att, p["wfc"], p["bfc"], Co=D, K=1, compute_dtype=self.compute_dtype)
+        y = ops.conv1d(att, p["wfc"], p["bfc"], Co=D, K=1, compute_dtype=cd, out_dtype=x.dtype)
         return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens if mask_rows else None)
 
     def forward(self, q, k, v, mask=None):
@@ -89,14 +92,17 @@ class PositionwiseFeedForward(HipModule):
         )
 
     def run(self, x, lens=None):
-        """LN(w_2(relu(w_1(x))) + x), pad rows zeroed when lens is given."""
+        """LN(w_2(relu(w_1(x))) + x) in x's dtype (the residual stream, see
+        MultiHeadAttention.run), pad rows zeroed when lens is given."""
         p = self._packed(x.device, self._build)
         k1, k2 = self.kernel_size
         d_hid = self.w_1.out_channels
+        cd = self.compute_dtype
         h = ops.conv1d(x, p["w1"], p["b1"], Co=d_hid, K=k1, pad=(k1 - 1) // 2,
-                       post_act=ops.ACT_RELU, compute_dtype=self.compute_dtype)
+                       post_act=ops.ACT_RELU, compute_dtype=cd, out_dtype=cd,
+                       tag=getattr(self, "timer_tag", None))
         y = ops.conv1d(h, p["w2"], p["b2"], Co=x.shape[-1], K=k2, pad=(k2 - 1) // 2,
-                       compute_dtype=self.compute_dtype)
+                       compute_dtype=cd, out_dtype=x.dtype)
         return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens)
 
     def forward(self, x):

@@ -60,11 +60,10 @@ def get_vocoder(config, device, checkpoint=None):
     vocoder = hifigan.Generator(hifigan.AttrDict(_hifigan_config()))
     path = checkpoint or {"LJSpeech": "scripts/hifigan/generator_LJSpeech.pth.tar",
                           "universal": "scripts/hifigan/generator_universal.pth.tar"}[speaker]
-    if path is not None and os.path.exists(path):
-        ckpt = torch.load(path, map_location="cpu", weights_only=True)
-        vocoder.load_state_dict(ckpt["generator"])
-    elif checkpoint is not None:
-        raise FileNotFoundError(path)
+    # a missing checkpoint raises, as torch.load does in the reference (utils/model.py:64-67):
+    # never synthesise with random weights
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    vocoder.load_state_dict(ckpt["generator"])
     vocoder.eval()
     vocoder.remove_weight_norm()
     return vocoder.to(device)
