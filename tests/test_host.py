@@ -140,3 +140,14 @@ def test_synthetic_glyphs_shape_and_ink():
     assert 0.05 < ink < 0.25
     d = synth.durations(np.random.default_rng(1), 4, 12, 512)
     assert (d.sum(1) == 512).all() and (d >= 1).all()
+
+
+def test_vo_tune_rejects_timing_ablations():
+    """Kernel configurations that skip loads for timing ablations give wrong results: the shipped
+    library refuses to select them (only a -DVO_ABLATIONS build dispatches them)."""
+    from visual_onoma_to_wave_amd import _lib
+    L = _lib.lib()
+    for v in (13, 16, 17, 25):
+        assert L.vo_tune(b"pair_cfg", v) != 0
+        assert b"ablation" in L.vo_last_error()
+    assert L.vo_tune(b"pair_cfg", 0) == 0

@@ -9,7 +9,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvonoma.so")
+# VO_LIB_PATH: an alternative build of the same library (A/B timing of two kernel builds in
+# tools/); the product path loads lib/libvonoma.so
+LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "lib", "libvonoma.so")
 
 VO_F32, VO_BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3

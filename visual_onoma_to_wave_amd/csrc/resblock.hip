@@ -34,7 +34,8 @@ struct PairArgs {
 };
 
 // WC x WT waves: wave (wc, wt) owns channels [wc*C/WC, (wc+1)*C/WC) of rows [wt*16*NJ, ..+16*NJ)
-// ABL (timing ablations only, garbage results): 1 = no weight-group loads, 2 = no window /
+// ABL (timing ablations only, garbage results; dispatched only with -DVO_ABLATIONS): 1 = no
+// weight-group loads, 2 = no window /
 // residual loads, 3 = neither; bit 4 = no weight LDS stores
 // PRIO (A/B only; both within run-to-run noise on the C = 128 pair): 1 = s_setprio(1) around
 // each MFMA cluster; 2 = static: the younger half of the waves runs at priority 1 (guide T5)
@@ -310,18 +311,26 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     auto p1_epilogue = [&]() {
       float bz[8 * NH];
       lane_bias(0, bz);
+      // rows outside [0, T) exist only in the first / last tile of an utterance: a uniform test
+      // keeps the zero-padding select out of every other tile (per-element selects compiled to
+      // exec-mask branches around each value)
+      const bool interior = t0 - h2 >= 0 && t0 - h2 + R1 <= T;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int r = wt * 16 * NJ + 16 * j + lr;
         const int pos = t0 - h2 + r;
-        const bool inside = pos >= 0 && pos < T;
+        const float keep = (interior || (pos >= 0 && pos < T)) ? 1.f : 0.f;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
           float f[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
-            f[e] = inside ? fmaxf(z, z * slope) : 0.f;
+            f[e] = fmaxf(z, z * slope);
+          }
+          if (!interior) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] *= keep;
           }
           const int ch = n0 + 8 * h;
           store8(t1 + (ch >> 5) * T1R * 32 + rb_off(r, (ch & 31) >> 3, 2), f);
@@ -497,6 +506,10 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
 
 using namespace vo;
 
+int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                 const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
+                 hipStream_t st, int* handled);  // resblock2.hip
+
 extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                                 void* y, const void* acc, int B, int T, int C, int K, int dil, float slope,
                                 float out_scale, void* stream) {
@@ -518,6 +531,14 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
+  // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
+  // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
+  // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.
+  if ((C == 64 && cfg != 9 && cfg < 20) || cfg == 30 || cfg == 31) {
+    int handled = 0;
+    const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
   if (C == 32) {
     if (cfg == 3) return pair_launch<32, 1, 4, 8, true, 1>(a, B, st);
     if (cfg == 4) return pair_launch<32, 1, 8, 8, true, 1, 0, 0, false, false, true, false, true>(a, B, st);
@@ -536,7 +557,12 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // pair_cfg 1 = the register-staged 128-row kernel, 13 = its no-global-load timing ablation.
     // In the bench step: s1 0.62 -> 0.545 ms per launch (tools/bench_ab.sh).
     if (cfg == 1) return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
+#ifdef VO_ABLATIONS  // timing ablations (garbage results): never in the shipped dispatch
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
+    if (cfg == 16) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, true>(a, B, st);
+    if (cfg == 17) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, false, true>(a, B, st);
+    if (cfg == 25) return pair_launch<128, 2, 4, 4, false, 1, 1, 0, false, true, true, false, true>(a, B, st);
+#endif
     if (cfg == 2) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
     if (cfg == 3) return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
     // two 4-wave workgroups per CU (79 KB LDS each: 128-row in-place tiles, half-tap weight
@@ -549,11 +575,12 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
     // SIMD (12 waves, 2 x 6) 15 % slower.
-    // timing ablations (garbage results): no window / residual loads -- 0.67 -> 0.56 ms at
-    // k = 11, 0.30 -> 0.21 at k = 3: the chip-wide burst of window loads after P2 (17 MB at
-    // once); fetching the window during the last P2 group instead was 11-20 % slower
-    if (cfg == 16) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, true>(a, B, st);
-    if (cfg == 17) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, false, true>(a, B, st);
+    // timing ablations (VO_ABLATIONS builds only): no window / residual loads 0.70 -> 0.58 ms at
+    // k = 11, 0.52 -> 0.41 at k = 7 (cfg 17); no weight DMA 0.70 -> 0.63 (cfg 25).  Measured and
+    // dropped in round 2 (tools/ab_pair2.py): the next window staged through registers during P2
+    // with T1 beside the window (192-row tiles: +20 %), the next group's DMA pieces spread between
+    // the tap steps (+2 %), 320 / 384-row tiles (spill), the version-2 kernel (pair_cfg 30: +5 % at
+    // k = 11 -- its in-P2 window loads wait behind the in-order vmcnt of the weight DMA)
     if (cfg == 9) {  // the previous defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);

@@ -226,19 +226,26 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
       if constexpr (RESW) __syncthreads();
       float bz[8 * NH];
       lane_bias(2 * s + ph, bz);
+      // frame rows outside [0, T) exist only in an utterance's first / last tile: a uniform test
+      // keeps the zero-padding selects (compiled to exec-mask branches per value) out of the rest
+      const bool interior = p0 >= 0 && p0 + F <= T;
       if (ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int r = wt * 16 * NJ + 16 * j + lr;
           const int pos = p0 + r;
-          const bool inside = pos >= 0 && pos < T;
+          const float keep = (interior || (pos >= 0 && pos < T)) ? 1.f : 0.f;
 #pragma unroll
           for (int h = 0; h < NH; ++h) {
             float f[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
-              f[e] = inside ? fmaxf(z, z * slope) : 0.f;
+              f[e] = fmaxf(z, z * slope);
+            }
+            if (!interior) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] *= keep;
             }
             const int ch = n0 + 8 * h;
             store8(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2), f);
@@ -258,7 +265,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
         for (int j = 0; j < NJ; ++j) {
           const int r = wt * 16 * NJ + 16 * j + lr;
           const int pos = p0 + r;
-          const bool inside = pos >= 0 && pos < T;
+          const bool inside = interior || (pos >= 0 && pos < T);
 #pragma unroll
           for (int h = 0; h < NH; ++h) {
             float xf[8];
@@ -272,8 +279,12 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
             }
             xres[j][h] = u32x4{w[0], w[1], w[2], w[3]};
             const int ch = n0 + 8 * h;
-            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) =
-                inside ? lrelu8(xres[j][h], slope) : u32x4{0u, 0u, 0u, 0u};
+            u32x4 v = lrelu8(xres[j][h], slope);
+            if (!interior) {
+              const uint32_t km = inside ? 0xffffffffu : 0u;
+              v = u32x4{v.x & km, v.y & km, v.z & km, v.w & km};
+            }
+            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) = v;
           }
         }
       } else {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows

@@ -25,6 +25,8 @@ extern "C" int vo_version(void) { return 1; }
 static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg", "rb3_cfg", "att_cfg", "ups_cfg", "post_cfg", "splitk_cfg"};
 static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {};
 
+static bool is_ablation(const char* key, int value);
+
 static void knobs_from_env() {
   static bool done = false;
   if (done) return;
@@ -38,12 +40,27 @@ static void knobs_from_env() {
     if (!eq) continue;
     *eq = 0;
     for (size_t i = 0; i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
-      if (!strcmp(tok, kKnobs[i])) g_knobs[i] = atoi(eq + 1);
+      if (!strcmp(tok, kKnobs[i]) && !is_ablation(tok, atoi(eq + 1))) g_knobs[i] = atoi(eq + 1);
   }
+}
+
+// pair_cfg values that select timing ablations (kernels that skip loads: garbage results); only
+// a build with -DVO_ABLATIONS dispatches them, and vo_tune rejects them in the shipped library
+static bool is_ablation(const char* key, int value) {
+#ifdef VO_ABLATIONS
+  (void)key; (void)value;
+  return false;
+#else
+  return !strcmp(key, "pair_cfg") && (value == 13 || value == 16 || value == 17 || value == 25);
+#endif
 }
 
 extern "C" int vo_tune(const char* key, int value) {
   knobs_from_env();
+  if (key && is_ablation(key, value)) {
+    vo_set_error("vo_tune: %s=%d is a timing ablation (wrong results); build with -DVO_ABLATIONS", key, value);
+    return VO_ERR_INVALID;
+  }
   for (size_t i = 0; key && i < sizeof(kKnobs) / sizeof(kKnobs[0]); ++i)
     if (!strcmp(key, kKnobs[i])) {
       g_knobs[i] = value;
