@@ -305,6 +305,11 @@ int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
 int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
 int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);
+/* Their adjoints (dL/dwav, fp32, written): g in the forward's output layout and dtype; the period
+ * fold adds the gradient of each right-pad row to the sample it mirrored. */
+int vo_period_fold_bwd(const void* g, int dtype, int B, int T, int P, float* gwav, void* stream);
+int vo_wav_cl8_bwd(const void* g, int dtype, int64_t n, float* gwav, void* stream);
+int vo_avgpool_wav_bwd(const float* g, int B, int T, float* gx, void* stream);
 int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
                   int dtype, float* out, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
@@ -345,6 +350,41 @@ int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out,
  * (hifigan/models.py:96-103,155-163, SubLayers.py:85-93) in the training backward. */
 int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, int64_t rows,
                   int width, float slope, void* out, int ldo, void* stream);
+
+/* ------------------------------------------------------------------ training glue (round 2)
+ * BatchNorm with batch statistics over channels-last x (M rows x C channels, VO_F32 / VO_BF16):
+ * y = (x - mean) rstd * gamma + beta (gamma / beta may both be NULL), mean_rstd[0..C) = mean,
+ * [C..2C) = 1/sqrt(var_biased + eps); running stats (both or neither): r = (1-m) r + m stat with
+ * the unbiased variance, *nbt += 1 (NULL: skipped).  workspace: vo_bn_workspace_size bytes.
+ * Replaces nn.BatchNorm1d/2d in training mode -- PostNet (scripts/transformer/Layers.py:129-137)
+ * and the glyph encoder's single-channel BatchNorm2d (C = 1; scripts/model/
+ * visual_feature_extractor.py:40-47).  vo_bn_bwd: dgamma = sum dy xhat, dbeta = sum dy,
+ * dx = gamma rstd (dy - dbeta / M - xhat dgamma / M) (dx in x's dtype).  Deterministic. */
+int64_t vo_bn_workspace_size(int M, int C);
+int vo_bn_train_fwd(const void* x, int dtype, int M, int C, const float* gamma, const float* beta, float eps,
+                    float momentum, float* run_mean, float* run_var, int64_t* nbt, float* mean_rstd,
+                    float* workspace, void* y, void* stream);
+int vo_bn_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, int M, int C, const float* gamma,
+              const float* mean_rstd, float* workspace, float* dgamma, float* dbeta, void* dx, void* stream);
+
+/* Glyph-encoder Conv2d(1, 1, 3, padding=1) on N single-channel H x W maps (fp32), w[0..9) the
+ * row-major kernel, w[9] the bias (scripts/model/visual_feature_extractor.py:40-47,60-72):
+ * forward, and the backward -> dx and dw[10] (weight + bias gradient; per-block partials summed in
+ * a fixed order, workspace: vo_vfe_conv_workspace_size bytes). */
+int64_t vo_vfe_conv_workspace_size(int N, int H, int W);
+int vo_vfe_conv_fwd(const float* x, int N, int H, int W, const float* w, float* y, void* stream);
+int vo_vfe_conv_bwd(const float* x, const float* dy, int N, int H, int W, const float* w, float* dx, float* dw,
+                    float* workspace, void* stream);
+
+/* Backward of vo_stft_mel_ex (clip off; the HiFi-GAN V1 training mel-loss front end):
+ * gmel (B, n_mels, F) = dL/dlogmel -> dwav (B, N) fp32 (written, not accumulated).  Per frame the
+ * spectrum is recomputed; the frame gradients (workspace: vo_stft_mel_bwd_workspace_size bytes)
+ * are gathered per sample over the overlapping frames and the reflect-padding mirrors in a
+ * fixed order.  n_mels <= 256. */
+int64_t vo_stft_mel_bwd_workspace_size(int B, int N, int n_fft, int hop, int pad);
+int vo_stft_mel_bwd(const float* wav, int B, int N, const float* window, const float* fb, int n_fft, int hop,
+                    int n_mels, int pad, float mag_eps, float log_floor, const float* gmel, float* dwav,
+                    float* workspace, void* stream);
 
 /* ------------------------------------------------------------------ training input pipeline
  * Glyph batch: B grayscale strips packed in px (strip b at img_off[b],

@@ -122,10 +122,25 @@ _SIGNATURES = {
     "vo_period_fold": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "vo_wav_cl8": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "vo_avgpool_wav": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "vo_period_fold_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "vo_wav_cl8_bwd": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
+    "vo_avgpool_wav_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "vo_gan_reduce": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
                               c_void_p]),
     "vo_gan_reduce_grad": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
                                    c_void_p, c_int, c_void_p]),
+    "vo_bn_workspace_size": (ctypes.c_int64, [c_int, c_int]),
+    "vo_bn_train_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_bn_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_void_p, c_void_p]),
+    "vo_vfe_conv_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),
+    "vo_vfe_conv_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_vfe_conv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p]),
+    "vo_stft_mel_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "vo_stft_mel_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_glyph_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                c_int, c_int, c_void_p, c_void_p]),
 }

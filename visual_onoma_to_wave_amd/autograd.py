@@ -11,7 +11,9 @@ The forward of every op is the same HIP kernel the inference path runs.  Backwar
 * attention backward: HIP -- ``vo_attention_bwd`` (flash-style: the row log-sum-exp is rebuilt
   from q / k, dQ and dK / dV in two MFMA kernels, nothing of size L x L stored);
 * LengthRegulator backward: HIP -- ``vo_length_regulate_bwd`` (segmented frame sums per token,
-  deterministic).
+  deterministic);
+* training-mode BatchNorm (PostNet, glyph encoder) forward / backward and the glyph encoder's
+  3 x 3 conv forward / backward: HIP -- ``vo_bn_*`` and ``vo_vfe_conv_*`` (train_glue.hip).
 
 All functions take and return channels-last (B, T, C) activations.
 """
@@ -135,32 +137,68 @@ class LengthRegulateFn(torch.autograd.Function):
         return ops.length_regulate_bwd(go.contiguous(), dur, ctx.shape[1], out_dtype=ctx.xdtype), None, None, None
 
 
+class BatchNormTrainFn(torch.autograd.Function):
+    """nn.BatchNorm* in training mode on HIP (``vo_bn_train_fwd`` / ``vo_bn_bwd``): batch
+    statistics per channel, the running-stat update (momentum, unbiased running variance,
+    ``num_batches_tracked`` += 1) done by the finalize kernel on the device -- nothing on the
+    host, so the step stays graph-capturable."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, bn):
+        xc = x.contiguous()
+        track = bn.track_running_stats and bn.running_mean is not None
+        y, mr = ops.bn_train_fwd(xc, weight, bias, bn.eps, bn.momentum,
+                                 bn.running_mean if track else None, bn.running_var if track else None,
+                                 bn.num_batches_tracked if track else None)
+        ctx.save_for_backward(xc, weight, mr)
+        ctx.has_affine = weight is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, mr = ctx.saved_tensors
+        dx, dg, db = ops.bn_bwd(x, gy.contiguous(), w, mr)
+        if not ctx.has_affine:
+            dg = db = None
+        return dx, dg, db, None
+
+
 def batch_norm_train(x, bn, dims):
-    """Training-mode BatchNorm (batch statistics over ``dims``; the channel is the one dim left)
-    with the running-stat update of ``nn.BatchNorm*`` (momentum, unbiased running variance,
-    ``num_batches_tracked``).  Reductions and elementwise ops of PyTorch-ROCm on the tensor as it
-    lies -- channels-last PostNet activations need no transpose, and the single-channel VFE
-    maps reduce over all blocks (MIOpen's spatial kernels took ~200 us a call on both)."""
-    n = 1
-    for d in dims:
-        n *= x.shape[d]
-    mean = x.mean(dims, keepdim=True)
-    xc = x - mean
-    var = (xc * xc).mean(dims, keepdim=True)
-    if bn.track_running_stats and bn.running_mean is not None:
-        with torch.no_grad():
-            bn.num_batches_tracked.add_(1)
-            m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
-            bn.running_mean.mul_(1.0 - m).add_(mean.detach().flatten().to(bn.running_mean.dtype), alpha=m)
-            bn.running_var.mul_(1.0 - m).add_(var.detach().flatten().to(bn.running_var.dtype),
-                                              alpha=m * n / max(n - 1, 1))
-    shape = [1] * x.dim()
-    ch = [d for d in range(x.dim()) if d not in dims and d - x.dim() not in dims]
-    shape[ch[0]] = x.shape[ch[0]]
-    y = xc * torch.rsqrt(var + bn.eps)
+    """Training-mode BatchNorm over ``dims`` (batch statistics; the channel is the one dim left):
+    channels-last (B, T, C) with dims (0, 1) -- PostNet, no transposes -- or a single-channel
+    (N, 1, H, W) map with dims (0, 2, 3) -- the glyph encoder."""
+    if bn.momentum is None:
+        raise NotImplementedError("batch_norm_train: cumulative-average BatchNorm (momentum=None)")
+    if not ((x.dim() == 3 and tuple(dims) == (0, 1)) or (x.dim() == 4 and tuple(dims) == (0, 2, 3) and
+                                                           x.shape[1] == 1)):
+        raise NotImplementedError(f"batch_norm_train: layout {tuple(x.shape)} over dims {dims}")
     if bn.affine:
-        y = y * bn.weight.view(shape) + bn.bias.view(shape)
-    return y.to(x.dtype)  # stay in the activation dtype (fp32 affine params would promote bf16)
+        return BatchNormTrainFn.apply(x, bn.weight, bn.bias, bn)
+    return BatchNormTrainFn.apply(x, None, None, bn)
+
+
+class VfeConvFn(torch.autograd.Function):
+    """The glyph encoder's Conv2d(1, 1, 3, padding=1) (``vo_vfe_conv_fwd`` / ``vo_vfe_conv_bwd``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        w10 = torch.cat([weight.detach().reshape(-1).float(), bias.detach().reshape(-1).float()])
+        xc = x.contiguous()
+        ctx.save_for_backward(xc, w10)
+        ctx.wshape = weight.shape
+        return ops.vfe_conv_fwd(xc, w10)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w10 = ctx.saved_tensors
+        dx, dw = ops.vfe_conv_bwd(x, gy.contiguous(), w10)
+        return dx, dw[:9].view(ctx.wshape), dw[9:]
+
+
+def vfe_conv(x, conv):
+    if conv.weight.shape != (1, 1, 3, 3) or conv.bias is None or conv.padding != (1, 1) or conv.stride != (1, 1):
+        raise NotImplementedError("vfe_conv: the HIP path covers Conv2d(1, 1, 3, padding=1) with bias")
+    return VfeConvFn.apply(x, conv.weight, conv.bias)
 
 
 def length_regulate(x, dur, max_len, out_dtype=None):

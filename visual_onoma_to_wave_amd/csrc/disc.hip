@@ -146,6 +146,39 @@ __global__ void __launch_bounds__(256) lrelu_mask_kernel(const TG* __restrict__ 
   }
 }
 
+// adjoints of the three input transforms above (dL/dwav, fp32):
+//  period fold: sample t gets row t / P of column t % P, plus the right-pad row that mirrored it
+template <typename TG>
+__global__ void __launch_bounds__(256) period_fold_bwd_kernel(const TG* __restrict__ g, int T, int P, int H,
+                                                              float* __restrict__ gw) {
+  const int b = blockIdx.y;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
+    float s = to_f32(g[(((int64_t)b * P + t % P) * H + t / P) * 8]);
+    const int tm = 2 * (T - 1) - t;  // the padded position that copied sample t, if it exists
+    if (tm >= T && tm < H * P) s += to_f32(g[(((int64_t)b * P + tm % P) * H + tm / P) * 8]);
+    gw[(int64_t)b * T + t] = s;
+  }
+}
+
+template <typename TG>
+__global__ void __launch_bounds__(256) wav_cl8_bwd_kernel(const TG* __restrict__ g, int64_t n, float* __restrict__ gw) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) gw[i] = to_f32(g[i * 8]);
+}
+
+//  average pool: x[t] feeds outputs o with 2o - 2 <= t <= 2o + 1, each with weight 1/4
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restrict__ g, int T, int T_out,
+                                                          float* __restrict__ gx) {
+  const int b = blockIdx.y;
+  const float* gb = g + (int64_t)b * T_out;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < T; t += gridDim.x * 256) {
+    const int o0 = t / 2;  // outputs o0 (taps 2, 3) and o0 + 1 (taps 0, 1)
+    float s = 0.f;
+    if (o0 < T_out) s += gb[o0];
+    if (o0 + 1 < T_out) s += gb[o0 + 1];
+    gx[(int64_t)b * T + t] = 0.25f * s;
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -247,5 +280,35 @@ extern "C" int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* re
     return VO_ERR_INVALID;
   }
 #undef VO_LM
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_period_fold_bwd(const void* g, int dtype, int B, int T, int P, float* gwav, void* stream) {
+  VO_CHECK_ARG(g && gwav && B > 0 && P >= 1 && T > P, "period_fold_bwd: bad arguments");
+  const int H = (T + P - 1) / P;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(period_fold_bwd_kernel<bf16_t>, dim3(grid_for(T), B), dim3(256), 0, st, (const bf16_t*)g, T, P,
+                       H, gwav);
+  else
+    hipLaunchKernelGGL(period_fold_bwd_kernel<float>, dim3(grid_for(T), B), dim3(256), 0, st, (const float*)g, T, P, H,
+                       gwav);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_wav_cl8_bwd(const void* g, int dtype, int64_t n, float* gwav, void* stream) {
+  VO_CHECK_ARG(g && gwav && n > 0, "wav_cl8_bwd: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(wav_cl8_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16_t*)g, n, gwav);
+  else
+    hipLaunchKernelGGL(wav_cl8_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)g, n, gwav);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_avgpool_wav_bwd(const float* g, int B, int T, float* gx, void* stream) {
+  VO_CHECK_ARG(g && gx && B > 0 && T > 0, "avgpool_wav_bwd: bad arguments");
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(T), B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g,
+                     T, T / 2 + 1, gx);
   VO_RETURN_LAUNCH();
 }

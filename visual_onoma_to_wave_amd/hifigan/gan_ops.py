@@ -14,9 +14,13 @@ Backward, per op:
     ``vo_conv1d_wgrad[_grouped]`` (MFMA over transposed LDS reads) and ``vo_colsum``;
   * input gradient of strided / grouped discriminator convs: the conv kernel once per stride
     phase (taps of the phase reversed, channel roles swapped, rows interleaved) -- ``_dgrad``;
-  * the mel-loss STFT backward: PyTorch-ROCm (``torch.stft``), and MIOpen
-    ``convolution_backward`` only for layouts none of the above covers (none in HiFi-GAN V1)
-    -- the fallback SURVEY.md 8(b) sanctions.
+  * the mel-loss STFT backward: ``vo_stft_mel_bwd`` (per frame: the spectrum recomputed, the
+    mel / log chain rule, an inverse FFT in LDS; then a deterministic gather over frames and
+    reflect mirrors);
+  * the discriminator input transforms (period fold, channels-last copy, average pool):
+    ``vo_period_fold_bwd`` / ``vo_wav_cl8_bwd`` / ``vo_avgpool_wav_bwd``;
+  * MIOpen ``convolution_backward`` only for layouts none of the above covers (none in
+    HiFi-GAN V1) -- the fallback SURVEY.md 8(b) sanctions.
 """
 
 from dataclasses import dataclass
@@ -311,15 +315,7 @@ class PeriodFoldFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         B, T = ctx.shape
-        p = ctx.period
-        H = g.shape[1]
-        gf = g[..., 0].float().reshape(B, p, H).transpose(1, 2).reshape(B, H * p)  # padded time order
-        gw = gf[:, :T].clone()
-        n_pad = H * p - T
-        if n_pad:  # reflect: padded sample T + i came from T - 2 - i
-            src = torch.arange(T - 2, T - 2 - n_pad, -1, device=g.device)
-            gw.index_add_(1, src, gf[:, T:])
-        return gw, None, None
+        return ops.period_fold_bwd(g.contiguous(), B, T, ctx.period), None, None
 
 
 class WavCl8Fn(torch.autograd.Function):
@@ -329,7 +325,7 @@ class WavCl8Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return g[..., 0].float().contiguous(), None
+        return ops.wav_cl8_bwd(g.contiguous()), None
 
 
 class AvgPoolFn(torch.autograd.Function):
@@ -340,13 +336,7 @@ class AvgPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        # adjoint of AvgPool1d(4, 2, padding 2, count_include_pad): each output spreads g / 4
-        T = ctx.T
-        gx = F.conv_transpose1d(g[:, None, :], g.new_full((1, 1, 4), 0.25), stride=2, padding=2)
-        gx = gx[:, 0, :T]
-        if gx.shape[1] < T:
-            gx = F.pad(gx, (0, T - gx.shape[1]))
-        return gx.contiguous()
+        return ops.avgpool_wav_bwd(g.float().contiguous(), ctx.T)
 
 
 class GanLossFn(torch.autograd.Function):
@@ -393,18 +383,5 @@ class MelFn(torch.autograd.Function):
     def backward(ctx, g):
         wav, window, fb = ctx.saved_tensors
         n_fft, hop = ctx.cfg
-        with torch.enable_grad():
-            w = wav.detach().requires_grad_(True)
-            mel = mel_reference(w, window, fb, n_fft, hop)
-            (gw,) = torch.autograd.grad(mel, w, g)
-        return gw, None, None, None, None
-
-
-def mel_reference(wav, window, fb, n_fft, hop):
-    """torch restatement used only for MelFn's backward (recomputation)."""
-    p = (n_fft - hop) // 2
-    y = F.pad(wav[:, None, :], (p, p), mode="reflect")[:, 0]
-    spec = torch.stft(y, n_fft, hop_length=hop, win_length=n_fft, window=window, center=False,
-                      return_complex=True)
-    mag = torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-9)
-    return torch.log(torch.clamp(torch.matmul(fb.t(), mag), min=1e-5))
+        return (ops.stft_mel_bwd(wav.contiguous(), window, fb, g.float().contiguous(), n_fft=n_fft, hop=hop,
+                                 pad=(n_fft - hop) // 2, mag_eps=1e-9), None, None, None, None)

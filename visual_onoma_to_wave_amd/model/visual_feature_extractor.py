@@ -89,19 +89,21 @@ class VisualFeatureExtractor(HipModule):
 
     def train_run(self, images, out_dtype):
         """Training forward (BatchNorm2d uses batch statistics, so the eval-folded stencil kernel
-        does not apply): slices as a strided view, embedder via PyTorch-ROCm, bridge on HIP."""
+        does not apply): the slices gathered into (B n, 1, 24, 102) maps, then conv (vo_vfe_conv),
+        BatchNorm with batch statistics (vo_bn_train_fwd), ReLU, and the bridge on HIP."""
         from .. import autograd as AG
         B, C, H, W = images.shape
         n = int((W - (self.stride // 2) * self.slice_width * 2) / self.slice_width)
         sl = images[..., : n * self.slice_width].reshape(B, C, H, n, self.slice_width)
         x = sl.permute(0, 3, 1, 2, 4).reshape(B * n, C, H, self.slice_width)
-        for m in self.embedder:  # BatchNorm2d with batch statistics off MIOpen (1 channel)
+        self._supported()
+        for m in self.embedder:
             if isinstance(m, nn.BatchNorm2d):
                 x = AG.batch_norm_train(x, m, (0, 2, 3))
             elif isinstance(m, nn.ReLU):
                 x = torch.relu(x)
             else:
-                x = m(x)
+                x = AG.vfe_conv(x, m)
         y = AG.linear(x.reshape(1, B * n, -1).to(out_dtype), self.bridge[0].weight, self.bridge[0].bias,
                       relu=True, compute_dtype=out_dtype)
         return y.view(B, n, self.embed_dim)

@@ -472,6 +472,101 @@ def stft_mel_ex(wav, window, fb, n_fft=1024, hop=256, n_mels=80, pad=None, mag_e
     return mel
 
 
+def stft_mel_bwd(wav, window, fb, gmel, n_fft=1024, hop=256, pad=None, mag_eps=1e-9, log_floor=1e-5):
+    """Backward of ``stft_mel_ex`` (clip off): gmel (B, n_mels, F) = dL/dlogmel -> dL/dwav (B, N) fp32."""
+    _contig(wav, "wav")
+    _contig(gmel, "gmel")
+    B, N = wav.shape
+    n_mels = fb.shape[1]
+    pad = n_fft // 2 if pad is None else pad
+    F = 1 + (N + 2 * pad - n_fft) // hop
+    if gmel.shape != (B, n_mels, F) or gmel.dtype != torch.float32 or wav.dtype != torch.float32:
+        raise ValueError(f"stft_mel_bwd: gmel {tuple(gmel.shape)} {gmel.dtype} vs ({B}, {n_mels}, {F}) fp32")
+    L = _lib.lib()
+    dwav = torch.empty_like(wav)
+    ws = torch.empty(int(L.vo_stft_mel_bwd_workspace_size(B, N, n_fft, hop, pad)) // 4, dtype=torch.float32,
+                     device=wav.device)
+    _lib.check(L.vo_stft_mel_bwd(_ptr(wav), B, N, _ptr(window), _ptr(fb), n_fft, hop, n_mels, pad, float(mag_eps),
+                                 float(log_floor), _ptr(gmel), _ptr(dwav), _ptr(ws), _stream(wav)), "vo_stft_mel_bwd")
+    return dwav
+
+
+# ----------------------------------------------------------------------------- training BatchNorm / glyph conv
+
+def _rows(x):
+    """Channels-last view as (M, C); a single-channel map (N, 1, H, W) is M = every pixel, C = 1."""
+    _contig(x, "x")
+    C = x.shape[-1] if x.dim() != 4 else x.shape[1]
+    if x.dim() == 4 and C != 1:
+        raise ValueError("bn: 4-d input must be single-channel (N, 1, H, W)")
+    return x.numel() // C, C
+
+
+def bn_train_fwd(x, gamma, beta, eps, momentum, running_mean=None, running_var=None, num_batches=None):
+    """BatchNorm with batch statistics over channels-last x (..., C) or (N, 1, H, W) in fp32 / bf16:
+    (y in x's dtype, mean_rstd (2C) fp32); running stats / num_batches updated in place when given."""
+    M, C = _rows(x)
+    L = _lib.lib()
+    y = torch.empty_like(x)
+    mr = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_bn_workspace_size(M, C)) // 4, dtype=torch.float32, device=x.device)
+    for t, n in ((gamma, "gamma"), (beta, "beta"), (running_mean, "running_mean"), (running_var, "running_var")):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != C or not t.is_contiguous()):
+            raise ValueError(f"bn_train_fwd: {n} must be contiguous fp32 of {C}")
+    if num_batches is not None and num_batches.dtype != torch.int64:
+        raise ValueError("bn_train_fwd: num_batches must be int64")
+    _lib.check(L.vo_bn_train_fwd(_ptr(x), vo_dtype(x), M, C, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+                                 _ptr(running_mean), _ptr(running_var), _ptr(num_batches), _ptr(mr), _ptr(ws), _ptr(y),
+                                 _stream(x)), "vo_bn_train_fwd")
+    return y, mr
+
+
+def bn_bwd(x, gy, gamma, mean_rstd):
+    """Backward of ``bn_train_fwd``: (dx in x's dtype, dgamma, dbeta) fp32."""
+    M, C = _rows(x)
+    _contig(gy, "gy")
+    if gy.shape != x.shape:
+        raise ValueError("bn_bwd: gy shape mismatch")
+    L = _lib.lib()
+    dx = torch.empty_like(x)
+    dg = torch.empty(C, dtype=torch.float32, device=x.device)
+    db = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_bn_workspace_size(M, C)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_bn_bwd(_ptr(x), vo_dtype(x), _ptr(gy), vo_dtype(gy), M, C, _ptr(gamma), _ptr(mean_rstd), _ptr(ws),
+                           _ptr(dg), _ptr(db), _ptr(dx), _stream(x)), "vo_bn_bwd")
+    return dx, dg, db
+
+
+def _vfe_shape(x):
+    _contig(x, "x")
+    if x.dim() != 4 or x.shape[1] != 1 or x.dtype != torch.float32:
+        raise ValueError(f"vfe conv: x must be (N, 1, H, W) fp32, got {tuple(x.shape)} {x.dtype}")
+    return x.shape[0], x.shape[2], x.shape[3]
+
+
+def vfe_conv_fwd(x, w10):
+    """Conv2d(1, 1, 3, padding=1): x (N, 1, H, W) fp32, w10 = 9 kernel taps (row-major) + bias."""
+    N, H, W = _vfe_shape(x)
+    y = torch.empty_like(x)
+    _lib.check(_lib.lib().vo_vfe_conv_fwd(_ptr(x), N, H, W, _ptr(w10), _ptr(y), _stream(x)), "vo_vfe_conv_fwd")
+    return y
+
+
+def vfe_conv_bwd(x, gy, w10):
+    """Backward of ``vfe_conv_fwd``: (dx, dw10)."""
+    N, H, W = _vfe_shape(x)
+    _contig(gy, "gy")
+    if gy.shape != x.shape or gy.dtype != torch.float32:
+        raise ValueError("vfe_conv_bwd: gy must match x")
+    L = _lib.lib()
+    dx = torch.empty_like(x)
+    dw = torch.empty(10, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_vfe_conv_workspace_size(N, H, W)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_vfe_conv_bwd(_ptr(x), _ptr(gy), N, H, W, _ptr(w10), _ptr(dx), _ptr(dw), _ptr(ws), _stream(x)),
+               "vo_vfe_conv_bwd")
+    return dx, dw
+
+
 # ----------------------------------------------------------------------------- HiFi-GAN training (C5)
 
 def pack_grouped_weight(w, dtype, groups=1, ci_pad=None):
@@ -513,6 +608,39 @@ def avgpool_wav(wav):
     out = torch.empty((B, T // 2 + 1), dtype=torch.float32, device=wav.device)
     _lib.check(_lib.lib().vo_avgpool_wav(_ptr(wav), B, T, _ptr(out), _stream(wav)), "vo_avgpool_wav")
     return out
+
+
+def period_fold_bwd(g, B, T, period):
+    """Adjoint of ``period_fold``: g (B * period, H, 8) -> dL/dwav (B, T) fp32."""
+    _contig(g, "g")
+    H = (T + period - 1) // period
+    if g.shape != (B * period, H, 8):
+        raise ValueError(f"period_fold_bwd: g {tuple(g.shape)} vs ({B * period}, {H}, 8)")
+    gw = torch.empty((B, T), dtype=torch.float32, device=g.device)
+    _lib.check(_lib.lib().vo_period_fold_bwd(_ptr(g), vo_dtype(g), B, T, period, _ptr(gw), _stream(g)),
+               "vo_period_fold_bwd")
+    return gw
+
+
+def wav_cl8_bwd(g):
+    """Adjoint of ``wav_cl8``: g (B, T, 8) -> (B, T) fp32 (channel 0)."""
+    _contig(g, "g")
+    if g.shape[-1] != 8:
+        raise ValueError("wav_cl8_bwd: g must end in 8 channels")
+    gw = torch.empty(g.shape[:-1], dtype=torch.float32, device=g.device)
+    _lib.check(_lib.lib().vo_wav_cl8_bwd(_ptr(g), vo_dtype(g), gw.numel(), _ptr(gw), _stream(g)), "vo_wav_cl8_bwd")
+    return gw
+
+
+def avgpool_wav_bwd(g, T):
+    """Adjoint of ``avgpool_wav``: g (B, T // 2 + 1) fp32 -> (B, T) fp32."""
+    _contig(g, "g")
+    B = g.shape[0]
+    if g.shape[1] != T // 2 + 1 or g.dtype != torch.float32:
+        raise ValueError("avgpool_wav_bwd: g must be (B, T // 2 + 1) fp32")
+    gx = torch.empty((B, T), dtype=torch.float32, device=g.device)
+    _lib.check(_lib.lib().vo_avgpool_wav_bwd(_ptr(g), B, T, _ptr(gx), _stream(g)), "vo_avgpool_wav_bwd")
+    return gx
 
 
 GAN_L1, GAN_ONE_MINUS_SQ, GAN_SQ = 0, 1, 2
