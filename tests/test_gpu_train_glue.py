@@ -1,0 +1,176 @@
+"""The round-2 training glue on HIP (train_glue.hip, disc.hip adjoints): forward and gradients
+against torch autograd of the reference formulation in fp64 on the CPU.
+
+* BatchNorm with batch statistics: PostNet's BatchNorm1d (scripts/transformer/Layers.py:129-137)
+  on channels-last (B, T, C) and the glyph encoder's single-channel BatchNorm2d
+  (scripts/model/visual_feature_extractor.py:40-47); running statistics and
+  ``num_batches_tracked`` as nn.BatchNorm* updates them;
+* the glyph encoder's Conv2d(1, 1, 3, padding=1): dx, dW, db;
+* the HiFi-GAN training mel (oracle.gan.mel_spectrogram, the meldataset recipe) backward;
+* the discriminator input transforms: MPD period fold (reflect pad), channels-last copy, MSD
+  AvgPool1d(4, 2, padding=2).
+
+Tolerances (relative L2): fp32 kernels 1e-5 (BatchNorm, conv: short fp32 sums), 1e-4 for the
+mel backward (1024-point fp32 FFTs and a 1 / melsum factor), bf16 activations 1e-2; the
+transform adjoints exact up to one fp32 rounding (<= 1e-6).
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _bn_case(shape, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(shape, generator=g, dtype=torch.float64) * 1.7 + 0.4
+    gy = torch.randn(shape, generator=g, dtype=torch.float64)
+    C = shape[-1] if len(shape) == 3 else 1
+    bn = torch.nn.BatchNorm1d(C) if len(shape) == 3 else torch.nn.BatchNorm2d(1)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.2, 0.2, generator=g)
+        bn.running_mean.uniform_(-0.1, 0.1, generator=g)
+        bn.running_var.uniform_(0.8, 1.2, generator=g)
+    return x, gy, bn
+
+
+@pytest.mark.parametrize("shape,dtype", [((4, 300, 512), torch.float32), ((3, 77, 80), torch.float32),
+                                         ((8, 512, 512), torch.bfloat16), ((384, 1, 24, 102), torch.float32),
+                                         ((5, 1, 24, 7), torch.float32)])
+def test_batch_norm_train_fwd_bwd(shape, dtype):
+    """y, running mean / var, num_batches_tracked, dx, dgamma, dbeta vs nn.BatchNorm in train mode."""
+    from visual_onoma_to_wave_amd import autograd as AG
+    x, gy, bn = _bn_case(shape, dtype, sum(shape))
+    ref_bn = torch.nn.BatchNorm1d(bn.num_features).double() if len(shape) == 3 else torch.nn.BatchNorm2d(1).double()
+    ref_bn.load_state_dict(bn.state_dict())
+    ref_bn.train()
+    # the reference runs (B, C, T); ours is channels-last (B, T, C)
+    xr = x.to(dtype).double().requires_grad_(True)
+    yr = ref_bn(xr.transpose(1, 2) if len(shape) == 3 else xr)
+    yr = yr.transpose(1, 2) if len(shape) == 3 else yr
+    (yr * gy).sum().backward()
+
+    bn = bn.cuda().train()
+    xg = x.to(dtype).cuda().requires_grad_(True)
+    dims = (0, 1) if len(shape) == 3 else (0, 2, 3)
+    y = AG.batch_norm_train(xg, bn, dims)
+    assert y.dtype == dtype and y.shape == x.shape
+    y.backward(gy.to(dtype).cuda())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    errs = {"y": rel_l2(y.detach().float().cpu(), yr.detach()), "dx": rel_l2(xg.grad.float().cpu(), xr.grad),
+            "dgamma": rel_l2(bn.weight.grad.cpu(), ref_bn.weight.grad),
+            "dbeta": rel_l2(bn.bias.grad.cpu(), ref_bn.bias.grad),
+            "running_mean": rel_l2(bn.running_mean.cpu(), ref_bn.running_mean),
+            "running_var": rel_l2(bn.running_var.cpu(), ref_bn.running_var)}
+    print(shape, dtype, {k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < (1e-5 if k.startswith("running") else tol) for k, v in errs.items()), errs
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
+
+
+def test_batch_norm_train_no_affine_no_tracking():
+    from visual_onoma_to_wave_amd import autograd as AG
+    bn = torch.nn.BatchNorm1d(64, affine=False, track_running_stats=False).cuda()
+    x = torch.randn(2, 50, 64, device="cuda", requires_grad=True)
+    y = AG.batch_norm_train(x, bn, (0, 1))
+    xr = x.detach().cpu().double().requires_grad_(True)
+    yr = F.batch_norm(xr.transpose(1, 2), None, None, training=True).transpose(1, 2)
+    g = torch.randn_like(yr)
+    y.backward(g.float().cuda())
+    (yr * g).sum().backward()
+    assert rel_l2(y.detach().cpu(), yr.detach()) < 1e-5 and rel_l2(x.grad.cpu(), xr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W", [(384, 24, 102), (3, 5, 4), (1, 1, 1)])
+def test_vfe_conv_fwd_bwd(N, H, W):
+    from visual_onoma_to_wave_amd import autograd as AG
+    g = torch.Generator().manual_seed(N * H + W)
+    conv = torch.nn.Conv2d(1, 1, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.uniform_(-0.5, 0.5, generator=g)
+        conv.bias.uniform_(-0.1, 0.1, generator=g)
+    x = torch.rand(N, 1, H, W, generator=g, dtype=torch.float64)
+    gy = torch.randn(N, 1, H, W, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    br = conv.bias.detach().double().requires_grad_(True)
+    yr = F.conv2d(xr, wr, br, padding=1)
+    (yr * gy).sum().backward()
+    conv = conv.cuda()
+    xg = x.float().cuda().requires_grad_(True)
+    y = AG.vfe_conv(xg, conv)
+    y.backward(gy.float().cuda())
+    errs = {"y": rel_l2(y.detach().cpu(), yr.detach()), "dx": rel_l2(xg.grad.cpu(), xr.grad),
+            "dw": rel_l2(conv.weight.grad.cpu(), wr.grad), "db": rel_l2(conv.bias.grad.cpu(), br.grad)}
+    print((N, H, W), {k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < 1e-5 for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("B,N", [(2, 8192), (3, 4000), (1, 1024)])
+def test_stft_mel_backward_vs_torch_autograd(B, N):
+    """MelFn (forward vo_stft_mel_ex, backward vo_stft_mel_bwd) against autograd through
+    oracle.gan.mel_spectrogram in fp64; N = 4000 is not a multiple of the hop and N = 1024 puts
+    most samples inside the reflect-padded regions."""
+    from oracle.mel import librosa_mel
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MelLoss
+    g = torch.Generator().manual_seed(B * N)
+    wav = (torch.rand(B, N, generator=g, dtype=torch.float64) * 2 - 1) * 0.6
+    wr = wav.clone().requires_grad_(True)
+    # oracle.gan.mel_spectrogram's recipe in double precision
+    basis = torch.from_numpy(librosa_mel(22050, 1024, 80, 0.0, 8000.0)).double()
+    p = (1024 - 256) // 2
+    yy = F.pad(wr[:, None, :], (p, p), mode="reflect")[:, 0]
+    spec = torch.stft(yy, 1024, hop_length=256, win_length=1024, window=torch.hann_window(1024, dtype=torch.float64),
+                      center=False, return_complex=True)
+    mel64 = torch.log(torch.clamp(basis @ torch.sqrt(spec.real ** 2 + spec.imag ** 2 + 1e-9), min=1e-5))
+    gm = torch.randn(mel64.shape, generator=g, dtype=torch.float64)
+    (mel64 * gm).sum().backward()
+    ml = MelLoss(1024, 80, 22050, 256, 1024, 0, 8000.0).cuda()
+    wg = wav.float().cuda().requires_grad_(True)
+    mel = ml.mel(wg)
+    mel.backward(gm.float().cuda())
+    e_fwd = rel_l2(mel.detach().cpu(), mel64.detach())
+    e_bwd = rel_l2(wg.grad.cpu(), wr.grad)
+    print((B, N), f"fwd {e_fwd:.1e} bwd {e_bwd:.1e}")
+    assert e_fwd < 1e-4 and e_bwd < 1e-4
+
+
+@pytest.mark.parametrize("T", [8192, 8191, 8190, 100])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_disc_input_adjoints(T, dtype):
+    """Period fold (p = 2, 3, 5, 7, 11: reflect pad to a multiple of p), the channels-last copy and
+    AvgPool1d(4, 2, padding=2): gradients vs autograd of the reference formulation."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as GO
+    g = torch.Generator().manual_seed(T)
+    B = 3
+    wav = torch.randn(B, T, generator=g)
+    for p in (2, 3, 5, 7, 11):
+        wr = wav.clone().double().requires_grad_(True)
+        x = wr
+        if T % p:
+            x = F.pad(x[:, None, :], (0, p - T % p), "reflect")[:, 0]
+        x = x.view(B, -1, p)  # (B, H, p): column c = samples h p + c
+        gy = torch.randn(B * p, x.shape[1], 8, generator=g).to(dtype)
+        gcol = gy[..., 0].double().view(B, p, -1).transpose(1, 2)  # (B, H, p)
+        (x * gcol).sum().backward()
+        wg = wav.cuda().requires_grad_(True)
+        out = GO.PeriodFoldFn.apply(wg, p, dtype)
+        assert out.shape == gy.shape
+        out.backward(gy.cuda())
+        assert rel_l2(wg.grad.cpu(), wr.grad) < 1e-6, p
+    wg = wav.cuda().requires_grad_(True)
+    gy = torch.randn(B, T, 8, generator=g).to(dtype)
+    GO.WavCl8Fn.apply(wg, dtype).backward(gy.cuda())
+    assert torch.equal(wg.grad.cpu(), gy[..., 0].float())
+    wr = wav.clone().double().requires_grad_(True)
+    yr = F.avg_pool1d(wr[:, None, :], 4, 2, padding=2)[:, 0]
+    gp = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    (yr * gp).sum().backward()
+    wg = wav.cuda().requires_grad_(True)
+    y = GO.AvgPoolFn.apply(wg)
+    assert y.shape == yr.shape
+    y.backward(gp.float().cuda())
+    assert rel_l2(wg.grad.cpu(), wr.grad) < 1e-6

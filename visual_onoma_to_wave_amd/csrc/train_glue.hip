@@ -1,0 +1,490 @@
+// Training-step glue that round 1 left on PyTorch-ROCm (config C4 / C5 backward):
+//
+//  * BatchNorm with batch statistics over channels-last rows (x: M rows x C channels), forward
+//    (Welford partials per row block merged in a fixed order -> mean / biased var, the running
+//    statistics update of nn.BatchNorm*, normalize + affine) and backward
+//    (dx = g rstd (dy - mean(dy) - xhat mean(dy xhat)), dgamma = sum dy xhat, dbeta = sum dy):
+//    PostNet's BatchNorm1d on (B, T, C) activations (scripts/transformer/Layers.py:67-137) and the
+//    glyph encoder's single-channel BatchNorm2d (scripts/model/visual_feature_extractor.py:40-47,
+//    C = 1: rows = every pixel);
+//  * the glyph encoder's 1 -> 1 channel 3 x 3 Conv2d (pad 1) forward and backward (input, weight
+//    and bias gradients; the weight / bias sums as per-block partials added in a fixed order);
+//  * the backward of the HiFi-GAN training log-mel (vo_stft_mel_ex with mag_eps): per frame the
+//    forward spectrum is recomputed, dL/d|X| = fb (g / melsum) on the bins whose mel sum passed the
+//    log floor, dX = dL/d|X| X / |X|, the one-sided inverse DFT of dX (a 1024-point complex FFT
+//    in LDS) times the window gives the frame gradient; a second kernel gathers the (<= n_fft / hop)
+//    overlapping frames and the reflect-padded mirror positions of every sample in a fixed order.
+// Everything deterministic (no atomics).
+
+#include <algorithm>
+
+#include "vo_common.h"
+
+namespace vo {
+
+// ------------------------------------------------------------------------------- BatchNorm
+
+struct Welford {
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Welford wf_merge(Welford a, Welford b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  const float fb = b.n / n;
+  return Welford{n, a.mean + d * fb, a.m2 + b.m2 + d * d * a.n * fb};
+}
+
+// block: 256 threads = CT channels x (256 / CT) row lanes; rows [blockIdx.x * RB, +RB)
+template <typename TX, int CT>
+__global__ void __launch_bounds__(256) bn_stats_kernel(const TX* __restrict__ x, int M, int C, int RB,
+                                                       float* __restrict__ part) {
+  constexpr int RS = 256 / CT;
+  __shared__ float sn[256], sm[256], s2[256];
+  const int tid = threadIdx.x;
+  const int cl = tid % CT, rl = tid / CT;
+  const int c = blockIdx.y * CT + cl;
+  const int r0 = blockIdx.x * RB;
+  const int r1 = min(r0 + RB, M);
+  Welford w{0.f, 0.f, 0.f};
+  if (c < C) {
+    for (int r = r0 + rl; r < r1; r += RS) {
+      const float v = to_f32(x[(int64_t)r * C + c]);
+      w.n += 1.f;
+      const float d = v - w.mean;
+      w.mean += d / w.n;
+      w.m2 += d * (v - w.mean);
+    }
+  }
+  sn[tid] = w.n; sm[tid] = w.mean; s2[tid] = w.m2;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int k = 1; k < RS; ++k) w = wf_merge(w, Welford{sn[k * CT + cl], sm[k * CT + cl], s2[k * CT + cl]});
+    float* p = part + ((int64_t)blockIdx.x * C + c) * 3;
+    p[0] = w.n; p[1] = w.mean; p[2] = w.m2;
+  }
+}
+
+// per channel: merge the row-block partials in order; mean / rstd for the normalisation and the
+// backward; running statistics: (1 - m) r + m stat, the variance unbiased (n / (n - 1))
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, float eps, float momentum,
+                                   float* __restrict__ mean_rstd, float* __restrict__ run_mean,
+                                   float* __restrict__ run_var, int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  Welford w{0.f, 0.f, 0.f};
+  for (int b = 0; b < nb; ++b) {
+    const float* p = part + ((int64_t)b * C + c) * 3;
+    w = wf_merge(w, Welford{p[0], p[1], p[2]});
+  }
+  const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
+  mean_rstd[c] = w.mean;
+  mean_rstd[C + c] = rsqrtf(var + eps);
+  if (run_mean) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * w.mean;
+    const float unb = w.n > 1.f ? w.m2 / (w.n - 1.f) : var;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+template <typename TX>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const TX* __restrict__ x, int64_t total, int C,
+                                                       const float* __restrict__ mean_rstd,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       TX* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    float v = (to_f32(x[i]) - mean_rstd[c]) * mean_rstd[C + c];
+    if (gamma) v = v * gamma[c] + beta[c];
+    y[i] = from_f32<TX>(v);
+  }
+}
+
+// backward partial sums per row block: [sum dy, sum dy * xhat] per channel
+template <typename TX, typename TG, int CT>
+__global__ void __launch_bounds__(256) bn_bwd_stats_kernel(const TX* __restrict__ x, const TG* __restrict__ dy,
+                                                           int M, int C, int RB, const float* __restrict__ mean_rstd,
+                                                           float* __restrict__ part) {
+  constexpr int RS = 256 / CT;
+  __shared__ float sa[256], sb[256];
+  const int tid = threadIdx.x;
+  const int cl = tid % CT, rl = tid / CT;
+  const int c = blockIdx.y * CT + cl;
+  const int r0 = blockIdx.x * RB;
+  const int r1 = min(r0 + RB, M);
+  float a = 0.f, bsum = 0.f;
+  if (c < C) {
+    const float mu = mean_rstd[c], rs = mean_rstd[C + c];
+    for (int r = r0 + rl; r < r1; r += RS) {
+      const int64_t i = (int64_t)r * C + c;
+      const float g = to_f32(dy[i]);
+      a += g;
+      bsum += g * (to_f32(x[i]) - mu) * rs;
+    }
+  }
+  sa[tid] = a; sb[tid] = bsum;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int k = 1; k < RS; ++k) {
+      a += sa[k * CT + cl];
+      bsum += sb[k * CT + cl];
+    }
+    float* p = part + ((int64_t)blockIdx.x * C + c) * 2;
+    p[0] = a; p[1] = bsum;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nb; ++k) {
+    a += part[((int64_t)k * C + c) * 2];
+    b += part[((int64_t)k * C + c) * 2 + 1];
+  }
+  dbeta[c] = a;
+  dgamma[c] = b;
+}
+
+template <typename TX, typename TG>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const TX* __restrict__ x, const TG* __restrict__ dy,
+                                                           int64_t total, int C, float inv_m,
+                                                           const float* __restrict__ mean_rstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ dgamma,
+                                                           const float* __restrict__ dbeta, TX* __restrict__ dx) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const float rs = mean_rstd[C + c];
+    const float xh = (to_f32(x[i]) - mean_rstd[c]) * rs;
+    const float g = gamma ? gamma[c] : 1.f;
+    const float v = g * rs * (to_f32(dy[i]) - dbeta[c] * inv_m - xh * dgamma[c] * inv_m);
+    dx[i] = from_f32<TX>(v);
+  }
+}
+
+// ------------------------------------------------------------------------------- 3 x 3 single-channel conv
+
+constexpr int VC_TILE = 256;  // pixels per block (the weight / bias partials: one row per block)
+
+__global__ void __launch_bounds__(VC_TILE) vfe_conv_fwd_kernel(const float* __restrict__ x, int N, int H, int W,
+                                                               const float* __restrict__ w, float* __restrict__ y) {
+  const int64_t total = (int64_t)N * H * W;
+  const int64_t i = (int64_t)blockIdx.x * VC_TILE + threadIdx.x;
+  if (i >= total) return;
+  const int wq = (int)(i % W), hq = (int)((i / W) % H);
+  const int64_t base = i - (int64_t)hq * W - wq;
+  float s = w[9];  // bias
+#pragma unroll
+  for (int di = -1; di <= 1; ++di)
+#pragma unroll
+    for (int dj = -1; dj <= 1; ++dj) {
+      const int h = hq + di, ww = wq + dj;
+      if (h >= 0 && h < H && ww >= 0 && ww < W) s += w[(di + 1) * 3 + (dj + 1)] * x[base + (int64_t)h * W + ww];
+    }
+  y[i] = s;
+}
+
+// dx = correlation of dy with the flipped kernel; per block: the 10 weight / bias partial sums
+__global__ void __launch_bounds__(VC_TILE) vfe_conv_bwd_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ dy, int N, int H, int W,
+                                                               const float* __restrict__ w, float* __restrict__ dx,
+                                                               float* __restrict__ part) {
+  __shared__ float red[10][VC_TILE / 64];
+  const int64_t total = (int64_t)N * H * W;
+  const int64_t i = (int64_t)blockIdx.x * VC_TILE + threadIdx.x;
+  float pw[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) pw[k] = 0.f;
+  if (i < total) {
+    const int wq = (int)(i % W), hq = (int)((i / W) % H);
+    const int64_t base = i - (int64_t)hq * W - wq;
+    float s = 0.f;
+    const float g = dy[i];
+#pragma unroll
+    for (int di = -1; di <= 1; ++di)
+#pragma unroll
+      for (int dj = -1; dj <= 1; ++dj) {
+        const int h = hq + di, ww = wq + dj;
+        if (h >= 0 && h < H && ww >= 0 && ww < W) {
+          // y[h, ww] used x[hq, wq] with kernel tap (-di, -dj): dx += w[1 - di][1 - dj] dy[h, ww]
+          s += w[(1 - di) * 3 + (1 - dj)] * dy[base + (int64_t)h * W + ww];
+          // dW[di + 1][dj + 1] += dy[hq, wq] x[hq + di, wq + dj]
+          pw[(di + 1) * 3 + (dj + 1)] = g * x[base + (int64_t)h * W + ww];
+        }
+      }
+    pw[9] = g;
+    dx[i] = s;
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const float v = wave_sum(pw[k]);
+    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 10) {
+    float v = 0.f;
+    for (int q = 0; q < VC_TILE / 64; ++q) v += red[threadIdx.x][q];
+    part[(int64_t)blockIdx.x * 10 + threadIdx.x] = v;
+  }
+}
+
+__global__ void vfe_conv_wgrad_finalize_kernel(const float* __restrict__ part, int nb, float* __restrict__ dw) {
+  // one wave per weight: lanes stride over blocks in order, a fixed-shape tree inside the wave
+  const int k = blockIdx.x;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 64) s += part[(int64_t)b * 10 + k];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) dw[k] = s;
+}
+
+// ------------------------------------------------------------------------------- STFT log-mel backward
+
+constexpr int SMB_MAX_N = 2048;
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * (n - 1) - i;
+  return i;
+}
+
+// in-place-free radix-2 Stockham FFT of length L (power of two) on buf[src]; sign -1 forward,
+// +1 inverse (unnormalised); returns the buffer holding the result
+__device__ int fft_stockham(float2 (*buf)[SMB_MAX_N], int L, float sign, int tid, int nthreads) {
+  int src = 0;
+  for (int ns = 1; ns < L; ns <<= 1) {
+    for (int j = tid; j < L / 2; j += nthreads) {
+      const int k = j & (ns - 1);
+      const float2 u = buf[src][j];
+      const float2 v = buf[src][j + L / 2];
+      float s, c;
+      sincospif(sign * (float)k / (float)ns, &s, &c);
+      const float2 tv = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+      const int out = (j - k) * 2 + k;
+      buf[src ^ 1][out] = make_float2(u.x + tv.x, u.y + tv.y);
+      buf[src ^ 1][out + ns] = make_float2(u.x - tv.x, u.y - tv.y);
+    }
+    __syncthreads();
+    src ^= 1;
+  }
+  return src;
+}
+
+// one workgroup per (frame, utterance): gframe[b][f][n] = d loss / d x_frame[n] (after the window)
+__global__ void __launch_bounds__(256) stft_mel_bwd_frame_kernel(const float* __restrict__ wav, int N, int F,
+                                                                 const float* __restrict__ window,
+                                                                 const float* __restrict__ fb, int n_fft, int hop,
+                                                                 int n_mels, int pad, float mag_eps, float log_floor,
+                                                                 const float* __restrict__ gmel,
+                                                                 float* __restrict__ gframe) {
+  __shared__ float2 buf[2][SMB_MAX_N];
+  __shared__ float mag[SMB_MAX_N / 2 + 1];
+  __shared__ float xre[SMB_MAX_N / 2 + 1], xim[SMB_MAX_N / 2 + 1];
+  __shared__ float dm[256];  // d loss / d melsum per mel bin (n_mels <= 256)
+  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int n = n_fft, half = n / 2;
+  const float* x = wav + (int64_t)b * N;
+  const int start = f * hop - pad;
+
+  // forward: full n-point complex FFT of the windowed real frame
+  for (int m = tid; m < n; m += 256) buf[0][m] = make_float2(x[reflect_idx(start + m, N)] * window[m], 0.f);
+  __syncthreads();
+  int s = fft_stockham(buf, n, -1.f, tid, 256);
+  for (int k = tid; k <= half; k += 256) {
+    const float2 z = buf[s][k];
+    xre[k] = z.x;
+    xim[k] = z.y;
+    mag[k] = sqrtf(z.x * z.x + z.y * z.y + mag_eps);
+  }
+  __syncthreads();
+  // mel sums and their log-floor derivative
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nf = half + 1;
+  for (int m = wave; m < n_mels; m += 4) {
+    float acc = 0.f;
+    for (int k = lane; k < nf; k += 64) acc += fb[(int64_t)k * n_mels + m] * mag[k];
+    acc = wave_sum(acc);
+    if (lane == 0) dm[m] = acc >= log_floor ? gmel[((int64_t)b * n_mels + m) * F + f] / acc : 0.f;
+  }
+  __syncthreads();
+  // dX[k] = (fb dm)[k] X[k] / |X[k]| for k <= n/2, zero above: the inverse DFT's real part is the
+  // gradient w.r.t. the windowed frame (Re sum_k conj-free D_k e^{+2 pi i k t / n})
+  for (int k = tid; k < n; k += 256) {
+    float2 d = make_float2(0.f, 0.f);
+    if (k <= half) {
+      float g = 0.f;
+      for (int m = 0; m < n_mels; ++m) g += fb[(int64_t)k * n_mels + m] * dm[m];
+      const float sc = g / mag[k];
+      d = make_float2(sc * xre[k], sc * xim[k]);
+    }
+    buf[0][k] = d;
+  }
+  __syncthreads();
+  s = fft_stockham(buf, n, 1.f, tid, 256);
+  float* out = gframe + ((int64_t)b * F + f) * n;
+  for (int m = tid; m < n; m += 256) out[m] = buf[s][m].x * window[m];
+}
+
+// dwav[b][i] = sum over padded positions p with reflect(p - pad) == i and frames f covering p
+// (f hop <= p < f hop + n_fft) of gframe[b][f][p - f hop], in a fixed order
+__global__ void __launch_bounds__(256) stft_mel_bwd_gather_kernel(const float* __restrict__ gframe, int N, int F,
+                                                                  int n_fft, int hop, int pad,
+                                                                  float* __restrict__ dwav) {
+  const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (i >= N) return;
+  const float* gf = gframe + (int64_t)b * F * n_fft;
+  float s = 0.f;
+  int ps[3];
+  int np = 0;
+  ps[np++] = i + pad;                                    // the sample itself
+  if (i >= 1 && i <= pad) ps[np++] = pad - i;            // mirrored into the left pad
+  if (i <= N - 2 && i >= N - 1 - pad) ps[np++] = pad + 2 * (N - 1) - i;  // mirrored into the right pad
+  for (int q = 0; q < np; ++q) {
+    const int p = ps[q];
+    int f0 = p - n_fft + 1;
+    f0 = f0 <= 0 ? 0 : (f0 + hop - 1) / hop;
+    const int f1 = min(p / hop, F - 1);
+    for (int f = f0; f <= f1; ++f) s += gf[(int64_t)f * n_fft + (p - f * hop)];
+  }
+  dwav[(int64_t)b * N + i] = s;
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+// ---- BatchNorm: x (M, C) channels-last, dtype VO_F32 / VO_BF16; workspace: bn workspace size
+extern "C" int64_t vo_bn_workspace_size(int M, int C) {
+  const int CT = C == 1 ? 1 : 64;
+  const int RB = C == 1 ? 8192 : 512;
+  const int64_t nb = (M + RB - 1) / RB;
+  (void)CT;
+  return nb * C * 3 * (int64_t)sizeof(float);
+}
+
+static void bn_geometry(int M, int C, int* CT, int* RB, int* nb) {
+  *CT = C == 1 ? 1 : 64;
+  *RB = C == 1 ? 8192 : 512;
+  *nb = (M + *RB - 1) / *RB;
+}
+
+extern "C" int vo_bn_train_fwd(const void* x, int dtype, int M, int C, const float* gamma, const float* beta,
+                               float eps, float momentum, float* run_mean, float* run_var, int64_t* nbt,
+                               float* mean_rstd, float* workspace, void* y, void* stream) {
+  VO_CHECK_ARG(x && y && mean_rstd && workspace && M > 0 && C > 0, "bn_train_fwd: bad arguments");
+  VO_CHECK_ARG(dtype == VO_F32 || dtype == VO_BF16, "bn_train_fwd: dtype");
+  VO_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "bn_train_fwd: gamma and beta together");
+  VO_CHECK_ARG((run_mean == nullptr) == (run_var == nullptr), "bn_train_fwd: running stats together");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int CT, RB, nb;
+  bn_geometry(M, C, &CT, &RB, &nb);
+  const dim3 grid((unsigned)nb, (unsigned)((C + CT - 1) / CT));
+  if (dtype == VO_F32) {
+    if (CT == 1) hipLaunchKernelGGL((bn_stats_kernel<float, 1>), grid, dim3(256), 0, st, (const float*)x, M, C, RB, workspace);
+    else hipLaunchKernelGGL((bn_stats_kernel<float, 64>), grid, dim3(256), 0, st, (const float*)x, M, C, RB, workspace);
+  } else {
+    if (CT == 1) hipLaunchKernelGGL((bn_stats_kernel<bf16_t, 1>), grid, dim3(256), 0, st, (const bf16_t*)x, M, C, RB, workspace);
+    else hipLaunchKernelGGL((bn_stats_kernel<bf16_t, 64>), grid, dim3(256), 0, st, (const bf16_t*)x, M, C, RB, workspace);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, workspace, nb, C, eps,
+                     momentum, mean_rstd, run_mean, run_var, nbt);
+  const int64_t total = (int64_t)M * C;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+  if (dtype == VO_F32)
+    hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)x, total, C, mean_rstd,
+                       gamma, beta, (float*)y);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<bf16_t>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)x, total, C,
+                       mean_rstd, gamma, beta, (bf16_t*)y);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_bn_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, int M, int C, const float* gamma,
+                         const float* mean_rstd, float* workspace, float* dgamma, float* dbeta, void* dx, void* stream) {
+  VO_CHECK_ARG(x && dy && mean_rstd && workspace && dgamma && dbeta && dx && M > 0 && C > 0, "bn_bwd: bad arguments");
+  VO_CHECK_ARG((x_dtype == VO_F32 || x_dtype == VO_BF16) && (dy_dtype == VO_F32 || dy_dtype == VO_BF16),
+               "bn_bwd: dtypes");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int CT, RB, nb;
+  bn_geometry(M, C, &CT, &RB, &nb);
+  const dim3 grid((unsigned)nb, (unsigned)((C + CT - 1) / CT));
+#define VO_BNB_STATS(TX, TG)                                                                                     \
+  do {                                                                                                           \
+    if (CT == 1)                                                                                                 \
+      hipLaunchKernelGGL((bn_bwd_stats_kernel<TX, TG, 1>), grid, dim3(256), 0, st, (const TX*)x, (const TG*)dy, M, \
+                         C, RB, mean_rstd, workspace);                                                           \
+    else                                                                                                         \
+      hipLaunchKernelGGL((bn_bwd_stats_kernel<TX, TG, 64>), grid, dim3(256), 0, st, (const TX*)x, (const TG*)dy, M, \
+                         C, RB, mean_rstd, workspace);                                                           \
+  } while (0)
+  if (x_dtype == VO_F32 && dy_dtype == VO_F32) VO_BNB_STATS(float, float);
+  else if (x_dtype == VO_F32) VO_BNB_STATS(float, bf16_t);
+  else if (dy_dtype == VO_F32) VO_BNB_STATS(bf16_t, float);
+  else VO_BNB_STATS(bf16_t, bf16_t);
+#undef VO_BNB_STATS
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, workspace, nb, C,
+                     dgamma, dbeta);
+  const int64_t total = (int64_t)M * C;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+  const float inv_m = 1.f / (float)M;
+#define VO_BNB_APPLY(TX, TG)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<TX, TG>), dim3(blocks), dim3(256), 0, st, (const TX*)x, (const TG*)dy, total, \
+                     C, inv_m, mean_rstd, gamma, dgamma, dbeta, (TX*)dx)
+  if (x_dtype == VO_F32 && dy_dtype == VO_F32) VO_BNB_APPLY(float, float);
+  else if (x_dtype == VO_F32) VO_BNB_APPLY(float, bf16_t);
+  else if (dy_dtype == VO_F32) VO_BNB_APPLY(bf16_t, float);
+  else VO_BNB_APPLY(bf16_t, bf16_t);
+#undef VO_BNB_APPLY
+  VO_RETURN_LAUNCH();
+}
+
+// ---- glyph-encoder conv: x (N, H, W) fp32, w[10] = 3 x 3 kernel (row-major) + bias
+extern "C" int64_t vo_vfe_conv_workspace_size(int N, int H, int W) {
+  const int64_t nb = ((int64_t)N * H * W + VC_TILE - 1) / VC_TILE;
+  return nb * 10 * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_vfe_conv_fwd(const float* x, int N, int H, int W, const float* w, float* y, void* stream) {
+  VO_CHECK_ARG(x && w && y && N > 0 && H > 0 && W > 0, "vfe_conv_fwd: bad arguments");
+  const int64_t total = (int64_t)N * H * W;
+  hipLaunchKernelGGL(vfe_conv_fwd_kernel, dim3((unsigned)((total + VC_TILE - 1) / VC_TILE)), dim3(VC_TILE), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, N, H, W, w, y);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_vfe_conv_bwd(const float* x, const float* dy, int N, int H, int W, const float* w, float* dx,
+                               float* dw, float* workspace, void* stream) {
+  VO_CHECK_ARG(x && dy && w && dx && dw && workspace && N > 0 && H > 0 && W > 0, "vfe_conv_bwd: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = (int64_t)N * H * W;
+  const int nb = (int)((total + VC_TILE - 1) / VC_TILE);
+  hipLaunchKernelGGL(vfe_conv_bwd_kernel, dim3((unsigned)nb), dim3(VC_TILE), 0, st, x, dy, N, H, W, w, dx, workspace);
+  hipLaunchKernelGGL(vfe_conv_wgrad_finalize_kernel, dim3(10), dim3(64), 0, st, workspace, nb, dw);
+  VO_RETURN_LAUNCH();
+}
+
+// ---- log-mel backward (the framing of vo_stft_mel_ex, clip off): gmel (B, n_mels, F) -> dwav (B, N)
+extern "C" int64_t vo_stft_mel_bwd_workspace_size(int B, int N, int n_fft, int hop, int pad) {
+  const int64_t F = 1 + (N + 2 * (int64_t)pad - n_fft) / hop;
+  return (int64_t)B * F * n_fft * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_stft_mel_bwd(const float* wav, int B, int N, const float* window, const float* fb, int n_fft, int hop,
+                               int n_mels, int pad, float mag_eps, float log_floor, const float* gmel, float* dwav,
+                               float* workspace, void* stream) {
+  VO_CHECK_ARG(wav && window && fb && gmel && dwav && workspace, "stft_mel_bwd: null pointer");
+  VO_CHECK_ARG(n_fft >= 8 && n_fft <= SMB_MAX_N && (n_fft & (n_fft - 1)) == 0, "stft_mel_bwd: n_fft=%d", n_fft);
+  VO_CHECK_ARG(hop > 0 && n_mels > 0 && n_mels <= 256 && B > 0 && pad >= 0 && N > pad && N + 2 * pad >= n_fft,
+               "stft_mel_bwd: bad sizes");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int F = 1 + (N + 2 * pad - n_fft) / hop;
+  hipLaunchKernelGGL(stft_mel_bwd_frame_kernel, dim3((unsigned)F, (unsigned)B), dim3(256), 0, st, wav, N, F, window,
+                     fb, n_fft, hop, n_mels, pad, mag_eps, log_floor, gmel, workspace);
+  hipLaunchKernelGGL(stft_mel_bwd_gather_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, st,
+                     workspace, N, F, n_fft, hop, pad, dwav);
+  VO_RETURN_LAUNCH();
+}
