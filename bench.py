@@ -324,7 +324,7 @@ def bench_train(a, dev, rank, world, dist):
             "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
-            "final_loss": round(float(losses[0]), 5), "hip_graph": graphed,
+            "final_loss": round(float(losses[0].detach()) if torch.is_tensor(losses[0]) else float(losses[0]), 5), "hip_graph": graphed,
             "allreduce_bytes_per_step": n_grad * (2 if comm is not None else 4) if dist else 0,
             "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
                        "seq_len": a.mel_len, "src_len": a.src_len,

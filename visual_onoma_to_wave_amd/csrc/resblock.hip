@@ -580,7 +580,11 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // dropped in round 2 (tools/ab_pair2.py): the next window staged through registers during P2
     // with T1 beside the window (192-row tiles: +20 %), the next group's DMA pieces spread between
     // the tap steps (+2 %), 320 / 384-row tiles (spill), the version-2 kernel (pair_cfg 30: +5 % at
-    // k = 11 -- its in-P2 window loads wait behind the in-order vmcnt of the weight DMA)
+    // k = 11 -- its in-P2 window loads wait behind the in-order vmcnt of the weight DMA), and an
+    // L2 / MALL prefetch of the epilogue's bytes (next window, residual, accumulator) by LDS-DMA
+    // pieces into a trash row during P2: +8 % with 1 KiB pieces (1-4 per wave per group: +8..18 %),
+    // +7 % with 8 KiB one-dword-per-line pieces (26 per tile) -- the piece issue costs more than
+    // the exposed loads it shortens
     if (cfg == 9) {  // the previous defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
