@@ -393,7 +393,9 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
     if (K == 7) return pair2_launch<128, 2, 4, 4, 7, true, 1>(a, B, st);
     return pair2_launch<128, 2, 4, 4, 11, true, 1>(a, B, st);
   }
-  // C = 64: 8 waves of 64 rows, 512-row tiles, 2-tap register-staged groups (cfg 31: LDS-DMA)
+  // C = 64: 8 waves of 64 rows, 512-row tiles, 2-tap register-staged groups (cfg 31: LDS-DMA).
+  // Measured and dropped: two 4-wave workgroups of 256-row tiles per CU (LDS-DMA weights): 4-8 %
+  // faster alone (tools/ab_pair2.py), but s2 -3.6 % / s3 +4 % and the same 13.75 ms in the bench step
   if (cfg == 31) {
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, true, 2>(a, B, st);
     return pair2_launch<64, 1, 8, 4, 11, true, 2>(a, B, st);
