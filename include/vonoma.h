@@ -299,7 +299,8 @@ int vo_char_features(const float* energy, const float* fstats, int F, const int3
  *  vo_wav_cl8: (B, T) -> (B, T, 8) (channel 0); vo_avgpool_wav: AvgPool1d(4, 2, padding 2),
  *    (B, T) -> (B, T/2 + 1);
  *  vo_gan_reduce: *out += sum over a (rows x width) view of |a-b| (kind 0), (1-a)^2 (kind 1)
- *    or a^2 (kind 2); vo_gan_reduce_grad: ga = *scale * d(sum)/da. */
+ *    or a^2 (kind 2), deterministic (block partials in workspace, >= 512 floats, added in order);
+ *    vo_gan_reduce_grad: ga = *scale * d(sum)/da. */
 int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
                     int dst_dtype, void* stream);
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
@@ -311,38 +312,43 @@ int vo_period_fold_bwd(const void* g, int dtype, int B, int T, int P, float* gwa
 int vo_wav_cl8_bwd(const void* g, int dtype, int64_t n, float* gwav, void* stream);
 int vo_avgpool_wav_bwd(const float* g, int B, int T, float* gx, void* stream);
 int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
-                  int dtype, float* out, void* stream);
+                  int dtype, float* out, float* workspace, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
                        int width, int dtype, const float* scale, void* ga, int ldg, void* stream);
 
 /* ------------------------------------------------------------------ training backward
  * Weight gradient of a channels-last conv on MFMA (replaces the MIOpen weight pass of the
  * training backward):
- *   dw[(k*M + m)*N + n] += sum_{b, t < T_A} A[b, t, m] * B[b, t*S + k*dil - pad, n]
- * (tap-major (K, M, N): the caller permutes to the (M, N, K) conv weight order)
- * (B rows outside [0, T_B) read as 0; pre_a / pre_b: leaky-ReLU(slope) applied to that operand).
+ *   dw[(m*N + n)*K + k] = sum_{b, t < T_A} A[b, t, m] * B[b, t*S + k*dil - pad, n]
+ * (written in the conv weight's own (M, N, K) order; B rows outside [0, T_B) read as 0;
+ * pre_a / pre_b: leaky-ReLU(slope) applied to that operand).
  * Conv1d (Co, Ci, K): A = dY (T_out rows, M = Co), B = pre(x) (T_in rows, N = Ci).
  * ConvTranspose1d (Ci, Co, 2s): A = pre(x) (T_in, M = Ci), B = dY (T_up, N = Co), S = s, pad p.
- * dw fp32, accumulated with atomics: the caller zeroes it.  dtype: VO_BF16 or VO_F32 for both.
- * vo_colsum: out[c] += sum_r x[r*ld + c] (bias gradient). */
+ * dw fp32.  Deterministic: each row split stores its partial tile into ``workspace``
+ * (vo_conv1d_wgrad_workspace_size bytes for the same B, T_A, M, N, K, groups) and a second
+ * kernel adds the splits in a fixed order.  dtype: VO_BF16 or VO_F32 for both operands.
+ * vo_colsum: out[c] = sum_r x[r*ld + c] (bias gradient; block partials in workspace,
+ * vo_colsum_workspace_size bytes, added in order). */
+int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, int K, int groups);
 int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
                     int N, int K, int S, int dil, int pad, int pre_a, int pre_b, float slope,
-                    int dtype, float* dw, void* stream);
+                    int dtype, float* dw, float* workspace, void* stream);
 /* Grouped conv (groups > 1): M = C_out / groups and N = C_in / groups per group, lda >= groups*M,
  * ldb >= groups*N; group g reads A columns [g*M, (g+1)*M), B columns [g*N, (g+1)*N) and writes
- * block g of dw laid out (groups, K, M, N).  Replaces MIOpen's grouped weight pass of
+ * rows [g*M, (g+1)*M) of dw laid out (groups*M, N, K).  Replaces MIOpen's grouped weight pass of
  * the multi-scale discriminator (HiFi-GAN V1 MSD). */
 int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
                             int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
-                            int pre_b, float slope, int dtype, float* dw, void* stream);
-/* vo_conv1d_wgrad_grouped + the bias gradient in the same launch: db[g*M + m] += sum over all
+                            int pre_b, float slope, int dtype, float* dw, float* workspace, void* stream);
+/* vo_conv1d_wgrad_grouped + the bias gradient in the same launch: db[g*M + m] = sum over all
  * A rows of A[.., g*M + m] (the conv form, A = dY; pre_a must be 0), summed by the tap-0
- * workgroups as they stage A.  db fp32 (groups*M), zeroed by the caller (one buffer with dw
- * saves a fill and the separate vo_colsum launch). */
+ * workgroups as they stage A (saves the separate vo_colsum launch). */
 int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B,
                          int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
-                         int pre_b, float slope, int dtype, float* dw, float* db, void* stream);
-int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream);
+                         int pre_b, float slope, int dtype, float* dw, float* db, float* workspace,
+                         void* stream);
+int64_t vo_colsum_workspace_size(int64_t rows, int C);
+int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, float* workspace, void* stream);
 
 /* Leaky-ReLU / ReLU backward mask: out[r, c] = g[r, c] * (ref[r, c] > 0 ? 1 : slope) over a
  * (rows x width) view with leading dimensions (out may alias g; ref = the activation's input, or

@@ -101,9 +101,11 @@ def test_training_reduces_loss(device):
 def test_graphed_train_step_matches_eager(device):
     """train.GraphedTrainStep (HIP-graph replay with the capturable Adam and a device-tensor
     learning rate, replays launched back to back with no host wait) against the same number of
-    eager train_step calls (fp32, dropout off).  The warm-up steps before the capture are undone,
-    so 12 calls are 12 updates.  The weight-gradient atomics make two eager runs differ slightly;
-    training amplifies that, so the graphed run is held to the spread of a second eager run."""
+    eager train_step calls (fp32, dropout off, the same capturable Adam).  The warm-up steps
+    before the capture are undone, so 12 calls are 12 updates.  Every backward kernel is
+    deterministic (row-split partials added in a fixed order, no atomics), so two eager runs are
+    bit-identical and the replayed run must be too: a stale input, learning rate or packed
+    weight, an extra warm-up update or a read outside stream order would show as any difference."""
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
     from visual_onoma_to_wave_amd.train import GraphedTrainStep, train_step
     pc, mc, tc = configs()
@@ -116,7 +118,7 @@ def test_graphed_train_step_matches_eager(device):
         load_into(m, vtts_arrays())
         m = m.to(device).train().set_precision("fp32")
         _no_dropout(m)
-        opt = ScheduledOptim(m, tc, mc, 0, capturable=graphed)
+        opt = ScheduledOptim(m, tc, mc, 0, capturable=True)
         per_step = []
         if graphed:
             run = GraphedTrainStep(m, opt, FastSpeech2Loss(), warmup=3)
@@ -132,17 +134,11 @@ def test_graphed_train_step_matches_eager(device):
         finals.append((np.array([float(x) for x in per_step]),
                        torch.cat([p.detach().flatten().cpu() for p in m.parameters()])))
     (l0, p0), (l1, p1), (lg, pg) = finals
-    assert np.isfinite(lg).all()
-    p_noise = float((p1 - p0).norm() / p0.norm())
-    p_err = float((pg - p0).norm() / p0.norm())
-    l_noise, l_err = float(np.abs(l1 - l0).max()), float(np.abs(lg - l0).max())
-    print(f"graphed vs eager: params {p_err:.2e} (eager spread {p_noise:.2e}), per-step losses {l_err:.2e} "
-          f"(eager spread {l_noise:.2e})")
-    # twelve Adam steps at lr up to 3e-4 move the weights by ~1e-2 of their norm and the loss
-    # 25 -> 7.5: a replay with a stale input / learning rate / packed weight, or an extra warm-up
-    # update, differs at that scale.
-    assert p_err < max(10 * p_noise, 5e-4) and p_err < 1e-3
-    assert l_err < max(10 * l_noise, 1e-2)
+    assert np.isfinite(lg).all() and l0[-1] < 0.6 * l0[0]  # the twelve updates really train
+    print(f"graphed vs eager: params {float((pg - p0).norm() / p0.norm()):.2e}, per-step losses "
+          f"{float(np.abs(lg - l0).max()):.2e}; eager vs eager {float((p1 - p0).norm() / p0.norm()):.2e}")
+    assert torch.equal(p1, p0) and np.array_equal(l1, l0), "eager training is not deterministic"
+    assert torch.equal(pg, p0) and np.array_equal(lg, l0), "graph replay differs from the eager steps"
 
 
 def test_inference_after_graphed_training_uses_new_weights(device):

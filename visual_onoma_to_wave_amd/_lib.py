@@ -105,17 +105,19 @@ _SIGNATURES = {
                             c_void_p, c_void_p, c_void_p]),
     "vo_stft_mel_ex": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_conv1d_wgrad_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "vo_conv1d_wgrad": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p]),
+                                c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_conv1d_wgrad_grouped": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p,
-                                        c_void_p]),
+                                        c_void_p, c_void_p]),
     "vo_conv1d_wgrad_bias": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
-                                     c_void_p]),
+                                     c_void_p, c_void_p]),
     "vo_lrelu_mask": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, ctypes.c_int64, c_int, c_float,
                               c_void_p, c_int, c_void_p]),
-    "vo_colsum": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "vo_colsum_workspace_size": (c_int64, [c_int64, c_int]),
+    "vo_colsum": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),
     "vo_pack_grouped": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
@@ -125,7 +127,7 @@ _SIGNATURES = {
     "vo_period_fold_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "vo_wav_cl8_bwd": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "vo_avgpool_wav_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
-    "vo_gan_reduce": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
+    "vo_gan_reduce": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p,
                               c_void_p]),
     "vo_gan_reduce_grad": (c_int, [c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_int, c_void_p,
                                    c_void_p, c_int, c_void_p]),

@@ -255,7 +255,6 @@ conv1d_kernel(ConvArgs a) {
     n_chunks = min(a.kcs, n_chunks - z0);
   }
   const int tsteps = (a.K + TPS - 1) / TPS;
-  const int n_steps = n_chunks * tsteps;
   const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE;
   // prologue activation as one select: none -> slope 1, relu -> 0, lrelu -> slope
   const float pre_s = a.pre_act == VO_ACT_RELU ? 0.f : (a.pre_act == VO_ACT_LRELU ? a.pre_slope : 1.f);

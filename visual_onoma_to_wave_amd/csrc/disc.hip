@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) avgpool_kernel(const float* __restrict__ 
 template <typename TA>
 __global__ void __launch_bounds__(256) gan_reduce_kernel(int kind, const TA* __restrict__ a, int lda,
                                                          const TA* __restrict__ b, int ldb, int64_t rows, int width,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ part) {
   __shared__ float red[4];
   const int64_t n = rows * width;
   float s = 0.f;
@@ -99,7 +99,16 @@ __global__ void __launch_bounds__(256) gan_reduce_kernel(int kind, const TA* __r
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// *out += the block partials added in block order (one wave: lanes stride the blocks, a fixed tree)
+__global__ void __launch_bounds__(64) gan_reduce_final_kernel(const float* __restrict__ part, int n,
+                                                              float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 64) s += part[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[0] += s;
 }
 
 // gradient of scale * reduction wrt a (b held constant), written in a's layout
@@ -231,19 +240,20 @@ extern "C" int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stre
 }
 
 extern "C" int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
-                             int dtype, float* out, void* stream) {
-  VO_CHECK_ARG(a && out && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce: bad arguments");
+                             int dtype, float* out, float* workspace, void* stream) {
+  VO_CHECK_ARG(a && out && workspace && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce: bad arguments");
   VO_CHECK_ARG(rows > 0 && width > 0 && lda >= width && (kind != 0 || ldb >= width), "gan_reduce: bad shape");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // every block ends in one atomic on the same scalar: at most 512 of them (4096 same-address
-  // atomics serialised at L2 took ~34 us a call; the grid-stride loop keeps the loads coalesced)
+  // at most 512 block partials (workspace: 512 floats), added in order by one wave (deterministic;
+  // the grid-stride loop keeps the loads coalesced)
   const int g = std::min(grid_for(rows * width), 512);
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(gan_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
-                       (const bf16_t*)b, ldb, rows, width, out);
+                       (const bf16_t*)b, ldb, rows, width, workspace);
   else
     hipLaunchKernelGGL(gan_reduce_kernel<float>, dim3(g), dim3(256), 0, st, kind, (const float*)a, lda,
-                       (const float*)b, ldb, rows, width, out);
+                       (const float*)b, ldb, rows, width, workspace);
+  hipLaunchKernelGGL(gan_reduce_final_kernel, dim3(1), dim3(64), 0, st, workspace, g, out);
   VO_RETURN_LAUNCH();
 }
 

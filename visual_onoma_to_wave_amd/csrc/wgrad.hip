@@ -2,9 +2,10 @@
 // (training paths C4 / C5): replaces the MIOpen ``convolution_backward`` weight pass that
 // SURVEY.md 8(b) allowed as the initial fallback.
 //
-//   dW[(k * M + m) * N + n] += sum_{b, t < T_A} A[b, t, m] * B[b, t * S + k * dil - pad, n]
-// (tap-major: a wave's atomics cover 4 runs of 16 consecutive floats; in the conv weight's own
-// (m, n, k) order every lane hit its own cache line and the atomics took 70-85 % of the time)
+//   dW[m, n, k] = sum_{b, t < T_A} A[b, t, m] * B[b, t * S + k * dil - pad, n]
+// (the per-split partial tiles are tap-major (K, M, N): a wave's stores cover runs of 16
+// consecutive floats; round 1's fp32 atomics in the weight's (m, n, k) order hit one cache line
+// per lane and took 70-85 % of the time)
 //
 // (rows of B outside [0, T_B) are zero; optional leaky-ReLU applied to either operand as it is
 // staged).  Conv1d (Co, Ci, K):      A = dY (rows T_out, M = Co), B = pre(x) (rows T_in, N = Ci),
@@ -15,8 +16,11 @@
 // N/64 tiles, taps); each workgroup stages 64-row chunks of both operands into LDS in their
 // natural channels-last layout and reads the MFMA fragments transposed -- ds_read_b64_tr_b16
 // (gfx950) delivers 4 rows of one channel per lane, so the reduction dimension (rows) lands
-// on the fragment's k without a transpose pass.  Partial sums of the row splits meet in fp32
-// atomics (the caller zeroes dW).  fp32 parity mode: the same tiles with 16x16x4 f32 MFMAs.
+// on the fragment's k without a transpose pass.  Every row split stores its partial tile into a
+// caller-owned workspace; a second kernel adds the splits in order and writes dW in the conv
+// weight's own (M, N, K) order -- deterministic (bit-identical run to run, so a graph replay can
+// be checked bit for bit against eager steps), no zero fill, no permute copy.  fp32 parity mode:
+// the same tiles with 16x16x4 f32 MFMAs.
 
 #include <algorithm>
 
@@ -35,9 +39,11 @@ struct WgradArgs {
   int M, N, K, S, dil, pad, Bn;
   int pre_a, pre_b; float slope;
   int rows_per_split;
-  float* dw;
-  float* db;  // nullable: bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
-  int abl;  // timing ablations (wgrad_cfg 10 / 11): 1 = plain stores instead of atomics, 2 = no loads
+  float* part;  // [split][groups][K][M][N] partial tiles, then [split][groups][M] bias partials
+  int64_t n_w;  // groups * K * M * N
+  int64_t n_tot;  // n_w + groups * M (with bias) or n_w: floats per split
+  bool bias;  // bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
+  int abl;  // timing ablation (wgrad_cfg 11): 2 = no loads
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
 // and B columns [g N, (g+1) N) and writes block g of the (groups, K, M, N) result
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   const int64_t r_end = min(rows, r_begin + p.rows_per_split);
   const TC* A = reinterpret_cast<const TC*>(p.a) + (int64_t)grp * p.M;
   const TC* Bs = reinterpret_cast<const TC*>(p.bsrc) + (int64_t)grp * p.N;
-  float* dw = p.dw + ((int64_t)grp * p.K + k) * p.M * p.N;
+  float* dw = p.part + (int64_t)blockIdx.x * p.n_tot + ((int64_t)grp * p.K + k) * p.M * p.N;
   constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
   constexpr int VPR = WG_T / EV;            // vectors per staged row
   constexpr int NV = WG_R * VPR / 256;      // vectors per thread per operand
@@ -81,8 +87,8 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused bias gradient: the workgroups of tap 0 and the first N tile see every A row of their M
   // tile exactly once -> column sums of the staged A chunks (thread: column tid & 63, rows 16 x
-  // (tid >> 6) ..), one LDS reduction and one atomic per column at the end
-  const bool do_bias = p.db != nullptr && k == 0 && n0 == 0;  // workgroup-uniform
+  // (tid >> 6) ..), one LDS reduction and one partial per column at the end
+  const bool do_bias = p.bias && k == 0 && n0 == 0;  // workgroup-uniform
   float bsum = 0.f;
 
   for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
@@ -195,7 +201,8 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
     bred[tid >> 6][tid & 63] = bsum;
     __syncthreads();
     if (tid < 64 && m0 + tid < p.M)
-      atomicAdd(p.db + (int64_t)grp * p.M + m0 + tid, bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid]);
+      p.part[(int64_t)blockIdx.x * p.n_tot + p.n_w + (int64_t)grp * p.M + m0 + tid] =
+          bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
   }
 
   // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[k][m][n]
@@ -207,18 +214,34 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
-        if (m < p.M && n < p.N) {
-          if (p.abl & 1)
-            dw[(int64_t)m * p.N + n] = acc[i][j][e];
-          else
-            atomicAdd(dw + (int64_t)m * p.N + n, acc[i][j][e]);
-        }
+        if (m < p.M && n < p.N) dw[(int64_t)m * p.N + n] = acc[i][j][e];
       }
 }
 
-// column sums of a (rows x C) channels-last tensor -> out[C] (fp32 atomics; caller zeroes).
+// dW[((g M + m) N + n) K + k] = sum over splits in order of part[s][g][k][m][n]; db likewise
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int splits, int64_t n_w,
+                                                           int64_t n_tot, int M, int N, int K,
+                                                           float* __restrict__ dw, float* __restrict__ db) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_tot; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int q = 0; q < splits; ++q) s += part[(int64_t)q * n_tot + i];
+    if (i < n_w) {
+      const int n = (int)(i % N);
+      const int64_t r = i / N;
+      const int m = (int)(r % M);
+      const int64_t gk = r / M;
+      const int k = (int)(gk % K), g = (int)(gk / K);
+      dw[(((int64_t)g * M + m) * N + n) * K + k] = s;
+    } else {
+      db[i - n_w] = s;
+    }
+  }
+}
+
+// column sums of a (rows x C) channels-last tensor -> out[C] (written): per-block partials in a
+// workspace, added in block order by wgrad_reduce_kernel's bias path (deterministic).
 // Thread t owns the 8-channel vector t % (C / 8) of rows t / (C / 8) + k * (256 / (C / 8)):
-// coalesced 16-byte loads, register accumulation, one LDS reduction and C atomics per block.
+// coalesced 16-byte loads, register accumulation, one LDS reduction and C partials per block.
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, int64_t rows, int C, int ld,
                                                      int rows_per_block, float* __restrict__ out) {
@@ -242,7 +265,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, in
   for (int c = tid; c < C; c += 256) {  // channel c = vector c / 8, element c % 8
     float s = 0.f;
     for (int q = 0; q < per; ++q) s += red[(q * nv + c / 8) * 8 + (c % 8)];
-    atomicAdd(out + c, s);
+    out[(int64_t)blockIdx.x * C + c] = s;
   }
 }
 
@@ -250,10 +273,36 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, in
 
 using namespace vo;
 
+// row-split plan shared by the workspace query and the launch: enough workgroups to fill 256
+// CUs ~4 deep, at least 4 chunks of 64 rows each, serial row chains of at most 64 chunks (a small
+// tile x tap grid -- the MSD's 32 x 16 groups -- otherwise leaves one workgroup walking every row)
+static void wgrad_plan(int B, int T_A, int M, int N, int K, int groups, int64_t* splits_out, int* rps_out) {
+  const int64_t zk = (int64_t)K * groups;
+  const int64_t rows = (int64_t)B * T_A;
+  const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
+  const int wc = vo_tune_get("wgrad_cfg");
+  const int64_t target = wc == 1 ? 4096 : wc == 2 ? 8192 : wc == 3 ? 16384 : 1024;
+  int64_t splits = std::max<int64_t>(1, (target + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
+  const int64_t max_rows = wc == 4 ? 2048 : wc == 5 ? 8192 : wc == 6 ? (int64_t)1 << 40 : 4096;
+  splits = std::max<int64_t>(splits, (rows + max_rows - 1) / max_rows);
+  const int rps = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
+  *splits_out = (rows + rps - 1) / rps;
+  *rps_out = rps;
+}
+
+extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, int K, int groups) {
+  if (B <= 0 || T_A <= 0 || M <= 0 || N <= 0 || K <= 0 || groups <= 0) return 0;
+  int64_t splits;
+  int rps;
+  wgrad_plan(B, T_A, M, N, K, groups, &splits, &rps);
+  return splits * ((int64_t)groups * K * M * N + (int64_t)groups * M) * (int64_t)sizeof(float);
+}
+
 extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
                                     int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
-                                    float slope, int dtype, float* dw, float* db, void* stream) {
-  VO_CHECK_ARG(a && b && dw, "conv1d_wgrad: null pointer");
+                                    float slope, int dtype, float* dw, float* db, float* workspace, void* stream) {
+  VO_CHECK_ARG(a && b && dw && workspace, "conv1d_wgrad: null pointer");
   VO_CHECK_ARG(!db || !pre_a, "conv1d_wgrad: the fused bias gradient sums A as stored (pre_a must be off)");
   VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1 && groups >= 1, "conv1d_wgrad: bad sizes");
   const int ev = dtype == VO_BF16 ? 8 : 4;
@@ -263,22 +312,16 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   WgradArgs p;
   p.a = a; p.lda = lda; p.T_A = T_A; p.bsrc = b; p.ldb = ldb; p.T_B = T_B;
   p.M = M; p.N = N; p.K = K; p.S = S; p.dil = dil; p.pad = pad; p.Bn = B;
-  p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope; p.dw = dw; p.db = db;
+  p.pre_a = pre_a; p.pre_b = pre_b; p.slope = slope;
+  p.part = workspace;
+  p.bias = db != nullptr;
+  p.n_w = (int64_t)groups * K * M * N;
+  p.n_tot = p.n_w + (db ? (int64_t)groups * M : 0);
+  p.abl = vo_tune_get("wgrad_cfg") == 11 ? 2 : 0;  // 11: no loads (timing)
   const int64_t zk = (int64_t)K * groups;
-  const int64_t rows = (int64_t)B * T_A;
   const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
-  // enough workgroups to fill 256 CUs ~4 deep, at least 4 chunks of 64 rows each
-  const int wc = vo_tune_get("wgrad_cfg");
-  const int64_t target = wc == 1 ? 4096 : wc == 2 ? 8192 : wc == 3 ? 16384 : 1024;
-  p.abl = wc >= 10 ? wc - 9 : 0;  // 10: no atomics, 11: no loads, 12: neither
-  int64_t splits = std::max<int64_t>(1, (target + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
-  splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
-  // serial row chains of at most 64 chunks (a small tile x tap grid -- the MSD's 32 x 16 groups --
-  // otherwise leaves one workgroup walking every row)
-  const int64_t max_rows = wc == 4 ? 2048 : wc == 5 ? 8192 : wc == 6 ? (int64_t)1 << 40 : 4096;
-  splits = std::max<int64_t>(splits, (rows + max_rows - 1) / max_rows);
-  p.rows_per_split = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
-  splits = (rows + p.rows_per_split - 1) / p.rows_per_split;
+  int64_t splits;
+  wgrad_plan(B, T_A, M, N, K, groups, &splits, &p.rows_per_split);
   VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)zk);
@@ -286,34 +329,52 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
+  const unsigned rg = (unsigned)std::min<int64_t>((p.n_tot + 255) / 256, 2048);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, workspace, (int)splits, p.n_w, p.n_tot, M, N, K,
+                     dw, db);
   VO_RETURN_LAUNCH();
 }
 
 extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
                                        int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
-                                       float slope, int dtype, float* dw, void* stream) {
+                                       float slope, int dtype, float* dw, float* workspace, void* stream) {
   return vo_conv1d_wgrad_bias(a, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, groups, pre_a, pre_b, slope, dtype,
-                              dw, nullptr, stream);
+                              dw, nullptr, workspace, stream);
 }
 
 extern "C" int vo_conv1d_wgrad(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M, int N,
                                int K, int S, int dil, int pad, int pre_a, int pre_b, float slope, int dtype, float* dw,
-                               void* stream) {
+                               float* workspace, void* stream) {
   return vo_conv1d_wgrad_grouped(a, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, 1, pre_a, pre_b, slope, dtype, dw,
-                                 stream);
+                                 workspace, stream);
 }
 
-extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, void* stream) {
-  VO_CHECK_ARG(x && out && rows > 0 && C > 0 && ld >= C && C % 8 == 0 && ld % 8 == 0 && C <= 2048,
-               "colsum: bad arguments (C %% 8 == 0, C <= 2048)");
-  // ~1024 blocks of >= 8 row passes each: enough parallelism for 256 CUs, few atomics per channel
+static int colsum_blocks(int64_t rows, int C, int* rpb) {
+  // ~1024 blocks of >= 8 row passes each: enough parallelism for 256 CUs
   const int per = 256 / (C / 8 > 0 ? C / 8 : 1);
-  const int rpb = (int)std::max<int64_t>(8 * std::max(per, 1), (rows + 1023) / 1024);
+  *rpb = (int)std::max<int64_t>(8 * std::max(per, 1), (rows + 1023) / 1024);
+  return (int)((rows + *rpb - 1) / *rpb);
+}
+
+extern "C" int64_t vo_colsum_workspace_size(int64_t rows, int C) {
+  if (rows <= 0 || C <= 0) return 0;
+  int rpb;
+  return (int64_t)colsum_blocks(rows, C, &rpb) * C * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, float* workspace,
+                         void* stream) {
+  VO_CHECK_ARG(x && out && workspace && rows > 0 && C > 0 && ld >= C && C % 8 == 0 && ld % 8 == 0 && C <= 2048,
+               "colsum: bad arguments (C %% 8 == 0, C <= 2048)");
+  int rpb;
+  const int g = colsum_blocks(rows, C, &rpb);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const unsigned g = (unsigned)((rows + rpb - 1) / rpb);
   if (dtype == VO_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, rows, C, ld, rpb, out);
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, rows, C, ld, rpb, workspace);
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, rows, C, ld, rpb, out);
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, rows, C, ld, rpb, workspace);
+  // the block partials [g][C] added in block order: the reduce kernel's bias path (n_w = 0)
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min((C + 255) / 256, 2048)), dim3(256), 0, st, workspace,
+                     g, (int64_t)0, (int64_t)C, 1, 1, 1, (float*)nullptr, out);
   VO_RETURN_LAUNCH();
 }

@@ -49,7 +49,7 @@ class HifiGanTrainer:
     decay is written into the captured step without re-capturing."""
 
     def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None, graphed=False,
-                 comm_dtype=None):
+                 comm_dtype=None, capturable=None):
         self.generator = generator
         device = device or next(generator.parameters()).device
         self.mpd = (mpd or MultiPeriodDiscriminator()).to(device)
@@ -59,11 +59,16 @@ class HifiGanTrainer:
         self._graph = None
         if graphed:
             _check_graph_runtime()
-        lr = (lambda: torch.tensor(float(h.learning_rate), device=device)) if graphed else (lambda: h.learning_rate)
+        # capturable AdamW (device-tensor step counts and learning rates) is required for the graph
+        # and may be chosen for eager steps too (capturable=True: the same update arithmetic)
+        cap = graphed if capturable is None else bool(capturable)
+        if graphed and not cap:
+            raise ValueError("graphed training needs the capturable optimizer")
+        lr = (lambda: torch.tensor(float(h.learning_rate), device=device)) if cap else (lambda: h.learning_rate)
         self.optim_g = torch.optim.AdamW(generator.parameters(), lr(), betas=[h.adam_b1, h.adam_b2],
-                                         capturable=graphed)
+                                         capturable=cap)
         self.optim_d = torch.optim.AdamW(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
-                                         lr(), betas=[h.adam_b1, h.adam_b2], capturable=graphed)
+                                         lr(), betas=[h.adam_b1, h.adam_b2], capturable=cap)
         self.sched_g = torch.optim.lr_scheduler.ExponentialLR(self.optim_g, gamma=h.lr_decay)
         self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
         self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,

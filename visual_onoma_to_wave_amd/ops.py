@@ -668,8 +668,9 @@ def gan_reduce(kind, a, b=None, out=None):
         b = lb
     if out is None:
         out = torch.zeros((), dtype=torch.float32, device=a.device)
+    ws = torch.empty(512, dtype=torch.float32, device=a.device)  # block partials (deterministic sum)
     _lib.check(_lib.lib().vo_gan_reduce(kind, _ptr(la), lda, _ptr(b), ldb, rows, width, vo_dtype(a), _ptr(out),
-                                        _stream(a)), "vo_gan_reduce")
+                                        _ptr(ws), _stream(a)), "vo_gan_reduce")
     return out
 
 
@@ -781,18 +782,17 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     if with_bias and (pre_a is not None or transposed):
         raise ValueError("conv1d_wgrad: the fused bias gradient needs the conv form with a = dY as stored")
     mg, ng = M // groups, N // groups
-    n_w = groups * K * mg * ng
-    buf = torch.zeros(n_w + (M if with_bias else 0), dtype=torch.float32, device=a.device)  # one fill
-    dw = buf[:n_w].view(groups, K, mg, ng)  # tap-major (kernel order)
-    db = buf[n_w:] if with_bias else None
+    L = _lib.lib()
+    w = torch.empty((M, ng, K), dtype=torch.float32, device=a.device)  # written in weight order
+    db = torch.empty(M, dtype=torch.float32, device=a.device) if with_bias else None
+    ws = torch.empty(int(L.vo_conv1d_wgrad_workspace_size(B, T_A, mg, ng, K, groups)) // 4, dtype=torch.float32,
+                     device=a.device)  # row-split partials, added in a fixed order (deterministic)
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
-    _lib.check(_lib.lib().vo_conv1d_wgrad_bias(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K,
-                                               S, dil, pad, groups, int(pre_a is not None),
-                                               int(pre_b is not None), float(slope), vo_dtype(a), _ptr(dw),
-                                               _ptr(db), _stream(a)), "vo_conv1d_wgrad")
-    w = dw.permute(0, 2, 3, 1).reshape(M, ng, K)
+    _lib.check(L.vo_conv1d_wgrad_bias(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K, S, dil, pad, groups,
+                                      int(pre_a is not None), int(pre_b is not None), float(slope), vo_dtype(a),
+                                      _ptr(w), _ptr(db), _ptr(ws), _stream(a)), "vo_conv1d_wgrad")
     return (w, db) if with_bias else w
 
 
@@ -827,6 +827,9 @@ def colsum(x):
     if C % 8:
         x = torch.nn.functional.pad(x, (0, 8 - C % 8)).contiguous()
         return colsum(x)[:C]
-    out = torch.zeros(C, dtype=torch.float32, device=x.device)
-    _lib.check(_lib.lib().vo_colsum(_ptr(x), x.numel() // C, C, C, vo_dtype(x), _ptr(out), _stream(x)), "vo_colsum")
+    rows = x.numel() // C
+    L = _lib.lib()
+    out = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_colsum_workspace_size(rows, C)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_colsum(_ptr(x), rows, C, C, vo_dtype(x), _ptr(out), _ptr(ws), _stream(x)), "vo_colsum")
     return out
