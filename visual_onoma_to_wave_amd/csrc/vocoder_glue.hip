@@ -7,6 +7,8 @@
 // pack_weight_kernel: weight-norm fold (models.py:105-109,167-174), BatchNorm fold and the
 //   [K][Co][Ci] / polyphase ConvTranspose1d layouts the conv1d kernel reads.
 
+#include <algorithm>
+
 #include "vo_common.h"
 
 namespace vo {
@@ -182,6 +184,42 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
   }
 }
 
+// without the weight-norm fold: one thread per DESTINATION element (grid-stride), the source
+// gathered -- the whole weight is L2-resident while it is walked, and the stores, which the
+// per-row kernel above scattered 2 bytes at a time across the taps (8 us for a 256 x 256 x 9
+// training weight), go out as contiguous 128-byte wave rows
+template <typename TD>
+__global__ void __launch_bounds__(256) pack_weight_lin_kernel(const float* __restrict__ src,
+                                                              const float* __restrict__ row_scale, int mode, int Co,
+                                                              int Ci, int K, int stride, TD* __restrict__ dst) {
+  const int64_t n = (int64_t)Co * Ci * K;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int64_t si;
+    int co;
+    if (mode == VO_PACK_CONV) {  // dst[k][co][ci] <- src[co][ci][k]
+      const int ci = (int)(i % Ci);
+      const int64_t r = i / Ci;
+      co = (int)(r % Co);
+      const int k = (int)(r / Co);
+      si = ((int64_t)co * Ci + ci) * K + k;
+    } else if (mode == VO_PACK_DGRAD) {  // dst[K-1-k][ci][co] <- src[co][ci][k]
+      co = (int)(i % Co);
+      const int64_t r = i / Co;
+      const int ci = (int)(r % Ci);
+      const int k = K - 1 - (int)(r / Ci);
+      si = ((int64_t)co * Ci + ci) * K + k;
+    } else {  // ConvTranspose1d: dst[kk][r*Co + co][ci] <- src[ci][co][r + s*(1-kk)]
+      const int ci = (int)(i % Ci);
+      const int64_t q = i / Ci;
+      const int col = (int)(q % ((int64_t)stride * Co)), kk = (int)(q / ((int64_t)stride * Co));
+      const int rr = col / Co;
+      co = col - rr * Co;
+      si = ((int64_t)ci * Co + co) * K + rr + stride * (1 - kk);
+    }
+    dst[i] = from_f32<TD>(src[si] * (row_scale ? row_scale[co] : 1.f));
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -228,6 +266,17 @@ extern "C" int vo_pack_weight(const float* src, const float* g, const float* row
   VO_CHECK_ARG(mode == VO_PACK_CONV || mode == VO_PACK_DGRAD || (mode == VO_PACK_CONVT && stride >= 1 && K == 2 * stride),
                "pack_weight: bad mode/stride (K must be 2*stride for ConvTranspose1d)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!g) {
+    const int64_t n = (int64_t)Co * Ci * K;
+    const dim3 lg((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+    if (dst_dtype == VO_BF16)
+      hipLaunchKernelGGL(pack_weight_lin_kernel<bf16_t>, lg, dim3(256), 0, st, src, row_scale, mode, Co, Ci, K, stride,
+                         (bf16_t*)dst);
+    else
+      hipLaunchKernelGGL(pack_weight_lin_kernel<float>, lg, dim3(256), 0, st, src, row_scale, mode, Co, Ci, K, stride,
+                         (float*)dst);
+    VO_RETURN_LAUNCH();
+  }
   dim3 grid((unsigned)(mode == VO_PACK_CONVT ? Ci : Co));
   if (dst_dtype == VO_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, grid, dim3(256), 0, st, src, g, row_scale, mode, Co, Ci, K, stride,
