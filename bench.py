@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="infer: skip the C2 / C3 sub-measurements")
     ap.add_argument("--no-graph", action="store_true", help="train / gan modes: eager steps instead of one HIP graph")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="infer: run acoustic model and vocoder back to back instead of overlapping the acoustic "
+                         "model of batch i+1 (own stream) with the vocoder of batch i")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="train / gan under torchrun: gradient all-reduce dtype")
     ap.add_argument("--mode", default="infer", choices=["infer", "c2", "c3", "train", "gan"],
@@ -422,6 +425,20 @@ def infer(a, dev, rank, world, dist):
         out = model(*args)
         return gen.run(out[1])  # postnet mel is already channels-last (B, T, 80): no transpose
 
+    if not a.no_pipeline:
+        # two-stage serving pipeline (visual_onoma_to_wave_amd.pipeline): the acoustic model of
+        # batch i + 1 runs on its own stream while the vocoder synthesises batch i -- every step
+        # still runs one whole acoustic pass and one whole vocoder pass
+        from visual_onoma_to_wave_amd.pipeline import SynthesisPipeline
+        pipe = SynthesisPipeline(model, gen, dev)
+
+        def step():  # noqa: F811
+            pipe.submit(*args)
+            return pipe.next_wav()[1]
+
+        with torch.no_grad():
+            pipe.submit(*args)  # the pipeline's first stage, before the warm-up and timed steps
+
     with torch.no_grad():
         for _ in range(a.warmup):
             step()
@@ -455,7 +472,9 @@ def infer(a, dev, rank, world, dist):
                                    "energy) -> HiFi-GAN V1 generator -> B x 131072 samples",
                        "model": "vTTS (35.3M) + HiFi-GAN V1 (13.9M)", "global_batch": a.batch * world,
                        "per_gpu_batch": a.batch, "seq_len": a.mel_len, "src_len": a.src_len,
-                       "parallelism": f"replicas x{world} (no data-path collective)"},
+                       "parallelism": f"replicas x{world} (no data-path collective)",
+                       "pipeline": ("sequential" if a.no_pipeline else
+                                    "acoustic(batch i+1) on its own stream || vocoder(batch i)")},
             "mel_frames_per_s": round(frames / elapsed, 1),
             "x_realtime": round(value / SR, 1),
             "roofline": roof,

@@ -185,3 +185,28 @@ def test_generator_c3_vs_oracle(gen, oracle_gsd):
         e = rel_l2(wav[b:b + 1], ref)
         print(f"utterance {b}: rel-L2 {e:.2e} (bar {tol:.2e})")
         assert e < tol, (b, e, tol)
+
+
+def test_synthesis_pipeline_matches_sequential(vtts, gen):
+    """pipeline.SynthesisPipeline (acoustic model of batch i + 1 on its own stream while batch i is
+    vocoded) returns, batch for batch, exactly what the sequential model -> Generator.run gives."""
+    from visual_onoma_to_wave_amd.pipeline import SynthesisPipeline
+    vtts.set_precision("mixed")
+    gen.set_compute_dtype(torch.bfloat16)
+    batches = []
+    for seed in (11, 12, 13):
+        args = _c2_args(seed, True, True)
+        batches.append([a.cuda() if torch.is_tensor(a) else a for a in args] + [None, True])
+    with torch.no_grad():
+        ref = [gen.run(vtts(*b)[1]).cpu() for b in batches]
+        pipe = SynthesisPipeline(vtts, gen)
+        pipe.submit(*batches[0])
+        got = []
+        for i in range(len(batches)):
+            if i + 1 < len(batches):
+                pipe.submit(*batches[i + 1])
+            got.append(pipe.next_wav()[1])
+        torch.cuda.synchronize()
+    assert pipe.pending() == 0
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g.cpu())
