@@ -11,5 +11,5 @@ timeout -k 10 300 python bench.py > "$OUT/bench.out" 2> "$OUT/bench.err" || { ta
 tail -1 "$OUT/bench.out" > "$OUT/bench.json"
 cat "$OUT/bench.json"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 10 --cpu-seconds 0 > /dev/null 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 10 --cpu-seconds 0 --no-configs > /dev/null 2>&1 || exit 1
 python tools/trace_tail_stats.py "$OUT/prof/run_kernel_trace.csv" conv_post_rows_kernel 4 3 && rm -f "$OUT/prof/run_kernel_trace.csv"

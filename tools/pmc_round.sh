@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
   lc=$(echo $c | tr 'A-Z' 'a-z')
-  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/raw_$lc" -o run -- python bench.py --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/$lc.log" 2>&1 || { tail -5 "$OUT/$lc.log"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/raw_$lc" -o run -- python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-configs > "$OUT/$lc.log" 2>&1 || { tail -5 "$OUT/$lc.log"; exit 1; }
   f=$(find "$OUT/raw_$lc" -name '*counter_collection.csv' | head -1)
   [ -n "$f" ] || { echo "no counter csv for $c"; exit 1; }
   python - "$f" "$OUT/$lc.csv" <<'PY'
