@@ -138,6 +138,122 @@ __global__ void __launch_bounds__(256) gan_reduce_grad_kernel(int kind, const TA
 
 static int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 4096); }
 
+// 8-element vector forms of the three kernels above (width and leading dimensions multiples of 8,
+// 16-byte aligned bases): one 16 / 32-byte load per operand per 8 elements, and the row / column
+// split of the flat index (a 64-bit division per ELEMENT in the scalar kernels, which made them
+// 10-30 us calls) per vector, or none at all when every operand is contiguous (FLAT)
+struct RowMap {
+  int64_t wv;  // vectors per row
+  __device__ __forceinline__ void at(int64_t v, int64_t* r, int* c) const {
+    *r = v / wv;
+    *c = (int)(v - *r * wv) * 8;
+  }
+};
+
+template <typename TA, bool FLAT>
+__global__ void __launch_bounds__(256) gan_reduce_v8_kernel(int kind, const TA* __restrict__ a, int lda,
+                                                            const TA* __restrict__ b, int ldb, int64_t rows,
+                                                            int width, float* __restrict__ part) {
+  __shared__ float red[4];
+  const RowMap rm{width / 8};
+  const int64_t nv = rows * rm.wv;
+  float s = 0.f;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    int64_t oa = v * 8, ob = v * 8;
+    if constexpr (!FLAT) {
+      int64_t r;
+      int c;
+      rm.at(v, &r, &c);
+      oa = r * lda + c;
+      ob = r * ldb + c;
+    }
+    float x[8];
+    load8(a + oa, x);
+    if (kind == 0) {
+      float y[8];
+      load8(b + ob, y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += fabsf(x[e] - y[e]);
+    } else if (kind == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (1.f - x[e]) * (1.f - x[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += x[e] * x[e];
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+template <typename TA, bool FLAT>
+__global__ void __launch_bounds__(256) gan_reduce_grad_v8_kernel(int kind, const TA* __restrict__ a, int lda,
+                                                                 const TA* __restrict__ b, int ldb, int64_t rows,
+                                                                 int width, const float* __restrict__ scale,
+                                                                 TA* __restrict__ ga, int ldg) {
+  const RowMap rm{width / 8};
+  const int64_t nv = rows * rm.wv;
+  const float sc = *scale;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    int64_t oa = v * 8, ob = v * 8, og = v * 8;
+    if constexpr (!FLAT) {
+      int64_t r;
+      int c;
+      rm.at(v, &r, &c);
+      oa = r * lda + c;
+      ob = r * ldb + c;
+      og = r * ldg + c;
+    }
+    float x[8], g[8];
+    load8(a + oa, x);
+    if (kind == 0) {
+      float y[8];
+      load8(b + ob, y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = x[e] - y[e];
+        g[e] = d > 0.f ? sc : (d < 0.f ? -sc : 0.f);
+      }
+    } else if (kind == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = -2.f * (1.f - x[e]) * sc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = 2.f * x[e] * sc;
+    }
+    store8(ga + og, g);
+  }
+}
+
+template <typename TG, typename TR, bool FLAT>
+__global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict__ g, int ldg,
+                                                            const TR* __restrict__ ref, int ldr, int64_t rows,
+                                                            int width, float slope, TG* __restrict__ out, int ldo) {
+  const RowMap rm{width / 8};
+  const int64_t nv = rows * rm.wv;
+  for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
+    int64_t og = v * 8, orf = v * 8, oo = v * 8;
+    if constexpr (!FLAT) {
+      int64_t r;
+      int c;
+      rm.at(v, &r, &c);
+      og = r * ldg + c;
+      orf = r * ldr + c;
+      oo = r * ldo + c;
+    }
+    float x[8], q[8];
+    load8(g + og, x);
+    load8(ref + orf, q);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = q[e] > 0.f ? x[e] : x[e] * slope;
+    store8(out + oo, x);
+  }
+}
+
+static bool v8_ok(const void* p, int64_t ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % 8 == 0); }
+
 
 // leaky-ReLU backward mask: out = g * (ref > 0 ? 1 : slope) over a (rows x width) view with
 // leading dimensions (out may alias g).  ref = the activation's input or its output (same sign
@@ -246,13 +362,26 @@ extern "C" int vo_gan_reduce(int kind, const void* a, int lda, const void* b, in
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // at most 512 block partials (workspace: 512 floats), added in order by one wave (deterministic;
   // the grid-stride loop keeps the loads coalesced)
-  const int g = std::min(grid_for(rows * width), 512);
-  if (dtype == VO_BF16)
+  int g = std::min(grid_for(rows * width), 512);
+  if (width % 8 == 0 && v8_ok(a, lda) && v8_ok(b, ldb)) {
+    g = std::min(grid_for(rows * (width / 8)), 512);
+    const bool flat = lda == width && (!b || ldb == width);
+#define VO_GR(TA, F)                                                                                     \
+  hipLaunchKernelGGL((gan_reduce_v8_kernel<TA, F>), dim3(g), dim3(256), 0, st, kind, (const TA*)a, lda, \
+                     (const TA*)b, ldb, rows, width, workspace)
+    if (dtype == VO_BF16) {
+      if (flat) VO_GR(bf16_t, true); else VO_GR(bf16_t, false);
+    } else {
+      if (flat) VO_GR(float, true); else VO_GR(float, false);
+    }
+#undef VO_GR
+  } else if (dtype == VO_BF16) {
     hipLaunchKernelGGL(gan_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
                        (const bf16_t*)b, ldb, rows, width, workspace);
-  else
+  } else {
     hipLaunchKernelGGL(gan_reduce_kernel<float>, dim3(g), dim3(256), 0, st, kind, (const float*)a, lda,
                        (const float*)b, ldb, rows, width, workspace);
+  }
   hipLaunchKernelGGL(gan_reduce_final_kernel, dim3(1), dim3(64), 0, st, workspace, g, out);
   VO_RETURN_LAUNCH();
 }
@@ -262,6 +391,20 @@ extern "C" int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* 
   VO_CHECK_ARG(a && ga && scale && kind >= 0 && kind <= 2 && (kind != 0 || b), "gan_reduce_grad: bad arguments");
   VO_CHECK_ARG(rows > 0 && width > 0 && lda >= width && ldg >= width, "gan_reduce_grad: bad shape");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (width % 8 == 0 && v8_ok(a, lda) && v8_ok(b, ldb) && v8_ok(ga, ldg)) {
+    const int gv = grid_for(rows * (width / 8));
+    const bool flat = lda == width && (!b || ldb == width) && ldg == width;
+#define VO_GG(TA, F)                                                                                           \
+  hipLaunchKernelGGL((gan_reduce_grad_v8_kernel<TA, F>), dim3(gv), dim3(256), 0, st, kind, (const TA*)a, lda, \
+                     (const TA*)b, ldb, rows, width, scale, (TA*)ga, ldg)
+    if (dtype == VO_BF16) {
+      if (flat) VO_GG(bf16_t, true); else VO_GG(bf16_t, false);
+    } else {
+      if (flat) VO_GG(float, true); else VO_GG(float, false);
+    }
+#undef VO_GG
+    VO_RETURN_LAUNCH();
+  }
   const int g = grid_for(rows * width);
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(gan_reduce_grad_kernel<bf16_t>, dim3(g), dim3(256), 0, st, kind, (const bf16_t*)a, lda,
@@ -277,6 +420,29 @@ extern "C" int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* re
   VO_CHECK_ARG(g && ref && out, "lrelu_mask: null pointer");
   VO_CHECK_ARG(rows > 0 && width > 0 && ldg >= width && ldr >= width && ldo >= width, "lrelu_mask: bad shape");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (width % 8 == 0 && v8_ok(g, ldg) && v8_ok(ref, ldr) && v8_ok(out, ldo)) {
+    const int gv = grid_for(rows * (width / 8));
+    const bool flat = ldg == width && ldr == width && ldo == width;
+#define VO_LM8(TG, TR)                                                                                             \
+  do {                                                                                                             \
+    if (flat)                                                                                                      \
+      hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, true>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg,      \
+                         (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo);                                  \
+    else                                                                                                           \
+      hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, false>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg,     \
+                         (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo);                                  \
+  } while (0)
+    if (g_dtype == VO_BF16 && ref_dtype == VO_BF16) VO_LM8(bf16_t, bf16_t);
+    else if (g_dtype == VO_F32 && ref_dtype == VO_F32) VO_LM8(float, float);
+    else if (g_dtype == VO_BF16 && ref_dtype == VO_F32) VO_LM8(bf16_t, float);
+    else if (g_dtype == VO_F32 && ref_dtype == VO_BF16) VO_LM8(float, bf16_t);
+    else {
+      vo_set_error("lrelu_mask: bad dtypes");
+      return VO_ERR_INVALID;
+    }
+#undef VO_LM8
+    VO_RETURN_LAUNCH();
+  }
   const int gr = grid_for(rows * width);
 #define VO_LM(TG, TR)                                                                                          \
   hipLaunchKernelGGL((lrelu_mask_kernel<TG, TR>), dim3(gr), dim3(256), 0, st, (const TG*)g, ldg, (const TR*)ref, \
