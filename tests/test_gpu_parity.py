@@ -291,11 +291,12 @@ def test_conv1d_vs_torch_fp32(B, T, Ci, Co, K, dil, act, dt, tol):
     assert rel_l2(out.cpu(), ref) < tol
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 3])
 @pytest.mark.parametrize("B,T,C,K,dil", [(2, 1000, 256, 11, 5), (3, 300, 256, 3, 1), (1, 1, 256, 7, 3),
                                          (2, 4096, 256, 7, 3), (2, 517, 128, 11, 1)])
 def test_conv1d_mrf_stage0_tiles(B, T, C, K, dil, cfg):
-    """MRF stage-0 conv (variant 1: 256 x 256 tile, conv_cfg 1: 128 x 128) with lrelu prologue,
+    """MRF stage-0 conv (variant 1: 256 x 256 tile with LDS-DMA weights, conv_cfg 1: 128 x 128,
+    conv_cfg 3: register-staged weights) with lrelu prologue,
     residual and accumulate epilogue, against PyTorch fp32 at ragged T and Co < tile."""
     import torch.nn.functional as F
     from visual_onoma_to_wave_amd import _lib, ops

@@ -47,4 +47,4 @@ def main(cfgs=(0, 9)):
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(int(c) for c in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 9))

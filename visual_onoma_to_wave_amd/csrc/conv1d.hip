@@ -207,8 +207,27 @@ __device__ __forceinline__ void conv_partial_store(const ConvArgs& a, f32x4 (&ac
 // PRIO: s_setprio(1) around each MFMA cluster (keeps hipcc from moving the cluster across
 // the barriers; guide T5) -- A/B via conv_cfg.  ABL (timing ablation, garbage results):
 // 1 = no global loads in the main loop.
+// GL (bf16, NICE, stride 1): the weight taps are copied HBM / L2 -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave instruction, the XOR swizzle moved to the source
+// address as in the fused ResBlock kernels): no staging VGPRs and no ds_write for them.  The
+// next chunk's window is then fetched after the first step's DMA (so a step's vmcnt wait does not
+// drain it), which leaves it two steps instead of a whole chunk to arrive.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 8, "wait_vmcnt: 0..8");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0, int S = 1>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -291,8 +310,39 @@ conv1d_kernel(ConvArgs a) {
   }
 
   Raw8<TIN> win_r[MAXV];
-  Raw8<TC> w_r[WV];
-  bool win_ok[MAXV], w_ok[WV];
+  constexpr bool DMA = GL && NICE && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0;
+  constexpr int NW = NT / 64;
+  constexpr int GLN = DMA ? (TPS * BCO * VPR) / NT : 1;  // DMA instructions per wave per step
+  static_assert(!DMA || (TPS * BCO * VPR) % NT == 0, "conv1d GL: a step's weights must split into whole wave-KiB");
+  Raw8<TC> w_r[DMA ? 1 : WV];
+  bool win_ok[MAXV], w_ok[DMA ? 1 : WV];
+  int gl_t[GLN], gl_src[GLN];
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  if constexpr (DMA) {
+#pragma unroll
+    for (int s = 0; s < GLN; ++s) {
+      const int p = (s * NW + wave) * 64 + lane;  // LDS slot (16 B): tap t, row col, chunk q'
+      const int t = p / (BCO * VPR), rem = p - t * BCO * VPR;
+      const int col = rem / VPR, qs = rem - col * VPR;
+      const int q = qs ^ ((col >> (SHW - 1)) & 2);  // the swizzle of Lds<bf16_t>::off, on the source
+      gl_t[s] = t;
+      gl_src[s] = (co_blk + col) * a.Ci + q * 8;
+    }
+  }
+  auto load_w_dma = [&](int c, int k0, int buf) {
+    if constexpr (DMA) {
+      typedef __attribute__((address_space(3))) void lds_void;
+      typedef const __attribute__((address_space(1))) void g_void;
+      const int c0 = ci_lo + c * KC;
+#pragma unroll
+      for (int s = 0; s < GLN; ++s) {
+        const int k = min(k0 + gl_t[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
+        const TC* src = Wp + k * tap_stride + gl_src[s] + c0;
+        TC* dst = wt0 + buf * WSTRIDE + (s * NW + wave_u) * 64 * 8;
+        __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+      }
+    }
+  };
 
   auto load_window = [&](int c) {
     const int c0 = ci_lo + c * KC;
@@ -325,6 +375,7 @@ conv1d_kernel(ConvArgs a) {
     }
   };
   auto load_w = [&](int c, int k0) {
+    if constexpr (DMA) return;
     const int c0 = ci_lo + c * KC;
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
@@ -337,6 +388,7 @@ conv1d_kernel(ConvArgs a) {
     }
   };
   auto store_w = [&](int buf) {
+    if constexpr (DMA) return;
     TC* base = wt0 + buf * WSTRIDE;
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
@@ -363,8 +415,10 @@ conv1d_kernel(ConvArgs a) {
   // prologue
   load_window(0);
   load_w(0, 0);
+  load_w_dma(0, 0, 0);
   store_window(0);
   store_w(0);
+  if constexpr (DMA) wait_vmcnt<0>();
   __syncthreads();
 
   // One pipeline step = TPS taps of one 32-channel chunk c (weights in buffer s & 1).  The
@@ -398,19 +452,34 @@ conv1d_kernel(ConvArgs a) {
   int s = 0;
   for (int c = 0; c < n_chunks; ++c) {
     const bool more_chunks = c + 1 < n_chunks;
-    load_window(min(c + 1, n_chunks - 1));   // a whole chunk of MFMAs ahead of its use
+    if constexpr (!DMA) load_window(min(c + 1, n_chunks - 1));  // a whole chunk of MFMAs ahead of its use
     for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
       load_w(c, (tg + 1) * TPS);
+      if constexpr (DMA) {
+        load_w_dma(c, (tg + 1) * TPS, (s + 1) & 1);
+        if (tg == 0) load_window(min(c + 1, n_chunks - 1));  // issued after the DMA: in-order vmcnt
+      }
       mfma_step(c, tg, s);
       store_w((s + 1) & 1);
+      if constexpr (DMA) {  // this wave's DMA pieces landed (the window loads after them may not)
+        if (tg == 0)
+          wait_vmcnt<MAXV>();
+        else
+          wait_vmcnt<0>();
+      }
       __syncthreads();
     }
     load_w(min(c + 1, n_chunks - 1), 0);
+    if constexpr (DMA) {
+      load_w_dma(min(c + 1, n_chunks - 1), 0, (s + 1) & 1);
+      if (tsteps == 1) load_window(min(c + 1, n_chunks - 1));
+    }
     mfma_step(c, tsteps - 1, s);
     if (more_chunks) {
       store_w((s + 1) & 1);
       store_window((c + 1) & 1);
     }
+    if constexpr (DMA) wait_vmcnt<0>();
     __syncthreads();
     ++s;
   }
@@ -491,7 +560,7 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, int S = 1>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -520,7 +589,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
     return VO_ERR_INVALID;
   }
   const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S>
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL>
                    : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
   a.partial = nullptr;
   a.kcs = 0;
@@ -545,9 +614,9 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
 }
 
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0>
+          int PRIO = 0, int ABL = 0, bool GL = false>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
-  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1>(d, st);
+  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL>(d, st);
 }
 
 // HiFi-GAN discriminator layers (strided and/or grouped, C5): 64-row tiles so that a stride-4
@@ -688,9 +757,14 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
                  // twice the rows of the 128 x 128 tile: 0.095/0.151/0.208 -> 0.077/0.125/0.172 ms
                  // for k = 3/7/11 at B = 32, bit-identical).  conv_cfg 1 = the 128 x 128 tile.
         // s_setprio(1) around each MFMA cluster: +1-3 % (0.1667 -> 0.1654 ms at k = 11); conv_cfg 2 = without
+        // Round 2: weights by LDS-DMA (GL): 0.084 / 0.134 / 0.171 -> 0.083 / 0.126 / 0.163 ms for
+        // k = 3 / 7 / 11 alone (tools/ab_conv_cfg.py, bit-identical), within noise in the bench step;
+        // conv_cfg 3 = register-staged weights, 4 = GL with 3-tap steps (spills)
         if (vo_tune_get("conv_cfg") == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 2) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
-        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
+        if (vo_tune_get("conv_cfg") == 3) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
+        if (vo_tune_get("conv_cfg") == 4) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 3, 1, 1, 0, true>(d, st);
+        return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true>(d, st);
       }
       case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);
       case 3: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 1, 4, 4, 3>(d, st);

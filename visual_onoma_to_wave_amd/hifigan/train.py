@@ -19,7 +19,7 @@ import itertools
 import torch
 
 from .. import _base
-from ..train import GradBucketer, TrainState, _check_graph_runtime
+from ..train import GradBucketer, TrainState, _check_graph_runtime, quiesce_collectives
 from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiScaleDiscriminator, discriminator_loss,
                              feature_loss, generator_loss)
 
@@ -153,6 +153,8 @@ class HifiGanTrainer:
                 for _ in range(warmup):
                     self.step(self._x, self._y)
             torch.cuda.current_stream().wait_stream(side)
+            if self.bk_g is not None:
+                quiesce_collectives()
             gan_ops.reset_pack_cache()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):

@@ -30,6 +30,7 @@ call); ``GraphedTrainStep`` refuses to run when it is not in effect.
 """
 
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -215,6 +216,18 @@ class TrainState:
                             v.zero_()
 
 
+def quiesce_collectives(seconds=0.5):
+    """Before a capture that contains RCCL collectives: wait for the device, then give the
+    process group's watchdog thread (it polls its list of in-flight works every ~100 ms) time to
+    retire the warm-up steps' collectives.  An eager work still listed when the capture starts has
+    its end event on the communicator's stream, which the capture then joins; the watchdog's
+    event query on it fails ("operation not permitted on an event last recorded in a capturing
+    stream") and aborts the process -- a race we met once in the world-size-1 RCCL test."""
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        torch.cuda.synchronize()
+        time.sleep(seconds)
+
+
 def _check_graph_runtime():
     if not packet_capture_disabled():
         raise RuntimeError(
@@ -263,6 +276,8 @@ class GraphedTrainStep:
                 self.opt._update_learning_rate()
                 self._body(self.static)
         torch.cuda.current_stream().wait_stream(side)
+        if self.bucketer is not None:
+            quiesce_collectives()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = self._body(self.static)
