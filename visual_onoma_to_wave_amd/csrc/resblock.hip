@@ -584,7 +584,12 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // L2 / MALL prefetch of the epilogue's bytes (next window, residual, accumulator) by LDS-DMA
     // pieces into a trash row during P2: +8 % with 1 KiB pieces (1-4 per wave per group: +8..18 %),
     // +7 % with 8 KiB one-dword-per-line pieces (26 per tile) -- the piece issue costs more than
-    // the exposed loads it shortens
+    // the exposed loads it shortens; and a kernel with the weights out of LDS altogether (each
+    // wave's A fragments loaded from global one tap ahead into a register ring, no per-tap barrier,
+    // the freed LDS double-buffering the window, filled between taps): bit-identical but +20 %
+    // (k = 11: 0.69 -> 0.83 ms; MFMA busy 46.5 -> 38.6 %, waits on the fragment loads 56 % of wave
+    // cycles -- one tap of prefetch does not cover the L1 / L2 latency of 64 KiB of fragment loads
+    // per tap per CU, and a deeper ring does not fit the registers)
     if (cfg == 9) {  // the previous defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
