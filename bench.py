@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="infer: run acoustic model and vocoder back to back instead of overlapping the acoustic "
                          "model of batch i+1 (own stream) with the vocoder of batch i")
+    ap.add_argument("--stft-loss", type=float, default=0.0,
+                    help="gan: weight of the auxiliary multi-resolution STFT loss (0 = HiFi-GAN V1 losses only)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="train / gan under torchrun: gradient all-reduce dtype")
     ap.add_argument("--mode", default="infer", choices=["infer", "c2", "c3", "train", "gan"],
@@ -349,7 +351,8 @@ def bench_gan(a, dev, rank, world, dist):
     torch.manual_seed(1234)  # identical discriminator init on every rank (broadcast anyway)
     graphed = not a.no_graph
     tr = hifigan.HifiGanTrainer(g, h, distributed=dist is not None, device=dev, graphed=graphed,
-                                comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None)
+                                comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None,
+                                stft_loss_weight=a.stft_loss)
     run = tr.step_graphed if graphed else tr.step
     tr.set_compute_dtype(torch.float32 if a.precision == "fp32" else torch.bfloat16)
     B, seg = a.batch, h.segment_size
@@ -373,7 +376,9 @@ def bench_gan(a, dev, rank, world, dist):
             "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
             "losses": {k: round(float(v), 4) for k, v in losses.items()},
             "hip_graph": graphed,
-            "config": {"workload": "C5 HiFi-GAN V1 train step", "per_gpu_batch": B, "global_batch": B * world,
+            "config": {"workload": "C5 HiFi-GAN V1 train step" + (
+                           f" + {a.stft_loss} x multi-resolution STFT loss" if a.stft_loss else ""),
+                       "per_gpu_batch": B, "global_batch": B * world,
                        "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D, {a.comm_dtype})"}}))
 
 

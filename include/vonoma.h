@@ -392,6 +392,25 @@ int vo_stft_mel_bwd(const float* wav, int B, int N, const float* window, const f
                     int n_mels, int pad, float mag_eps, float log_floor, const float* gmel, float* dwav,
                     float* workspace, void* stream);
 
+/* Multi-resolution STFT loss (the auxiliary spectral loss of BASELINE.json config C5; Parallel
+ * WaveGAN's formulation: per resolution spectral convergence ||Y - X||_F / ||Y||_F and mean
+ * |log Y - log X| over STFT magnitudes).  vo_stft_mag: torch.stft(center=True, reflect padding
+ * n_fft / 2, onesided) of wav (B, N) fp32 with `window` (n_fft samples: the win_len window zero-
+ * padded to n_fft, centred, as torch.stft pads it) -> mag (B, 1 + N / hop, n_fft / 2 + 1) =
+ * sqrt(max(|X|^2, eps)); vo_stft_mag_bwd: gmag -> dwav (written; workspace
+ * vo_stft_mag_bwd_workspace_size bytes; deterministic gather as vo_stft_mel_bwd).
+ * vo_stft_loss: out[3] = (sum (y - x)^2, sum y^2, sum |log y - log x|) over n magnitudes
+ * (workspace >= 1536 floats); vo_stft_loss_grad: gx = d(w[0] sqrt(out0 / out1) + w[1] out2 / n)/dx with
+ * the weights w[2] (the incoming loss gradients) read on the device. */
+int vo_stft_mag(const float* wav, int B, int N, const float* window, int n_fft, int hop, float eps, float* mag,
+                void* stream);
+int64_t vo_stft_mag_bwd_workspace_size(int B, int N, int n_fft, int hop);
+int vo_stft_mag_bwd(const float* wav, int B, int N, const float* window, int n_fft, int hop, float eps,
+                    const float* gmag, float* dwav, float* workspace, void* stream);
+int vo_stft_loss(const float* xm, const float* ym, int64_t n, float* out, float* workspace, void* stream);
+int vo_stft_loss_grad(const float* xm, const float* ym, int64_t n, const float* sums, const float* w, float* gx,
+                      void* stream);
+
 /* ------------------------------------------------------------------ training input pipeline
  * Glyph batch: B grayscale strips packed in px (strip b at img_off[b],
  * H rows of img_w[b] uint8 columns) -> out (B, 1, H, W_out) fp32 = pixel / 255 with each

@@ -16,6 +16,12 @@ over effective (weight-norm / spectral-norm resolved) weights, in the reference 
 * losses: feature 2*sum mean|r-g|, discriminator sum mean((1-r)^2) + mean(g^2), generator
   sum mean((1-g)^2); mel L1 on the training mel (reflect pad (n_fft-hop)/2, center=False,
   periodic Hann, sqrt(|X|^2 + 1e-9), librosa slaney mel to sr/2, log clamp 1e-5) x 45.
+* multi_resolution_stft_loss(): the auxiliary loss BASELINE.json's config C5 names ("multi-res
+  STFT loss"), restated from Parallel WaveGAN (Yamamoto et al. 2020, section 2.3, eq. 4-6):
+  per (n_fft, hop, win) in ((1024, 120, 600), (2048, 240, 1200), (512, 50, 240)) the magnitude
+  |torch.stft(center=True, reflect, hann(win) zero-padded to n_fft)| with sqrt(clamp(|X|^2,
+  1e-7)), spectral convergence ||Y - X||_F / ||Y||_F and mean |log Y - log X|, each averaged
+  over the resolutions.  Parity unpinned (no reference code).
 """
 
 import torch
@@ -122,3 +128,25 @@ def gan_losses(mpd_params, msd_params, y, y_hat, y_mel):
     fm = feature_loss(fr1, fg1) + feature_loss(fr2, fg2)
     adv = generator_loss(sg1) + generator_loss(sg2)
     return loss_disc, adv + fm + mel, dict(mel=mel, fm=fm, adv=adv)
+
+
+STFT_RESOLUTIONS = ((1024, 120, 600), (2048, 240, 1200), (512, 50, 240))
+
+
+def stft_mag(x, n_fft, hop, win):
+    """|STFT| (B, frames, n_fft / 2 + 1) of x (B, N): center=True reflect padding, a hann(win)
+    window zero-padded to n_fft (torch.stft's own placement), sqrt(clamp(|X|^2, 1e-7))."""
+    window = torch.hann_window(win, dtype=x.dtype)
+    spec = torch.stft(x, n_fft, hop_length=hop, win_length=win, window=window, center=True, pad_mode="reflect",
+                      return_complex=True)
+    return torch.sqrt(torch.clamp(spec.real ** 2 + spec.imag ** 2, min=1e-7)).transpose(1, 2)
+
+
+def multi_resolution_stft_loss(x, y, resolutions=STFT_RESOLUTIONS):
+    """(spectral convergence, log-magnitude L1) of x against y, averaged over the resolutions."""
+    sc = mag = 0.0
+    for n_fft, hop, win in resolutions:
+        xm, ym = stft_mag(x, n_fft, hop, win), stft_mag(y, n_fft, hop, win)
+        sc = sc + torch.norm(ym - xm, p="fro") / torch.norm(ym, p="fro")
+        mag = mag + F.l1_loss(torch.log(ym), torch.log(xm))
+    return sc / len(resolutions), mag / len(resolutions)

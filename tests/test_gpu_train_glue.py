@@ -174,3 +174,49 @@ def test_disc_input_adjoints(T, dtype):
     assert y.shape == yr.shape
     y.backward(gp.float().cuda())
     assert rel_l2(wg.grad.cpu(), wr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("n_fft,hop,win", [(1024, 120, 600), (2048, 240, 1200), (512, 50, 240)])
+def test_stft_mag_fwd_bwd(n_fft, hop, win):
+    """vo_stft_mag / vo_stft_mag_bwd (StftMagFn) against torch.stft autograd in fp64."""
+    from oracle import gan as G
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as GO
+    g = torch.Generator().manual_seed(n_fft + hop)
+    x = (torch.rand(2, 8192, generator=g, dtype=torch.float64) * 2 - 1) * 0.5
+    xr = x.clone().requires_grad_(True)
+    mr = G.stft_mag(xr, n_fft, hop, win)
+    gm = torch.randn(mr.shape, generator=g, dtype=torch.float64)
+    (mr * gm).sum().backward()
+    window = torch.zeros(n_fft, dtype=torch.float64)
+    window[(n_fft - win) // 2: (n_fft - win) // 2 + win] = torch.hann_window(win, dtype=torch.float64)
+    xg = x.float().cuda().requires_grad_(True)
+    m = GO.StftMagFn.apply(xg, window.float().cuda(), n_fft, hop)
+    m.backward(gm.float().cuda())
+    e_f, e_b = rel_l2(m.detach().cpu(), mr.detach()), rel_l2(xg.grad.cpu(), xr.grad)
+    print((n_fft, hop, win), f"fwd {e_f:.1e} bwd {e_b:.1e}")
+    assert m.shape == mr.shape and e_f < 1e-5 and e_b < 1e-4
+
+
+def test_multi_resolution_stft_loss_vs_oracle():
+    """MultiResolutionSTFTLoss (HIP magnitudes, reductions and gradients) against
+    oracle.gan.multi_resolution_stft_loss autograd in fp64: both loss terms and d/dwav_hat."""
+    from oracle import gan as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MultiResolutionSTFTLoss
+    g = torch.Generator().manual_seed(3)
+    y = (torch.rand(3, 8192, generator=g, dtype=torch.float64) * 2 - 1) * 0.5
+    x = y + 0.1 * torch.randn(3, 8192, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    sc_r, mag_r = G.multi_resolution_stft_loss(xr, y)
+    (sc_r + 0.5 * mag_r).backward()
+    loss = MultiResolutionSTFTLoss().cuda()
+    xg = x.float().cuda().requires_grad_(True)
+    sc, mag = loss(xg, y.float().cuda())
+    (sc + 0.5 * mag).backward()
+    print(f"sc {float(sc):.6f} vs {float(sc_r):.6f}, mag {float(mag):.6f} vs {float(mag_r):.6f}, "
+          f"grad {rel_l2(xg.grad.cpu(), xr.grad):.1e}")
+    assert abs(float(sc) - float(sc_r)) < 1e-5 * max(1.0, float(sc_r))
+    assert abs(float(mag) - float(mag_r)) < 1e-5 * max(1.0, float(mag_r))
+    assert rel_l2(xg.grad.cpu(), xr.grad) < 1e-4
+    # deterministic: the same call again gives the same bits
+    sc2, mag2 = loss(xg.detach(), y.float().cuda())
+    assert torch.equal(sc2, sc.detach()) and torch.equal(mag2, mag.detach())

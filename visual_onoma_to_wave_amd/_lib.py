@@ -143,6 +143,12 @@ _SIGNATURES = {
     "vo_stft_mel_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "vo_stft_mel_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                 c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_stft_mag": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p]),
+    "vo_stft_mag_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int, c_int]),
+    "vo_stft_mag_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
+                                c_void_p, c_void_p]),
+    "vo_stft_loss": (c_int, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
+    "vo_stft_loss_grad": (c_int, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_glyph_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                c_int, c_int, c_void_p, c_void_p]),
 }

@@ -353,6 +353,123 @@ __global__ void __launch_bounds__(256) stft_mel_bwd_gather_kernel(const float* _
   dwav[(int64_t)b * N + i] = s;
 }
 
+// ------------------------------------------------------------------------------- STFT magnitude
+// torch.stft(center=True, reflect pad n_fft / 2, onesided) of a window zero-padded to n_fft, and
+// mag = sqrt(max(|X|^2, eps)): the multi-resolution STFT loss of Parallel WaveGAN-style vocoder
+// training.  One workgroup per (frame, utterance); mag laid out (B, F, n_fft / 2 + 1).
+__global__ void __launch_bounds__(256) stft_mag_kernel(const float* __restrict__ wav, int N, int F,
+                                                       const float* __restrict__ window, int n_fft, int hop,
+                                                       float eps, float* __restrict__ mag) {
+  __shared__ float2 buf[2][SMB_MAX_N];
+  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int n = n_fft, half = n / 2;
+  const float* x = wav + (int64_t)b * N;
+  const int start = f * hop - half;
+  for (int m = tid; m < n; m += 256) buf[0][m] = make_float2(x[reflect_idx(start + m, N)] * window[m], 0.f);
+  __syncthreads();
+  const int s = fft_stockham(buf, n, -1.f, tid, 256);
+  float* out = mag + ((int64_t)b * F + f) * (half + 1);
+  for (int k = tid; k <= half; k += 256) {
+    const float2 z = buf[s][k];
+    out[k] = sqrtf(fmaxf(z.x * z.x + z.y * z.y, eps));
+  }
+}
+
+// frame gradient of the magnitude: dX = gmag X / |X| where |X|^2 > eps (the clamp passes no
+// gradient below it), zero above n / 2; the inverse DFT's real part times the window
+__global__ void __launch_bounds__(256) stft_mag_bwd_frame_kernel(const float* __restrict__ wav, int N, int F,
+                                                                 const float* __restrict__ window, int n_fft,
+                                                                 int hop, float eps, const float* __restrict__ gmag,
+                                                                 float* __restrict__ gframe) {
+  __shared__ float2 buf[2][SMB_MAX_N];
+  const int f = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int n = n_fft, half = n / 2;
+  const float* x = wav + (int64_t)b * N;
+  const int start = f * hop - half;
+  for (int m = tid; m < n; m += 256) buf[0][m] = make_float2(x[reflect_idx(start + m, N)] * window[m], 0.f);
+  __syncthreads();
+  int s = fft_stockham(buf, n, -1.f, tid, 256);
+  const float* gm = gmag + ((int64_t)b * F + f) * (half + 1);
+  float2 d[SMB_MAX_N / 256];
+#pragma unroll
+  for (int u = 0; u < SMB_MAX_N / 256; ++u) {
+    const int k = tid + u * 256;
+    d[u] = make_float2(0.f, 0.f);
+    if (k <= half) {
+      const float2 z = buf[s][k];
+      const float p = z.x * z.x + z.y * z.y;
+      const float sc = p > eps ? gm[k] * rsqrtf(p) : 0.f;
+      d[u] = make_float2(sc * z.x, sc * z.y);
+    }
+  }
+  __syncthreads();  // every spectrum read done before the buffer is reused
+#pragma unroll
+  for (int u = 0; u < SMB_MAX_N / 256; ++u) {
+    const int k = tid + u * 256;
+    if (k < n) buf[0][k] = d[u];
+  }
+  __syncthreads();
+  s = fft_stockham(buf, n, 1.f, tid, 256);
+  float* out = gframe + ((int64_t)b * F + f) * n;
+  for (int m = tid; m < n; m += 256) out[m] = buf[s][m].x * window[m];
+}
+
+// multi-resolution STFT loss terms of one resolution over n magnitudes (x = generated, y =
+// target): part[block] = (sum (y - x)^2, sum y^2, sum |log y - log x|); one wave adds the block
+// partials in order into out[0..3)
+__global__ void __launch_bounds__(256) stft_loss_reduce_kernel(const float* __restrict__ xm,
+                                                               const float* __restrict__ ym, int64_t n,
+                                                               float* __restrict__ part) {
+  __shared__ float red[3][4];
+  float a = 0.f, c = 0.f, l = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float x = xm[i], y = ym[i];
+    a += (y - x) * (y - x);
+    c += y * y;
+    l += fabsf(__logf(y) - __logf(x));
+  }
+  a = wave_sum(a);
+  c = wave_sum(c);
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = c;
+    red[2][threadIdx.x >> 6] = l;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float* r = red[threadIdx.x];
+    part[(int64_t)blockIdx.x * 3 + threadIdx.x] = r[0] + r[1] + r[2] + r[3];
+  }
+}
+
+__global__ void __launch_bounds__(64) stft_loss_final_kernel(const float* __restrict__ part, int nb,
+                                                             float* __restrict__ out) {
+  for (int k = 0; k < 3; ++k) {
+    float v = 0.f;
+    for (int i = threadIdx.x; i < nb; i += 64) v += part[(int64_t)i * 3 + k];
+    v = wave_sum(v);
+    if (threadIdx.x == 0) out[k] = v;
+  }
+}
+
+// d/dx of w_sc * sqrt(A) / sqrt(C) + w_mag * L / n, A / C / L the sums above:
+//   w_sc (x - y) / (sqrt(A) sqrt(C)) + w_mag sign(log x - log y) / (n x)
+__global__ void __launch_bounds__(256) stft_loss_grad_kernel(const float* __restrict__ xm,
+                                                             const float* __restrict__ ym, int64_t n,
+                                                             const float* __restrict__ sums,
+                                                             const float* __restrict__ w, float* __restrict__ gx) {
+  const float w_sc = w[0], w_mag = w[1];  // device scalars: the incoming loss gradients (graph-safe)
+  const float sa = sqrtf(sums[0]), sc = sqrtf(sums[1]);
+  const float k_sc = sa > 0.f && sc > 0.f ? w_sc / (sa * sc) : 0.f;
+  const float k_mag = w_mag / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float x = xm[i], y = ym[i];
+    const float dl = __logf(x) - __logf(y);
+    gx[i] = k_sc * (x - y) + (dl > 0.f ? k_mag : (dl < 0.f ? -k_mag : 0.f)) / x;
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -486,5 +603,55 @@ extern "C" int vo_stft_mel_bwd(const float* wav, int B, int N, const float* wind
                      fb, n_fft, hop, n_mels, pad, mag_eps, log_floor, gmel, workspace);
   hipLaunchKernelGGL(stft_mel_bwd_gather_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, st,
                      workspace, N, F, n_fft, hop, pad, dwav);
+  VO_RETURN_LAUNCH();
+}
+
+// ---- STFT magnitude (multi-resolution STFT loss): wav (B, N) -> mag (B, 1 + N / hop, n_fft / 2 + 1)
+extern "C" int vo_stft_mag(const float* wav, int B, int N, const float* window, int n_fft, int hop, float eps,
+                           float* mag, void* stream) {
+  VO_CHECK_ARG(wav && window && mag, "stft_mag: null pointer");
+  VO_CHECK_ARG(n_fft >= 8 && n_fft <= SMB_MAX_N && (n_fft & (n_fft - 1)) == 0, "stft_mag: n_fft=%d", n_fft);
+  VO_CHECK_ARG(B > 0 && hop > 0 && N > n_fft / 2, "stft_mag: bad sizes (reflect padding needs N > n_fft / 2)");
+  const int F = 1 + N / hop;
+  hipLaunchKernelGGL(stft_mag_kernel, dim3((unsigned)F, (unsigned)B), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), wav, N, F, window, n_fft, hop, eps, mag);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int64_t vo_stft_mag_bwd_workspace_size(int B, int N, int n_fft, int hop) {
+  const int64_t F = 1 + N / hop;
+  return (int64_t)B * F * n_fft * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_stft_mag_bwd(const float* wav, int B, int N, const float* window, int n_fft, int hop, float eps,
+                               const float* gmag, float* dwav, float* workspace, void* stream) {
+  VO_CHECK_ARG(wav && window && gmag && dwav && workspace, "stft_mag_bwd: null pointer");
+  VO_CHECK_ARG(n_fft >= 8 && n_fft <= SMB_MAX_N && (n_fft & (n_fft - 1)) == 0, "stft_mag_bwd: n_fft=%d", n_fft);
+  VO_CHECK_ARG(B > 0 && hop > 0 && N > n_fft / 2, "stft_mag_bwd: bad sizes");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int F = 1 + N / hop;
+  hipLaunchKernelGGL(stft_mag_bwd_frame_kernel, dim3((unsigned)F, (unsigned)B), dim3(256), 0, st, wav, N, F, window,
+                     n_fft, hop, eps, gmag, workspace);
+  hipLaunchKernelGGL(stft_mel_bwd_gather_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, st,
+                     workspace, N, F, n_fft, hop, n_fft / 2, dwav);
+  VO_RETURN_LAUNCH();
+}
+
+// ---- one resolution's loss sums: out[3] = (sum (y-x)^2, sum y^2, sum |log y - log x|); workspace >= 3 * 512 floats
+extern "C" int vo_stft_loss(const float* xm, const float* ym, int64_t n, float* out, float* workspace, void* stream) {
+  VO_CHECK_ARG(xm && ym && out && workspace && n > 0, "stft_loss: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nb = (int)std::min<int64_t>((n + 255) / 256, 512);
+  hipLaunchKernelGGL(stft_loss_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, st, xm, ym, n, workspace);
+  hipLaunchKernelGGL(stft_loss_final_kernel, dim3(1), dim3(64), 0, st, workspace, nb, out);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_stft_loss_grad(const float* xm, const float* ym, int64_t n, const float* sums, const float* w,
+                                 float* gx, void* stream) {
+  VO_CHECK_ARG(xm && ym && sums && w && gx && n > 0, "stft_loss_grad: bad arguments");
+  const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(stft_loss_grad_kernel, dim3(nb), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xm, ym, n,
+                     sums, w, gx);
   VO_RETURN_LAUNCH();
 }

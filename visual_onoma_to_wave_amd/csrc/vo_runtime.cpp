@@ -89,7 +89,8 @@ static const char* const kSymbols[] = {
     "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask", "vo_conv1d_workspace_size",
     "vo_bn_workspace_size", "vo_bn_train_fwd", "vo_bn_bwd", "vo_vfe_conv_workspace_size", "vo_vfe_conv_fwd",
     "vo_vfe_conv_bwd", "vo_stft_mel_bwd_workspace_size", "vo_stft_mel_bwd", "vo_period_fold_bwd", "vo_wav_cl8_bwd",
-    "vo_avgpool_wav_bwd", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size",
+    "vo_avgpool_wav_bwd", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size", "vo_stft_mag",
+    "vo_stft_mag_bwd_workspace_size", "vo_stft_mag_bwd", "vo_stft_loss", "vo_stft_loss_grad",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

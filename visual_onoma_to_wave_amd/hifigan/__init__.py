@@ -12,7 +12,8 @@ class AttrDict(dict):
 def __getattr__(name):
     # training-side modules (config C5) load on first use
     if name in ("MultiPeriodDiscriminator", "MultiScaleDiscriminator", "DiscriminatorP", "DiscriminatorS",
-                "feature_loss", "discriminator_loss", "generator_loss", "MelLoss"):
+                "feature_loss", "discriminator_loss", "generator_loss", "MelLoss",
+                "MultiResolutionSTFTLoss"):
         from . import discriminators
         return getattr(discriminators, name)
     if name == "HifiGanTrainer":

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn import Conv1d, Conv2d
 
+from .. import ops
 from . import gan_ops as G
 
 LRELU_SLOPE = 0.1
@@ -224,3 +225,32 @@ class MelLoss(nn.Module):
 
     def forward(self, wav_hat, mel_target):
         return G.l1_mean(self.mel(wav_hat), mel_target)
+
+
+class MultiResolutionSTFTLoss(nn.Module):
+    """Auxiliary multi-resolution STFT loss (BASELINE.json config C5; Parallel WaveGAN,
+    Yamamoto et al. 2020): per resolution (n_fft, hop, win) the spectral convergence and the mean
+    log-magnitude L1 of |STFT| (hann window of win samples zero-padded to n_fft, center=True),
+    each averaged over the resolutions.  Forward, backward and reductions on HIP."""
+
+    def __init__(self, fft_sizes=(1024, 2048, 512), hop_sizes=(120, 240, 50), win_lengths=(600, 1200, 240)):
+        super().__init__()
+        self.res = list(zip(fft_sizes, hop_sizes, win_lengths))
+        for i, (n, _, w) in enumerate(self.res):
+            win = torch.zeros(n)
+            left = (n - w) // 2
+            win[left: left + w] = torch.hann_window(w)
+            self.register_buffer(f"window{i}", win, persistent=False)
+
+    def forward(self, wav_hat, wav):
+        """(sc, mag) of wav_hat (B, N) against wav (B, N)."""
+        sc = mag = 0.0
+        for i, (n, hop, _) in enumerate(self.res):
+            window = getattr(self, f"window{i}")
+            xm = G.StftMagFn.apply(wav_hat, window, n, hop)
+            with torch.no_grad():
+                ym = ops.stft_mag(wav.contiguous(), window, n, hop)
+            s, m = G.StftLossFn.apply(xm, ym)
+            sc = sc + s
+            mag = mag + m
+        return sc / len(self.res), mag / len(self.res)

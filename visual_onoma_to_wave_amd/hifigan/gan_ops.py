@@ -385,3 +385,38 @@ class MelFn(torch.autograd.Function):
         n_fft, hop = ctx.cfg
         return (ops.stft_mel_bwd(wav.contiguous(), window, fb, g.float().contiguous(), n_fft=n_fft, hop=hop,
                                  pad=(n_fft - hop) // 2, mag_eps=1e-9), None, None, None, None)
+
+
+class StftMagFn(torch.autograd.Function):
+    """|STFT| (center, reflect, onesided; sqrt(max(|X|^2, eps))) of wav (B, N) -> (B, F, bins)."""
+
+    @staticmethod
+    def forward(ctx, wav, window, n_fft, hop):
+        wav = wav.contiguous()
+        ctx.save_for_backward(wav, window)
+        ctx.cfg = (n_fft, hop)
+        return ops.stft_mag(wav, window, n_fft, hop)
+
+    @staticmethod
+    def backward(ctx, g):
+        wav, window = ctx.saved_tensors
+        n_fft, hop = ctx.cfg
+        return ops.stft_mag_bwd(wav, window, g.float().contiguous(), n_fft, hop), None, None, None
+
+
+class StftLossFn(torch.autograd.Function):
+    """One resolution of the multi-resolution STFT loss: (spectral convergence ||y - x||_F / ||y||_F,
+    mean |log y - log x|) of magnitudes x (differentiable) and y (target)."""
+
+    @staticmethod
+    def forward(ctx, xm, ym):
+        sums = ops.stft_loss_sums(xm, ym)
+        ctx.save_for_backward(xm, ym, sums)
+        return torch.sqrt(sums[0] / sums[1]), sums[2] / xm.numel()
+
+    @staticmethod
+    def backward(ctx, g_sc, g_mag):
+        xm, ym, sums = ctx.saved_tensors
+        w = torch.stack([g_sc if g_sc is not None else sums.new_zeros(()),
+                         g_mag if g_mag is not None else sums.new_zeros(())])
+        return ops.stft_loss_grad(xm, ym, sums, w), None

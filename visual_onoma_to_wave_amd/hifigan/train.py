@@ -6,6 +6,8 @@ null); the step follows the HiFi-GAN V1 recipe that config belongs to:
 
   D step: L_D = sum_{MPD, MSD} [mean((1 - D(y))^2) + mean(D(G(x).detach())^2)]
   G step: L_G = sum adv mean((1 - D(G(x)))^2) + 2 sum_l mean|D_l(y) - D_l(G(x))| + 45 L1(mel)
+          [+ stft_loss_weight (spectral convergence + log |STFT| L1) of the multi-resolution STFT
+           loss (BASELINE.json config C5's "multi-res STFT loss"; off by default = HiFi-GAN V1)]
 
 Multi-GPU: one process per GPU; generator and discriminator gradients are averaged by two
 bucketed RCCL all-reduces (``train.GradBucketer``) launched from backward hooks, so each
@@ -20,8 +22,8 @@ import torch
 
 from .. import _base
 from ..train import GradBucketer, TrainState, _check_graph_runtime, quiesce_collectives
-from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiScaleDiscriminator, discriminator_loss,
-                             feature_loss, generator_loss)
+from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiResolutionSTFTLoss, MultiScaleDiscriminator,
+                             discriminator_loss, feature_loss, generator_loss)
 
 
 def _single(disc, wav, grad):
@@ -49,7 +51,7 @@ class HifiGanTrainer:
     decay is written into the captured step without re-capturing."""
 
     def __init__(self, generator, h, mpd=None, msd=None, distributed=False, device=None, graphed=False,
-                 comm_dtype=None, capturable=None):
+                 comm_dtype=None, capturable=None, stft_loss_weight=0.0):
         self.generator = generator
         device = device or next(generator.parameters()).device
         self.mpd = (mpd or MultiPeriodDiscriminator()).to(device)
@@ -73,6 +75,8 @@ class HifiGanTrainer:
         self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
         self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,
                                 h.fmax_for_loss).to(device)
+        self.stft_loss_weight = float(stft_loss_weight)
+        self.stft_loss = MultiResolutionSTFTLoss().to(device) if self.stft_loss_weight else None
         self.bk_g = self.bk_d = None
         if distributed:
             self.bk_g = GradBucketer(list(generator.parameters()), comm_dtype=comm_dtype)
@@ -127,6 +131,12 @@ class HifiGanTrainer:
         loss_fm = feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
         loss_adv = generator_loss(g_f)[0] + generator_loss(g_s)[0]
         loss_gen_all = loss_adv + loss_fm + loss_mel
+        extra = {}
+        if self.stft_loss is not None:
+            sc, mag = self.stft_loss(y_g_hat, y)
+            loss_stft = (sc + mag) * self.stft_loss_weight
+            loss_gen_all = loss_gen_all + loss_stft
+            extra["stft"] = loss_stft.detach()
         loss_gen_all.backward()
         if self.bk_g is not None:
             self.bk_g.finish()
@@ -134,7 +144,7 @@ class HifiGanTrainer:
         for p in self._d_params():
             p.requires_grad_(True)
         return dict(disc=loss_disc_all.detach(), gen=loss_gen_all.detach(), mel=loss_mel.detach(),
-                    fm=loss_fm.detach(), adv=loss_adv.detach())
+                    fm=loss_fm.detach(), adv=loss_adv.detach(), **extra)
 
     def step_graphed(self, x_mel_cl, y, warmup=3):
         """``step`` as one HIP-graph replay (captured on the first call, after ``warmup`` eager

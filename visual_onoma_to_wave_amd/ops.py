@@ -491,6 +491,57 @@ def stft_mel_bwd(wav, window, fb, gmel, n_fft=1024, hop=256, pad=None, mag_eps=1
     return dwav
 
 
+def stft_mag(wav, window, n_fft, hop, eps=1e-7):
+    """torch.stft(center=True, reflect, onesided) magnitude sqrt(max(|X|^2, eps)) of wav (B, N) fp32
+    with ``window`` zero-padded to n_fft -> (B, 1 + N // hop, n_fft // 2 + 1)."""
+    _contig(wav, "wav")
+    B, N = wav.shape
+    if window.numel() != n_fft:
+        raise ValueError("stft_mag: window must be zero-padded to n_fft")
+    mag = torch.empty((B, 1 + N // hop, n_fft // 2 + 1), dtype=torch.float32, device=wav.device)
+    _lib.check(_lib.lib().vo_stft_mag(_ptr(wav), B, N, _ptr(window), n_fft, hop, float(eps), _ptr(mag), _stream(wav)),
+               "vo_stft_mag")
+    return mag
+
+
+def stft_mag_bwd(wav, window, gmag, n_fft, hop, eps=1e-7):
+    """Backward of ``stft_mag``: gmag (B, F, bins) -> dL/dwav (B, N) fp32."""
+    _contig(wav, "wav")
+    _contig(gmag, "gmag")
+    B, N = wav.shape
+    if gmag.shape != (B, 1 + N // hop, n_fft // 2 + 1):
+        raise ValueError("stft_mag_bwd: gmag shape")
+    L = _lib.lib()
+    dwav = torch.empty_like(wav)
+    ws = torch.empty(int(L.vo_stft_mag_bwd_workspace_size(B, N, n_fft, hop)) // 4, dtype=torch.float32,
+                     device=wav.device)
+    _lib.check(L.vo_stft_mag_bwd(_ptr(wav), B, N, _ptr(window), n_fft, hop, float(eps), _ptr(gmag), _ptr(dwav),
+                                 _ptr(ws), _stream(wav)), "vo_stft_mag_bwd")
+    return dwav
+
+
+def stft_loss_sums(xm, ym):
+    """(sum (y - x)^2, sum y^2, sum |log y - log x|) over two magnitude tensors -> fp32 (3,)."""
+    _contig(xm, "xm")
+    _contig(ym, "ym")
+    if xm.shape != ym.shape:
+        raise ValueError("stft_loss_sums: shape mismatch")
+    out = torch.empty(3, dtype=torch.float32, device=xm.device)
+    ws = torch.empty(3 * 512, dtype=torch.float32, device=xm.device)
+    _lib.check(_lib.lib().vo_stft_loss(_ptr(xm), _ptr(ym), xm.numel(), _ptr(out), _ptr(ws), _stream(xm)),
+               "vo_stft_loss")
+    return out
+
+
+def stft_loss_grad(xm, ym, sums, w):
+    """d(w[0] * spectral convergence + w[1] * log-magnitude L1)/dxm; w: fp32 (2,) on the device."""
+    w = w.float().contiguous()
+    gx = torch.empty_like(xm)
+    _lib.check(_lib.lib().vo_stft_loss_grad(_ptr(xm), _ptr(ym), xm.numel(), _ptr(sums), _ptr(w), _ptr(gx),
+                                            _stream(xm)), "vo_stft_loss_grad")
+    return gx
+
+
 # ----------------------------------------------------------------------------- training BatchNorm / glyph conv
 
 def _rows(x):
