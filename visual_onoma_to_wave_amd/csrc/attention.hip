@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restric
     for (int ks = 0; ks < 2; ++ks) {
       // whole-vector bit cast of packed words (per-element __bf16 inserts are mis-lowered by hipcc)
       auto pk = [](float lo, float hi) {
-        return (unsigned)from_f32<bf16_t>(lo) | ((unsigned)from_f32<bf16_t>(hi) << 16);
+        return (unsigned)pk_bf16(lo, hi);
       };
       const u4 pw = u4{pk(sacc[2 * ks][0], sacc[2 * ks][1]), pk(sacc[2 * ks][2], sacc[2 * ks][3]),
                        pk(sacc[2 * ks + 1][0], sacc[2 * ks + 1][1]), pk(sacc[2 * ks + 1][2], sacc[2 * ks + 1][3])};
@@ -315,8 +315,8 @@ __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restric
   bf16_t* orow = out + ((int64_t)b * L + qrow) * D + h * ATT_DK;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
-    uint32_t w0 = (uint32_t)from_f32<bf16_t>(o[dt][0] * inv) | ((uint32_t)from_f32<bf16_t>(o[dt][1] * inv) << 16);
-    uint32_t w1 = (uint32_t)from_f32<bf16_t>(o[dt][2] * inv) | ((uint32_t)from_f32<bf16_t>(o[dt][3] * inv) << 16);
+    uint32_t w0 = pk_bf16(o[dt][0] * inv, o[dt][1] * inv);
+    uint32_t w1 = pk_bf16(o[dt][2] * inv, o[dt][3] * inv);
     *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = make_uint2(w0, w1);
   }
 }

@@ -149,7 +149,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
     } else {
       const float ps = a.post_act == VO_ACT_RELU ? 0.f : (a.post_act == VO_ACT_LRELU ? a.post_slope : 1.f);
 #pragma unroll
-      for (int e = 0; e < 4 * NI; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * ps;
+      for (int e = 0; e < 4 * NI; ++e) v[e] = lrelu_max(v[e], ps);  // ps in [0, 1]
     }
 #pragma unroll
     for (int h = 0; h < NI; ++h) {
@@ -370,7 +370,7 @@ conv1d_kernel(ConvArgs a) {
       float f[8];
       win_r[s].to_f32(f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * pre_s;
+      for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
       store8(dst, f);
     }
   };
@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int
   } else {
     const float ps = a.post_act == VO_ACT_RELU ? 0.f : (a.post_act == VO_ACT_LRELU ? a.post_slope : 1.f);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * ps;
+    for (int e = 0; e < 4; ++e) v[e] = lrelu_max(v[e], ps);  // ps in [0, 1]
   }
   const int64_t off = (int64_t)b * a.ybs + (int64_t)t * a.ldy + c;
   if (a.res1) {
@@ -707,6 +707,9 @@ extern "C" int64_t vo_conv1d_workspace_size(const vo_conv1d_desc* d) {
 extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
   VO_CHECK_ARG(d != nullptr, "conv1d: null descriptor");
   VO_CHECK_ARG(d->x && d->w && d->y, "conv1d: null tensor pointer");
+  VO_CHECK_ARG((d->pre_act != VO_ACT_LRELU || (d->pre_slope >= 0.f && d->pre_slope <= 1.f)) &&
+                   (d->post_act != VO_ACT_LRELU || (d->post_slope >= 0.f && d->post_slope <= 1.f)),
+               "conv1d: leaky-ReLU slope outside [0, 1]");
   VO_CHECK_ARG(d->B > 0 && d->T_in > 0 && d->T_out > 0 && d->Ci > 0 && d->Co > 0 && d->K > 0,
                "conv1d: non-positive size (B=%d T_in=%d T_out=%d Ci=%d Co=%d K=%d)", d->B,
                d->T_in, d->T_out, d->Ci, d->Co, d->K);

@@ -15,7 +15,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int rb_off(int r, int q, int sh) { return r * 32 + 8 * (q ^ ((r >> (sh - 1)) & 2)); }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)from_f32<bf16_t>(lo) | ((uint32_t)from_f32<bf16_t>(hi) << 16);
+  return pk_bf16(lo, hi);
 }
 
 // leaky ReLU of 8 packed bf16 (0 <= slope <= 1: lrelu(v) = max(v, slope * v))
@@ -24,7 +24,7 @@ __device__ __forceinline__ u32x4 lrelu8(u32x4 u, float s) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
-    w[i] = pack_bf16x2(fmaxf(lo, lo * s), fmaxf(hi, hi * s));
+    w[i] = pk_bf16(lrelu_max(lo, s), lrelu_max(hi, s));
   }
   return u32x4{w[0], w[1], w[2], w[3]};
 }

@@ -25,6 +25,18 @@ template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float x) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
+// Two floats -> one packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even, NaN stays
+// NaN).  The pair of scalar conversions compiled to two v_cvt_pk_bf16_f32 and a v_or_b32_sdwa.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+// leaky ReLU max(v, s v) for 0 <= s <= 1.  IEEE maximum: unlike fmaxf it needs no operand
+// canonicalisation (fmaxf of a value bit-cast from bf16 compiled to two v_max_f32); the results
+// are identical (a NaN input gives a NaN either way).
+__device__ __forceinline__ float lrelu_max(float v, float s) { return __builtin_elementwise_maximum(v, v * s); }
+
 // ---------------------------------------------------------------- 8-element vectors
 // Load 8 consecutive elements (16 B for bf16, 32 B for f32) as floats.
 __device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
@@ -46,7 +58,7 @@ __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    w[i] = (uint32_t)from_f32<bf16_t>(v[2 * i]) | ((uint32_t)from_f32<bf16_t>(v[2 * i + 1]) << 16);
+    w[i] = pk_bf16(v[2 * i], v[2 * i + 1]);
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
@@ -54,8 +66,8 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 __device__ __forceinline__ void store4(bf16_t* p, const float (&v)[4]) {
-  uint32_t a = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
-  uint32_t b = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
+  uint32_t a = pk_bf16(v[0], v[1]);
+  uint32_t b = pk_bf16(v[2], v[3]);
   *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
 }
 __device__ __forceinline__ void store4(float* p, const float (&v)[4]) {

@@ -56,7 +56,7 @@ template <> struct WgTile<float> { static constexpr int PITCH = 68; };
 
 __device__ __forceinline__ uint32_t lrelu_pack(uint32_t w, float s) {
   const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
-  return (uint32_t)from_f32<bf16_t>(fmaxf(lo, lo * s)) | ((uint32_t)from_f32<bf16_t>(fmaxf(hi, hi * s)) << 16);
+  return pk_bf16(lrelu_max(lo, s), lrelu_max(hi, s));
 }
 
 // 4 waves as 2 x 2, each a 32 x 32 sub-tile = 2 x 2 MFMA tiles
