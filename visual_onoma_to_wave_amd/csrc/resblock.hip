@@ -21,6 +21,7 @@
 // conv1d.hip.
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mrf_common.h"
 
@@ -311,29 +312,26 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     auto p1_epilogue = [&]() {
       float bz[8 * NH];
       lane_bias(0, bz);
-      // rows outside [0, T) exist only in the first / last tile of an utterance: a uniform test
-      // keeps the zero-padding select out of every other tile (per-element selects compiled to
-      // exec-mask branches around each value)
+      // rows outside [0, T) exist only in the first / last tile of an utterance
       const bool interior = t0 - h2 >= 0 && t0 - h2 + R1 <= T;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int r = wt * 16 * NJ + 16 * j + lr;
         const int pos = t0 - h2 + r;
-        const float keep = (interior || (pos >= 0 && pos < T)) ? 1.f : 0.f;
+        // c2's zero padding: one AND per packed dword (rows outside [0, T) -> +0)
+        const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
-          float f[8];
+          uint32_t w[4];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
-            f[e] = fmaxf(z, z * slope);
-          }
-          if (!interior) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] *= keep;
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const int e = 2 * e2;
+            const float z0 = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
+            const float z1 = acc[2 * h + (e + 1) / 4][j][(e + 1) & 3] + bz[8 * h + e + 1];
+            w[e2] = pk_bf16(lrelu_max(z0, slope), lrelu_max(z1, slope)) & km;
           }
           const int ch = n0 + 8 * h;
-          store8(t1 + (ch >> 5) * T1R * 32 + rb_off(r, (ch & 31) >> 3, 2), f);
+          *reinterpret_cast<u32x4*>(t1 + (ch >> 5) * T1R * 32 + rb_off(r, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -428,8 +426,25 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     }
 
     // P2 epilogue: y = (c2 + b2 + x) * out_scale (+ acc)
-    if constexpr (LATE) load_res();
-    if constexpr (IP) {  // IP: the MRF accumulator rows are read here (registers are short)
+    if constexpr (LATE) {
+      // the residual and accumulator rows; the next tile's window is requested before the y
+      // stores (vmcnt retires in issue order: the window store no longer waits for them)
+      const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);
+        const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          if constexpr ((ABL & 2) != 0) {
+            xres[j][h] = ares[j][h] = u32x4{(unsigned)pos, 0u, 0u, 0u};
+          } else {
+            xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+            ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+          }
+        }
+      }
+    } else if constexpr (IP) {  // IP: the MRF accumulator rows are read here (registers are short)
       if (a.acc) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -442,29 +457,54 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     }
     float b2z[8 * NH];
     lane_bias(1, b2z);
+    // y rows through a buffer resource covering exactly this tile's valid rows: the rows past
+    // it (r >= BT, or past T) fall outside the resource and their stores are dropped by the
+    // hardware -- no per-lane branch, and a fixed number of stores per wave
+    const int valid = min(BT, T - t0);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
+    u32x4 yv[NJ][NH];
+    auto epilogue = [&](auto with_acc) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          float xf[8], af8[8];
+          uint32_t w[4];
+          unpack8(xres[j][h], xf);
+          if constexpr (decltype(with_acc)::value) unpack8(ares[j][h], af8);
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            float q[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int e = 2 * e2 + u;
+              q[u] = (acc[2 * h + e / 4][j][e & 3] + b2z[8 * h + e] + xf[e]) * a.out_scale;
+              if constexpr (decltype(with_acc)::value) q[u] += af8[e];
+            }
+            w[e2] = pk_bf16(q[0], q[1]);
+          }
+          yv[j][h] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    };
+    if (a.acc)
+      epilogue(std::true_type{});
+    else
+      epilogue(std::false_type{});
+    // the next window's registers are taken once the y values are packed: with the accumulators,
+    // residual and window live at once the C = 128 kernel spilled and the C = 32 kernel lost its
+    // fourth wave per SIMD (146 VGPRs; s3 +12 %)
+    if constexpr (LATE && IP) load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int r = wt * 16 * NJ + 16 * j + lr;
-      const int pos = t0 + r;
-      if (r >= BT || pos >= T) continue;
-      const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        float xf[8], af8[8], q[8];
-        unpack8(xres[j][h], xf);
-        unpack8(ares[j][h], af8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          q[e] = (acc[2 * h + e / 4][j][e & 3] + b2z[8 * h + e] + xf[e]) * a.out_scale + (a.acc ? af8[e] : 0.f);
-        store8(a.y + off + 8 * h, q);
-      }
+      for (int h = 0; h < NH; ++h)
+        __builtin_amdgcn_raw_buffer_store_b128(yv[j][h], yrs, (r * C + n0 + 8 * h) * (int)sizeof(bf16_t), 0, 0);
     }
     if constexpr (RES) __syncthreads();
     if constexpr (IP) {  // P2's T1 reads ended at the last group barrier
-      if constexpr (LATE) {  // no window registers live in P2 (HP: the other workgroup of the CU
-                             // covers this load's latency)
-        if (has_next) load_win(tile + 1);
-      }
       if (has_next) store_win();
       __syncthreads();
     }

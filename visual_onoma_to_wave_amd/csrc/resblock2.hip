@@ -18,6 +18,7 @@
 // Dilation <= DMAX (5: the HiFi-GAN V1 MRF); the region rows are sized for it at compile time.
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mrf_common.h"
 
@@ -247,21 +248,20 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       for (int j = 0; j < NJ; ++j) {
         const int r = wt * 16 * NJ + 16 * j + lr;
         const int pos = t0 - H2 + r;
-        const float keep = (interior || (pos >= 0 && pos < T)) ? 1.f : 0.f;
+        // c2's zero padding: one AND per packed dword (rows outside [0, T) -> +0)
+        const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
-          float f[8];
+          uint32_t w[4];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
-            f[e] = fmaxf(z, z * slope);
-          }
-          if (!interior) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] *= keep;
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const int e = 2 * e2;
+            const float z0 = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
+            const float z1 = acc[2 * h + (e + 1) / 4][j][(e + 1) & 3] + bz[8 * h + e + 1];
+            w[e2] = pk_bf16(lrelu_max(z0, slope), lrelu_max(z1, slope)) & km;
           }
           const int ch = n0 + 8 * h;
-          store8(reg + (ch >> 5) * WR * 32 + rb_off(r, (ch & 31) >> 3, 2), f);
+          *reinterpret_cast<u32x4*>(reg + (ch >> 5) * WR * 32 + rb_off(r, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -304,41 +304,63 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
 #pragma unroll 1
     for (int g = NGW; g < NG; ++g) p2_group(g, 0, 0);
 
-    // ---- P2 epilogue: the window goes to LDS first (T1's reads ended at the last group barrier;
-    // its registers are free before the residual rows arrive), then
-    // y = (c2 + b2 + x) * out_scale (+ acc)
-    if (has_next) store_win();
+    // ---- P2 epilogue: the residual rows are requested first, the window goes to LDS while
+    // they are in flight (T1's reads ended at the last group barrier), then
+    // y = (c2 + b2 + x) * out_scale (+ acc), stored through a buffer resource that covers exactly
+    // the tile's valid rows (the stores of the rows past it are dropped: no per-lane branch)
     u32x4 xres[NJ][NH], ares[NJ][NH];
     const bf16_t* accp = a.acc ? a.acc : a.x;  // loaded either way (no branch), added only with acc
+    if (C >= 128 && has_next) store_win();  // C = 128: no registers to spare for the early loads
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);
       const int64_t off = ((int64_t)b * T + pos) * C + n0;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
-        ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
-      }
+      for (int h = 0; h < NH; ++h) xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+    }
+    if (C < 128 && has_next) store_win();  // its registers are free before the accumulator rows are requested
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pos = min(t0 + wt * 16 * NJ + 16 * j + lr, T - 1);
+      const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
     }
     float b2z[8 * NH];
     lane_bias(1, b2z);
+    const int valid = min(BT, T - t0);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
+    auto epilogue = [&](auto with_acc) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int r = wt * 16 * NJ + 16 * j + lr;
-      const int pos = t0 + r;
-      if (r >= BT || pos >= T) continue;
-      const int64_t off = ((int64_t)b * T + pos) * C + n0;
+      for (int j = 0; j < NJ; ++j) {
+        const int r = wt * 16 * NJ + 16 * j + lr;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        float xf[8], af8[8], q[8];
-        unpack8(xres[j][h], xf);
-        unpack8(ares[j][h], af8);
+        for (int h = 0; h < NH; ++h) {
+          float xf[8], af8[8];
+          uint32_t w[4];
+          unpack8(xres[j][h], xf);
+          if constexpr (decltype(with_acc)::value) unpack8(ares[j][h], af8);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          q[e] = (acc[2 * h + e / 4][j][e & 3] + b2z[8 * h + e] + xf[e]) * a.out_scale + (a.acc ? af8[e] : 0.f);
-        store8(a.y + off + 8 * h, q);
+          for (int e2 = 0; e2 < 4; ++e2) {
+            float q[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int e = 2 * e2 + u;
+              q[u] = (acc[2 * h + e / 4][j][e & 3] + b2z[8 * h + e] + xf[e]) * a.out_scale;
+              if constexpr (decltype(with_acc)::value) q[u] += af8[e];
+            }
+            w[e2] = pk_bf16(q[0], q[1]);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[0], w[1], w[2], w[3]}, yrs,
+                                                 (r * C + n0 + 8 * h) * (int)sizeof(bf16_t), 0, 0);
+        }
       }
-    }
+    };
+    if (a.acc)
+      epilogue(std::true_type{});
+    else
+      epilogue(std::false_type{});
     __syncthreads();  // the next window is visible before the next P1
   }
 }

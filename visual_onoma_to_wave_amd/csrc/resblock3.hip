@@ -20,6 +20,7 @@
 // Accumulation order per conv: tap-major, planes inner (as the streamed pair kernels).
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mrf_common.h"
 
@@ -224,31 +225,31 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
       if (k != 2) continue;
       // ---- end of a conv: every wave is past its reads of the region
       if constexpr (RESW) __syncthreads();
+      if (s == 2 && ph == 1) break;  // the last conv's epilogue follows the loop (its window
+                                     // registers must not be live around the loop)
       float bz[8 * NH];
       lane_bias(2 * s + ph, bz);
-      // frame rows outside [0, T) exist only in an utterance's first / last tile: a uniform test
-      // keeps the zero-padding selects (compiled to exec-mask branches per value) out of the rest
+      // frame rows outside [0, T) exist only in an utterance's first / last tile
       const bool interior = p0 >= 0 && p0 + F <= T;
       if (ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int r = wt * 16 * NJ + 16 * j + lr;
           const int pos = p0 + r;
-          const float keep = (interior || (pos >= 0 && pos < T)) ? 1.f : 0.f;
+          // c2's zero padding: one AND per packed dword (rows outside [0, T) -> +0)
+          const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
 #pragma unroll
           for (int h = 0; h < NH; ++h) {
-            float f[8];
+            uint32_t w[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float z = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
-              f[e] = fmaxf(z, z * slope);
-            }
-            if (!interior) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) f[e] *= keep;
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const int e = 2 * e2;
+              const float z0 = acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e];
+              const float z1 = acc[2 * h + (e + 1) / 4][j][(e + 1) & 3] + bz[8 * h + e + 1];
+              w[e2] = pk_bf16(lrelu_max(z0, slope), lrelu_max(z1, slope)) & km;
             }
             const int ch = n0 + 8 * h;
-            store8(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2), f);
+            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
           }
         }
       } else if (s < 2) {  // x_{s+1} = x_s + c2 + b2 (bf16), its lrelu'd copy over the region
@@ -287,29 +288,6 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
             *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) = v;
           }
         }
-      } else {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int r = wt * 16 * NJ + 16 * j + lr;
-          const int pos = p0 + r;
-          if (r < RB3_HALO || r >= F - RB3_HALO || pos >= T) continue;
-          const int64_t off = ((int64_t)b * T + pos) * C + n0;
-#pragma unroll
-          for (int h = 0; h < NH; ++h) {
-            float xf[8], af8[8], q[8];
-            unpack8(xres[j][h], xf);
-            if (a.acc) {
-              load8(a.acc + off + 8 * h, af8);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) af8[e] = 0.f;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              q[e] = (acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e] + xf[e]) * a.out_scale + af8[e];
-            store8(a.y + off + 8 * h, q);
-          }
-        }
       }
 #pragma unroll
       for (int i = 0; i < NI; ++i)
@@ -317,8 +295,73 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (g + 1 < NG) __syncthreads();  // region rewritten: visible before the next conv reads it
     }
-    // next window over the region (P2 of stage 2 ended its region reads at the last barrier)
-    load_win(has_next ? tile + 1 : tile);
+    {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows
+      float bz[8 * NH];
+      lane_bias(5, bz);
+      // the accumulator rows for every (j, h) at once (clamped, unconditional: without acc the
+      // x rows are read and not added) instead of one dependent load per store; the y values
+      // are packed, the next tile's window is requested (before the y stores: vmcnt retires in
+      // order), then the y rows go out through a buffer resource that covers exactly the
+      // tile's valid rows -- the stores of the halo rows and of rows past T fall outside it and
+      // are dropped by the hardware
+      u32x4 ares[NJ][NH], yv[NJ][NH];
+      const bf16_t* accp = a.acc ? a.acc : a.x;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int pos = min(max(p0 + wt * 16 * NJ + 16 * j + lr, 0), T - 1);
+        const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
+      }
+      auto epilogue = [&](auto with_acc) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            float xf[8], af8[8];
+            uint32_t w[4];
+            unpack8(xres[j][h], xf);
+            if constexpr (decltype(with_acc)::value) unpack8(ares[j][h], af8);
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              float q[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int e = 2 * e2 + u;
+                q[u] = (acc[2 * h + e / 4][j][e & 3] + bz[8 * h + e] + xf[e]) * a.out_scale;
+                if constexpr (decltype(with_acc)::value) q[u] += af8[e];
+              }
+              w[e2] = pk_bf16(q[0], q[1]);
+            }
+            yv[j][h] = u32x4{w[0], w[1], w[2], w[3]};
+          }
+        }
+      };
+      if (a.acc)
+        epilogue(std::true_type{});
+      else
+        epilogue(std::false_type{});
+      load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
+      const int t0 = p0 + RB3_HALO;  // the tile's first output position (frame row HALO)
+      const int valid = min(BT, T - t0);
+      const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int r = wt * 16 * NJ + 16 * j + lr - RB3_HALO;  // row within the resource
+        // rows before it: an offset past any resource (dropped like the rows past it)
+        const int roff = r >= 0 ? r * C * (int)sizeof(bf16_t) : 0x40000000;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+          __builtin_amdgcn_raw_buffer_store_b128(yv[j][h], yrs, roff + (n0 + 8 * h) * (int)sizeof(bf16_t), 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // next window (requested in the last epilogue) over the region (P2 of stage 2 ended its
+    // region reads at the last barrier)
     if (has_next) store_win();
     __syncthreads();
   }
