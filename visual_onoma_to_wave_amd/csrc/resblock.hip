@@ -612,6 +612,9 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // weight stream per MFMA of the 192-row kernel (384 rows spill)
     if (cfg == 6) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
     if (cfg == 7) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
+    // measured on the round-2 epilogue (tools/bench_ab.sh, two rounds each): the default k >= 7
+    // kernel with the pinned fragment pipeline (SB) +1.5 % (one spilled VGPR), with setprio
+    // around its MFMA clusters (PRIO 1) within noise -- neither kept.
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
     // SIMD (12 waves, 2 x 6) 15 % slower.
