@@ -200,6 +200,19 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
           load_grp(h + D < NGR ? h + D : h + D - NGR, (gcount + D) % NBUF);
           wb = wls + (gcount % NBUF) * GE;
         }
+        if (g == 0 && part == 0) {
+          // the tile's x rows (stage 0's residual, epilogue layout), requested with the first
+          // group (after its weight DMA: the group-end wait then covers both) instead of at the
+          // end of stage 0's c2, where each load's latency was exposed; xres is live across the
+          // tap loop anyway (x1 / x2)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int pos = min(max(p0 + wt * 16 * NJ + 16 * j + lr, 0), T - 1);
+            const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+            for (int h = 0; h < NH; ++h) xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+          }
+        }
 #pragma unroll
         for (int cl = 0; cl < (RESW ? NC : GPL); ++cl) {
           const int c = part * GPL + cl;
@@ -253,15 +266,6 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
           }
         }
       } else if (s < 2) {  // x_{s+1} = x_s + c2 + b2 (bf16), its lrelu'd copy over the region
-        if (s == 0) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            const int pos = min(max(p0 + wt * 16 * NJ + 16 * j + lr, 0), T - 1);
-            const int64_t off = ((int64_t)b * T + pos) * C + n0;
-#pragma unroll
-            for (int h = 0; h < NH; ++h) xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
-          }
-        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int r = wt * 16 * NJ + 16 * j + lr;
