@@ -218,24 +218,52 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       }
 }
 
-// dW[((g M + m) N + n) K + k] = sum over splits in order of part[s][g][k][m][n]; db likewise
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int splits, int64_t n_w,
-                                                           int64_t n_tot, int M, int N, int K,
-                                                           float* __restrict__ dw, float* __restrict__ db) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_tot; i += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int q = 0; q < splits; ++q) s += part[(int64_t)q * n_tot + i];
-    if (i < n_w) {
-      const int n = (int)(i % N);
-      const int64_t r = i / N;
-      const int m = (int)(r % M);
-      const int64_t gk = r / M;
-      const int k = (int)(gk % K), g = (int)(gk / K);
-      dw[(((int64_t)g * M + m) * N + n) * K + k] = s;
-    } else {
-      db[i - n_w] = s;
-    }
+// dW[((g M + m) N + n) K + k] = sum over splits of part[s][g][k][m][n]; db likewise.
+// A block holds G groups of 64 consecutive outputs (lane = output: coalesced) and W waves per
+// group: wave w of a group adds splits w, w + W, .. in order, then the W wave sums are added in
+// wave order -- a fixed order (deterministic run to run).  Many splits (small M x N tiles: ~340 at
+// M = N = 32, K = 3) take W = 16, 16 x the memory parallelism of one thread walking every split
+// (which took most of such a wgrad call); few splits over many outputs take W = 1, G = 4.
+template <int W, int G>
+__global__ void __launch_bounds__(64 * W * G) wgrad_reduce_kernel(const float* __restrict__ part, int splits,
+                                                                  int64_t n_w, int64_t n_tot, int M, int N, int K,
+                                                                  float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[W > 1 ? W * G : 1][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = wave % W, grp = wave / W;
+  const int64_t i = ((int64_t)blockIdx.x * G + grp) * 64 + lane;
+  float s = 0.f;
+  if (i < n_tot)
+    for (int q = w; q < splits; q += W) s += part[(int64_t)q * n_tot + i];
+  if constexpr (W > 1) {
+    red[wave][lane] = s;
+    __syncthreads();
+    if (w != 0) return;
+    s = red[grp * W][lane];
+#pragma unroll
+    for (int q = 1; q < W; ++q) s += red[grp * W + q][lane];
   }
+  if (i >= n_tot) return;
+  if (i < n_w) {
+    const int n = (int)(i % N);
+    const int64_t r = i / N;
+    const int m = (int)(r % M);
+    const int64_t gk = r / M;
+    const int k = (int)(gk % K), g = (int)(gk / K);
+    dw[(((int64_t)g * M + m) * N + n) * K + k] = s;
+  } else {
+    db[i - n_w] = s;
+  }
+}
+
+static void wgrad_reduce_launch(const float* part, int splits, int64_t n_w, int64_t n_tot, int M, int N, int K,
+                                float* dw, float* db, hipStream_t st) {
+  if (splits >= 32)
+    hipLaunchKernelGGL((wgrad_reduce_kernel<16, 1>), dim3((unsigned)((n_tot + 63) / 64)), dim3(1024), 0, st, part,
+                       splits, n_w, n_tot, M, N, K, dw, db);
+  else
+    hipLaunchKernelGGL((wgrad_reduce_kernel<1, 4>), dim3((unsigned)((n_tot + 255) / 256)), dim3(256), 0, st, part,
+                       splits, n_w, n_tot, M, N, K, dw, db);
 }
 
 // column sums of a (rows x C) channels-last tensor -> out[C] (written): per-block partials in a
@@ -329,9 +357,7 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
-  const unsigned rg = (unsigned)std::min<int64_t>((p.n_tot + 255) / 256, 2048);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, workspace, (int)splits, p.n_w, p.n_tot, M, N, K,
-                     dw, db);
+  wgrad_reduce_launch(workspace, (int)splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
   VO_RETURN_LAUNCH();
 }
 
@@ -374,7 +400,6 @@ extern "C" int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, 
   else
     hipLaunchKernelGGL(colsum_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, rows, C, ld, rpb, workspace);
   // the block partials [g][C] added in block order: the reduce kernel's bias path (n_w = 0)
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min((C + 255) / 256, 2048)), dim3(256), 0, st, workspace,
-                     g, (int64_t)0, (int64_t)C, 1, 1, 1, (float*)nullptr, out);
+  wgrad_reduce_launch(workspace, g, 0, C, 1, 1, 1, nullptr, out, st);
   VO_RETURN_LAUNCH();
 }
