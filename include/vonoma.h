@@ -293,7 +293,9 @@ int vo_char_features(const float* energy, const float* fstats, int F, const int3
  * Discriminator glue (the reference ships no discriminator code, only
  * the training hyper-parameters of scripts/hifigan/config.json):
  *  vo_pack_grouped: (Co, Ci/groups, K) fp32 -> dense [K][Co][Ci_pad] block-diagonal (zeros
- *    outside the groups and for ci >= Ci) for vo_conv1d's groups mode;
+ *    outside the groups and for ci >= Ci) for vo_conv1d's groups mode; vo_pack_grouped_blocks
+ *    writes the diagonal blocks only (an in-place update of a buffer whose other entries are
+ *    already zero);
  *  vo_period_fold: wav (B, T) -> (B*P, ceil(T/P), 8) channels-last, the MPD's reflect pad to a
  *    multiple of P and (T/P, P) view with each period column a separate sequence;
  *  vo_wav_cl8: (B, T) -> (B, T, 8) (channel 0); vo_avgpool_wav: AvgPool1d(4, 2, padding 2),
@@ -303,6 +305,8 @@ int vo_char_features(const float* energy, const float* fstats, int F, const int3
  *    vo_gan_reduce_grad: ga = *scale * d(sum)/da. */
 int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
                     int dst_dtype, void* stream);
+int vo_pack_grouped_blocks(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
+                           int dst_dtype, void* stream);
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
 int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
 int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);

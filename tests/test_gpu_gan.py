@@ -39,6 +39,26 @@ def test_strided_grouped_conv_vs_torch(B, T, Ci, Co, K, s, g, pad, dt, tol):
     assert rel_l2(out.float().cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Co,Ci,K,g,ci_pad", [(1024, 1024, 41, 16, None), (128, 128, 41, 4, None),
+                                              (256, 128, 41, 16, None), (64, 8, 5, 1, 16), (8, 16, 3, 2, 24)])
+def test_pack_grouped_blocks_in_place(Co, Ci, K, g, ci_pad, dt):
+    """vo_pack_grouped_blocks into a zeroed buffer == the dense pack, bit for bit, and a second
+    update of the same buffer with new weights == a fresh dense pack of them."""
+    from visual_onoma_to_wave_amd import ops
+    gen = torch.Generator().manual_seed(Co + Ci + K + g)
+    w1 = torch.randn(Co, Ci // g, K, generator=gen).cuda()
+    w2 = torch.randn(Co, Ci // g, K, generator=gen).cuda()
+    cp = Ci if ci_pad is None else ci_pad
+    buf = torch.zeros((K, Co, cp), dtype=dt, device="cuda")
+    for w in (w1, w2):
+        got = ops.pack_grouped_weight(w, dt, g, ci_pad, out=buf)
+        assert got.data_ptr() == buf.data_ptr()
+        assert torch.equal(buf, ops.pack_grouped_weight(w, dt, g, ci_pad))
+    with pytest.raises(ValueError):
+        ops.pack_grouped_weight(w1, dt, g, ci_pad, out=buf[:1])
+
+
 @pytest.mark.parametrize("T,p", [(8192, 2), (8192, 3), (8192, 5), (8191, 7), (8000, 11), (13, 11)])
 def test_period_fold_exact(T, p):
     from visual_onoma_to_wave_amd import ops

@@ -121,6 +121,7 @@ _SIGNATURES = {
     "vo_char_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),
     "vo_pack_grouped": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "vo_pack_grouped_blocks": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "vo_period_fold": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "vo_wav_cl8": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "vo_avgpool_wav": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),

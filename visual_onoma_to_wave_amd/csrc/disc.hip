@@ -34,6 +34,23 @@ __global__ void __launch_bounds__(256) pack_grouped_kernel(const float* __restri
   }
 }
 
+// The diagonal blocks only (dst's other entries are left as they are: a persistent packed
+// buffer is zeroed once and then updated in place after each optimizer step -- the dense
+// kernel above wrote groups x more, mostly zeros, on every repack).  One thread per source
+// element, consecutive threads on consecutive input channels of one (tap, output row): the
+// stores of a block row are contiguous.
+template <typename TD>
+__global__ void __launch_bounds__(256) pack_grouped_blocks_kernel(const float* __restrict__ src, int Co, int cig,
+                                                                  int cog, int K, int Ci_pad, TD* __restrict__ dst) {
+  const int64_t n = (int64_t)K * Co * cig;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % cig);
+    const int64_t r = i / cig;  // k * Co + co
+    const int co = (int)(r % Co), k = (int)(r / Co);
+    dst[r * Ci_pad + (co / cog) * cig + c] = from_f32<TD>(src[((int64_t)co * cig + c) * K + k]);
+  }
+}
+
 // wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
 // reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
 template <typename TD>
@@ -320,6 +337,23 @@ extern "C" int vo_pack_grouped(const float* src, int Co, int Ci, int K, int grou
                        (bf16_t*)dst);
   else
     hipLaunchKernelGGL(pack_grouped_kernel<float>, dim3(g), dim3(256), 0, st, src, Co, Ci, K, groups, Ci_pad,
+                       (float*)dst);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_pack_grouped_blocks(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
+                                      int dst_dtype, void* stream) {
+  VO_CHECK_ARG(src && dst, "pack_grouped_blocks: null pointer");
+  VO_CHECK_ARG(groups >= 1 && Co % groups == 0 && Ci % groups == 0 && Ci_pad >= Ci && K >= 1,
+               "pack_grouped_blocks: bad sizes Co=%d Ci=%d groups=%d Ci_pad=%d", Co, Ci, groups, Ci_pad);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int cig = Ci / groups, cog = Co / groups;
+  const int g = grid_for((int64_t)K * Co * cig);
+  if (dst_dtype == VO_BF16)
+    hipLaunchKernelGGL(pack_grouped_blocks_kernel<bf16_t>, dim3(g), dim3(256), 0, st, src, Co, cig, cog, K, Ci_pad,
+                       (bf16_t*)dst);
+  else
+    hipLaunchKernelGGL(pack_grouped_blocks_kernel<float>, dim3(g), dim3(256), 0, st, src, Co, cig, cog, K, Ci_pad,
                        (float*)dst);
   VO_RETURN_LAUNCH();
 }

@@ -82,7 +82,7 @@ static const char* const kSymbols[] = {
     "vo_pack_weight",    "vo_layernorm",     "vo_attention",   "vo_length_regulate", "vo_lr_lengths",
     "vo_variance_head",  "vo_vfe_stencil",   "vo_add_pos_class", "vo_conv_post",   "vo_transpose_bct",
     "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair", "vo_stft_mel_ex",
-    "vo_pack_grouped",   "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
+    "vo_pack_grouped",   "vo_pack_grouped_blocks", "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
     "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_attention_bwd_workspace_size", "vo_attention_bwd",

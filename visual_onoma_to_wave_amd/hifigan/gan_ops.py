@@ -57,14 +57,24 @@ class ConvSpec:
 _POST = {None: ops.ACT_NONE, "lrelu": ops.ACT_LRELU, "tanh": ops.ACT_TANH}
 
 
-def _pack(w, spec, dtype):
+def _pack(w, spec, dtype, slot=None):
+    """``slot(shape, dtype)`` (optional): a persistent zero-initialised buffer that the grouped
+    layout is written into in place -- its diagonal blocks only (``ops.pack_grouped_weight(out=)``)."""
     if spec.transposed is not None:
         return ops.pack_conv_weight(w, dtype, transposed_stride=spec.transposed[0])
     if spec.plain():
         return ops.pack_conv_weight(w, dtype)
     if spec.co_pad is not None and spec.co_pad > w.shape[0]:
         w = torch.cat([w.detach(), w.new_zeros((spec.co_pad - w.shape[0],) + tuple(w.shape[1:]))])
-    return ops.pack_grouped_weight(w, dtype, spec.groups, spec.ci_pad)
+    return _pack_grouped(w, dtype, spec.groups, spec.ci_pad, slot)
+
+
+def _pack_grouped(w, dtype, groups, ci_pad, slot):
+    if slot is None:
+        return ops.pack_grouped_weight(w, dtype, groups, ci_pad)
+    Co, cig, K = w.shape
+    return ops.pack_grouped_weight(w, dtype, groups, ci_pad, out=slot((K, Co, cig * groups if ci_pad is None else ci_pad),
+                                                                      dtype, w.device))
 
 
 def _bias(b, spec, n):
@@ -93,6 +103,27 @@ def reset_pack_cache():
     _CAPTURE_PACKS.clear()
 
 
+# Persistent packed buffers of the grouped (block-diagonal) layouts, per module and pack tag:
+# zeroed once, then only their diagonal blocks are rewritten when the weights change (the dense
+# repack wrote groups x more bytes, mostly zeros, after every optimizer step).  They outlive the
+# version cache above (a HIP graph captures the in-place updates at stable addresses).
+_SLOTS = weakref.WeakKeyDictionary()
+
+
+def _slot_fn(wkey, tag):
+    if wkey is None:
+        return None
+
+    def get(shape, dtype, device):
+        per = _SLOTS.setdefault(wkey[0], {})
+        buf = per.get(tag)
+        if buf is None or tuple(buf.shape) != tuple(shape) or buf.dtype != dtype or buf.device != device:
+            buf = torch.zeros(shape, dtype=dtype, device=device)
+            per[tag] = buf
+        return buf
+    return get
+
+
 def weight_key(m):
     """Cache key of a conv module's effective weight: the module and its parameters' version
     counters (bumped by every optimizer step / load_state_dict).  None (no caching) for
@@ -117,7 +148,8 @@ def _cached(wkey, tag, build):
 
 
 def _conv_fwd(x, w, b, res1, res2, spec, cdt, wkey=None):
-    wp = _cached(wkey, (spec, cdt, "fwd"), lambda: _pack(w, spec, cdt))
+    tag = (spec, cdt, "fwd")
+    wp = _cached(wkey, tag, lambda: _pack(w, spec, cdt, _slot_fn(wkey, tag)))
     if spec.transposed is not None:
         s, p = spec.transposed
         cout = w.shape[1]
@@ -171,12 +203,14 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
             continue
         J = len(taps)
         c_r = (r + pad - k_r) // S
-        def build(k_r=k_r):
+        tag = (spec, cdt, "dgrad", r, ci_out, co_in)
+
+        def build(k_r=k_r, tag=tag):
             # tap t <- k_r + S (J - 1 - t); a strided slice + flip (list indexing would copy the
             # index list host -> device, which a HIP-graph capture refuses)
             wsel = wt_get()[:, :, k_r::S].flip(-1).contiguous()
-            return ops.pack_grouped_weight(wsel, cdt, groups=g if ci_out == Ci else 1, ci_pad=co_in)
-        wp = _cached(wkey, (spec, cdt, "dgrad", r, ci_out, co_in), build)
+            return _pack_grouped(wsel, cdt, g if ci_out == Ci else 1, co_in, _slot_fn(wkey, tag))
+        wp = _cached(wkey, tag, build)
         ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,
                    groups=g if ci_out == Ci else 1)
     return out

@@ -620,12 +620,21 @@ def vfe_conv_bwd(x, gy, w10):
 
 # ----------------------------------------------------------------------------- HiFi-GAN training (C5)
 
-def pack_grouped_weight(w, dtype, groups=1, ci_pad=None):
-    """(Co, Ci/groups, K) fp32 -> dense [K][Co][Ci_pad] block-diagonal (vo_conv1d groups mode)."""
+def pack_grouped_weight(w, dtype, groups=1, ci_pad=None, out=None):
+    """(Co, Ci/groups, K) fp32 -> dense [K][Co][Ci_pad] block-diagonal (vo_conv1d groups mode).
+    ``out``: a buffer of that shape and dtype whose entries outside the diagonal blocks are zero
+    (a persistent packed weight): only the blocks are rewritten (vo_pack_grouped_blocks)."""
     w = w.detach().float().contiguous()
     Co, cig, K = w.shape
     Ci = cig * groups
     ci_pad = Ci if ci_pad is None else ci_pad
+    if out is not None:
+        if tuple(out.shape) != (K, Co, ci_pad) or out.dtype != dtype or not out.is_contiguous():
+            raise ValueError(f"pack_grouped_weight: out {tuple(out.shape)} {out.dtype}, "
+                             f"expected contiguous {(K, Co, ci_pad)} {dtype}")
+        _lib.check(_lib.lib().vo_pack_grouped_blocks(_ptr(w), Co, Ci, K, groups, ci_pad, _ptr(out),
+                                                     vo_dtype(dtype), _stream(w)), "vo_pack_grouped_blocks")
+        return out
     out = torch.empty((K, Co, ci_pad), dtype=dtype, device=w.device)
     _lib.check(_lib.lib().vo_pack_grouped(_ptr(w), Co, Ci, K, groups, ci_pad, _ptr(out), vo_dtype(dtype),
                                           _stream(w)), "vo_pack_grouped")
