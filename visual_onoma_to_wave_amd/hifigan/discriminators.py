@@ -55,6 +55,17 @@ def effective_weight(m):
     return m.weight
 
 
+def _weight(m):
+    """``effective_weight(m)``; while it needs no gradient (frozen discriminator in the G step, or
+    no_grad) the value is reused across forwards at unchanged parameter versions (the G step
+    runs each discriminator twice: real half without graph, generated half)."""
+    wkey = G.weight_key(m)
+    p = m.weight_v if hasattr(m, "weight_v") else m.weight
+    if wkey is None or (torch.is_grad_enabled() and p.requires_grad):
+        return effective_weight(m)
+    return G._cached(wkey, "w_eff", lambda: effective_weight(m).detach())
+
+
 class _DiscBase(nn.Module):
     compute_dtype = torch.bfloat16
 
@@ -96,10 +107,10 @@ class DiscriminatorP(_DiscBase):
         specs, post = self._specs()
         fmap = []
         for m, sp in zip(self.convs, specs):
-            x = G.conv(x, effective_weight(m)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
+            x = G.conv(x, _weight(m)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, effective_weight(m)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
+        y = G.conv(x, _weight(m)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap
@@ -146,10 +157,10 @@ class DiscriminatorS(_DiscBase):
         for m, (ci, co, k, s, g, p) in zip(self.convs, self.cfg):
             sp = G.ConvSpec(K=k, pad=p, stride=s, groups=g, post="lrelu", post_slope=LRELU_SLOPE,
                             ci_pad=8 if ci == 1 else None)
-            x = G.conv(x, effective_weight(m), m.bias, sp, cdt, wkey=G.weight_key(m))
+            x = G.conv(x, _weight(m), m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, effective_weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
+        y = G.conv(x, _weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap

@@ -262,7 +262,9 @@ class ConvFn(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         ga = None
         if need_x and spec.plain():
-            wd = ops.pack_dgrad_weight(w, cdt)
+            # cached per parameter version: a discriminator's next D step runs its backward at the
+            # versions its G step's backward already packed
+            wd = _cached(ctx.wkey, (spec, cdt, "dgrad_plain"), lambda: ops.pack_dgrad_weight(w, cdt))
             ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
                             pad=(spec.K - 1) * spec.dil - spec.pad, T_out=x.shape[1], out_dtype=x.dtype,
                             compute_dtype=cdt)
