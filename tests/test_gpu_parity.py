@@ -291,12 +291,13 @@ def test_conv1d_vs_torch_fp32(B, T, Ci, Co, K, dil, act, dt, tol):
     assert rel_l2(out.cpu(), ref) < tol
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 5, 6])
 @pytest.mark.parametrize("B,T,C,K,dil", [(2, 1000, 256, 11, 5), (3, 300, 256, 3, 1), (1, 1, 256, 7, 3),
                                          (2, 4096, 256, 7, 3), (2, 517, 128, 11, 1)])
 def test_conv1d_mrf_stage0_tiles(B, T, C, K, dil, cfg):
-    """MRF stage-0 conv (variant 1: 256 x 256 tile with LDS-DMA weights, conv_cfg 1: 128 x 128,
-    conv_cfg 3: register-staged weights) with lrelu prologue,
+    """MRF stage-0 conv (variant 1: 256 x 256 tile with LDS-DMA weights -- role-split staging for
+    k >= 5, conv_cfg 5 forces it, 6 disables it; conv_cfg 1: 128 x 128, conv_cfg 3: register-staged
+    weights) with lrelu prologue,
     residual and accumulate epilogue, against PyTorch fp32 at ragged T and Co < tile."""
     import torch.nn.functional as F
     from visual_onoma_to_wave_amd import _lib, ops
@@ -317,6 +318,30 @@ def test_conv1d_mrf_stage0_tiles(B, T, C, K, dil, cfg):
     finally:
         _lib.lib().vo_tune(b"conv_cfg", 0)
     assert rel_l2(out.float().cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,T,K,dil", [(2, 1000, 11, 5), (3, 300, 3, 1), (1, 1, 7, 3), (2, 4099, 7, 3)])
+def test_conv1d_stage0_role_split_bit_identical(B, T, K, dil):
+    """The role-split stage-0 conv (conv_cfg 5) equals the single-role kernel (conv_cfg 6) bit for bit,
+    with both the residual and the MRF accumulator operands, at ragged T (tile edges, T = 1)."""
+    from visual_onoma_to_wave_amd import _lib, ops
+    C = 256
+    g = torch.Generator().manual_seed(T + K)
+    x = torch.randn(B, T, C, generator=g).to(torch.bfloat16).cuda()
+    wp = ops.pack_conv_weight((torch.randn(C, C, K, generator=g) / (C * K) ** 0.5).cuda(), torch.bfloat16)
+    b = (torch.randn(C, generator=g) * 0.1).cuda()
+    res = torch.randn(B, T, C, generator=g).to(torch.bfloat16).cuda()
+    acc = torch.randn(B, T, C, generator=g).to(torch.bfloat16).cuda()
+    outs = []
+    for cfg in (5, 6):
+        _lib.lib().vo_tune(b"conv_cfg", cfg)
+        try:
+            outs.append(ops.conv1d(x, wp, b, Co=C, K=K, dil=dil, pad=dil * (K - 1) // 2, pre_act=ops.ACT_LRELU,
+                                   pre_slope=0.1, res1=res, res2=acc, out_scale=1 / 3, variant=1))
+            torch.cuda.synchronize()
+        finally:
+            _lib.lib().vo_tune(b"conv_cfg", 0)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("B,L,lens", [(4, 512, [512, 300, 1, 77]), (2, 1000, [1000, 999]), (3, 12, [12, 7, 5]),

@@ -1,6 +1,7 @@
 """One MRF kernel at a bench shape (B=32), launched a few times, for rocprofv3 counter passes.
 
     python tools/probes/mrf_probe.py pair C k d [pair_cfg]   |   python tools/probes/mrf_probe.py rb3 C
+    python tools/probes/mrf_probe.py conv 256 k d [conv_cfg]  (stage-0 conv, vo_conv1d variant 1, residual on)
 """
 import os
 import sys
@@ -27,6 +28,13 @@ def main():
         w = [ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
              for _ in range(2)]
         fn = lambda: ops.resblock_pair(x, w[0], b, w[1], b, k, d, 0.1, out=y, out_scale=1 / 3, acc=y)  # noqa: E731
+    elif kind == "conv":
+        k, d = int(sys.argv[3]), int(sys.argv[4])
+        if len(sys.argv) > 5:
+            _lib.lib().vo_tune(b"conv_cfg", int(sys.argv[5]))
+        w = ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
+        fn = lambda: ops.conv1d(x, w, b, Co=C, K=k, dil=d, pad=d * (k - 1) // 2, pre_act=ops.ACT_LRELU,  # noqa: E731
+                                pre_slope=0.1, out=y, res1=x, variant=1)
     else:
         w1 = [ops.pack_conv_weight(torch.randn(C, C, 3, device="cuda", generator=g) / (C * 3) ** 0.5, torch.bfloat16)
               for _ in range(3)]

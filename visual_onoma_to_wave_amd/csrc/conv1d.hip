@@ -107,6 +107,79 @@ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
 
 // epilogue: lane (g = lane>>4, lr = lane&15) holds channels [n0, n0 + 4*NI) of position
 // pos for each of its NJ position tiles
+// bf16 output, plain conv, whole 8-channel runs (vec_ok: ldy / y_bstride multiples of 8):
+// every residual / accumulator row of JG positions is requested before any is used (one memory
+// round trip per JG positions instead of one per position: the scalar form waited for each row's
+// load before its store, 8 times per 128-row wave tile), 16-byte loads and stores; the same
+// arithmetic in the same order as the scalar form (bit-identical)
+template <int NI, int NJ>
+__device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0, int n0,
+                                                  int wave_t0, int lr) {
+  static_assert(NI % 2 == 0, "8-channel runs");
+  constexpr int NH = NI / 2;
+  constexpr int JG = NJ < 2 ? NJ : 2;
+  bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (int64_t)b * a.ybs;
+  const bf16_t* R1 = reinterpret_cast<const bf16_t*>(a.res1 ? a.res1 : a.y) + (int64_t)b * a.ybs;
+  const bf16_t* R2 = reinterpret_cast<const bf16_t*>(a.res2 ? a.res2 : a.y) + (int64_t)b * a.ybs;
+  const bool r1 = a.res1 != nullptr, r2 = a.res2 != nullptr;
+  float bias[4 * NI];
+#pragma unroll
+  for (int e = 0; e < 4 * NI; ++e) bias[e] = a.bias ? a.bias[n0 + e] : 0.f;
+  const float ps = a.post_act == VO_ACT_RELU ? 0.f : (a.post_act == VO_ACT_LRELU ? a.post_slope : 1.f);
+  const bool tanh_act = a.post_act == VO_ACT_TANH;
+#pragma unroll
+  for (int j0 = 0; j0 < NJ; j0 += JG) {
+    uint4 rv1[JG][NH], rv2[JG][NH];
+#pragma unroll
+    for (int jj = 0; jj < JG; ++jj) {  // rows past T_out re-read the last row (not stored)
+      const int pos = min(t0 + wave_t0 + 16 * (j0 + jj) + lr, a.T_out - 1);
+      const int64_t off = (int64_t)pos * a.ldy + n0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        if (r1) rv1[jj][h] = *reinterpret_cast<const uint4*>(R1 + off + 8 * h);
+        if (r2) rv2[jj][h] = *reinterpret_cast<const uint4*>(R2 + off + 8 * h);
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < JG; ++jj) {
+      const int j = j0 + jj;
+      const int pos = t0 + wave_t0 + 16 * j + lr;
+      const int64_t off = (int64_t)min(pos, a.T_out - 1) * a.ldy + n0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float q[8], x1[8], x2[8];
+        if (r1) {
+          const uint32_t w[4] = {rv1[jj][h].x, rv1[jj][h].y, rv1[jj][h].z, rv1[jj][h].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            x1[2 * u] = __uint_as_float(w[u] << 16);
+            x1[2 * u + 1] = __uint_as_float(w[u] & 0xffff0000u);
+          }
+        }
+        if (r2) {
+          const uint32_t w[4] = {rv2[jj][h].x, rv2[jj][h].y, rv2[jj][h].z, rv2[jj][h].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            x2[2 * u] = __uint_as_float(w[u] << 16);
+            x2[2 * u + 1] = __uint_as_float(w[u] & 0xffff0000u);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = 2 * h + e / 4, r = e & 3;
+          float v = acc[i][j][r] + bias[8 * h + e];
+          v = tanh_act ? tanhf(v) : lrelu_max(v, ps);  // ps in [0, 1]
+          if (r1) v += x1[e];
+          v *= a.out_scale;
+          if (r2) v += x2[e];
+          q[e] = v;
+        }
+        if (pos < a.T_out) store8(Y + off + 8 * h, q);
+      }
+    }
+  }
+}
+
 template <typename TOUT, int NI, int NJ>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0, int co_blk,
                                               int wave_co0, int wave_t0, int lane) {
@@ -114,6 +187,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
   const int g = lane >> 4;
   const int n0 = co_blk + wave_co0 + NI * 4 * g;
   if (n0 >= a.Co) return;
+  if constexpr (std::is_same<TOUT, bf16_t>::value && NI % 2 == 0) {
+    // uniform per launch: plain conv, 8-element aligned rows, the lane's whole run inside Co
+    if (!a.transposed && (a.ldy & 7) == 0 && (a.ybs & 7) == 0 && a.Co % (4 * NI) == 0) {
+      conv_epilogue_vec<NI, NJ>(a, acc, b, t0, n0, wave_t0, lr);
+      return;
+    }
+  }
   TOUT* Y = reinterpret_cast<TOUT*>(a.y) + (int64_t)b * a.ybs;
   const TOUT* R1 = a.res1 ? reinterpret_cast<const TOUT*>(a.res1) + (int64_t)b * a.ybs : nullptr;
   const TOUT* R2 = a.res2 ? reinterpret_cast<const TOUT*>(a.res2) + (int64_t)b * a.ybs : nullptr;
@@ -226,8 +306,13 @@ __device__ __forceinline__ void wait_vmcnt() {
   if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 }
 
+// RS (with GL): the waves split the staging by role -- the first half issue every weight DMA piece,
+// the second half load and store every window chunk.  vmcnt is per wave and retires in issue order,
+// so a wave that waits for its weight DMA each step no longer drains the next chunk's window loads
+// (issued one chunk ahead, they got one step to land); and the step barriers are bare s_barrier
+// (LDS writes drained by lgkmcnt): __syncthreads' workgroup release fence waits vmcnt(0) too.
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -235,7 +320,13 @@ conv1d_kernel(ConvArgs a) {
   constexpr int BT = 16 * NJ * WT;
   constexpr int P = Lds<TC>::PITCH;
   constexpr int VPR = KC / 8;                 // 8-element vectors per row (4)
-  constexpr int MAXV = (((BT - 1) * S + 1 + HALO_MAX) * VPR + NT - 1) / NT;
+  constexpr bool DMA = GL && NICE && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0;
+  constexpr bool SPLIT = RS && DMA && (NT / 64) % 2 == 0;
+  constexpr int MAXV = SPLIT ? 1 : (((BT - 1) * S + 1 + HALO_MAX) * VPR + NT - 1) / NT;
+  // SPLIT: the window waves copy each chunk's window by LDS-DMA (XPW 1-KiB pieces per wave,
+  // lane-linear) into a raw staging area; at the chunk's end each lane applies the prologue
+  // activation to the 16 bytes it fetched and stores them into the swizzled window buffer
+  constexpr int XPW = SPLIT ? (((BT - 1) * S + 1 + HALO_MAX) * VPR + 64 * (NT / 128) - 1) / (64 * (NT / 128)) : 1;
   constexpr int WV = (TPS * BCO * VPR + NT - 1) / NT;
   constexpr int SHW = ilog2(4 * NI);
 
@@ -284,9 +375,10 @@ conv1d_kernel(ConvArgs a) {
   // out-of-range vectors are zeroed when they are written to LDS: a load under a divergent
   // branch gets an immediate s_waitcnt vmcnt(0) from the compiler, which serialised the
   // prefetch against HBM latency (seen in the ISA of the first version).
-  int xg[MAXV], xl[MAXV], xr[MAXV], xc[MAXV];  // xr: row-in-range flag
+  constexpr int MAXVA = MAXV;
+  int xg[MAXVA], xl[MAXVA], xr[MAXVA], xc[MAXVA];  // xr: row-in-range flag
 #pragma unroll
-  for (int s = 0; s < MAXV; ++s) {
+  for (int s = 0; s < MAXVA; ++s) {
     const int v = tid + s * NT;
     const int r = v / VPR, q = v % VPR;
     const int row = t0 * S - a.pad + r;
@@ -310,18 +402,24 @@ conv1d_kernel(ConvArgs a) {
   }
 
   Raw8<TIN> win_r[MAXV];
-  constexpr bool DMA = GL && NICE && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0;
   constexpr int NW = NT / 64;
-  constexpr int GLN = DMA ? (TPS * BCO * VPR) / NT : 1;  // DMA instructions per wave per step
-  static_assert(!DMA || (TPS * BCO * VPR) % NT == 0, "conv1d GL: a step's weights must split into whole wave-KiB");
+  constexpr int NWW = SPLIT ? NW / 2 : NW;  // waves issuing the weight DMA
+  constexpr int GLN = DMA ? (TPS * BCO * VPR) / (64 * NWW) : 1;  // DMA instructions per wave per step
+  static_assert(!DMA || (TPS * BCO * VPR) % (64 * NWW) == 0, "conv1d GL: a step's weights must split into whole wave-KiB");
   Raw8<TC> w_r[DMA ? 1 : WV];
-  bool win_ok[MAXV], w_ok[DMA ? 1 : WV];
-  int gl_t[GLN], gl_src[GLN];
+  bool win_ok[MAXVA], w_ok[DMA ? 1 : WV];
+  constexpr int GLNA = SPLIT ? 1 : GLN;
+  int gl_t[GLNA], gl_src[GLNA];
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  if constexpr (DMA) {
+  const int wave_w = wave_u % NWW;
+  // wave roles (uniform): SPLIT -> waves [0, NW/2) weights, [NW/2, NW) window; else every wave both
+  const bool wwave = !SPLIT || wave_u < NWW, xwave = !SPLIT || wave_u >= NWW;
+  const int wave_x = wave_u - NWW;  // SPLIT: window wave index
+  TC* const xraw = dummy + P;       // SPLIT: raw window pieces [NW - NWW][XPW][64 lanes][8]
+  if constexpr (DMA && !SPLIT) {
 #pragma unroll
     for (int s = 0; s < GLN; ++s) {
-      const int p = (s * NW + wave) * 64 + lane;  // LDS slot (16 B): tap t, row col, chunk q'
+      const int p = (s * NWW + wave_w) * 64 + lane;  // LDS slot (16 B): tap t, row col, chunk q'
       const int t = p / (BCO * VPR), rem = p - t * BCO * VPR;
       const int col = rem / VPR, qs = rem - col * VPR;
       const int q = qs ^ ((col >> (SHW - 1)) & 2);  // the swizzle of Lds<bf16_t>::off, on the source
@@ -334,11 +432,34 @@ conv1d_kernel(ConvArgs a) {
       typedef __attribute__((address_space(3))) void lds_void;
       typedef const __attribute__((address_space(1))) void g_void;
       const int c0 = ci_lo + c * KC;
+      if constexpr (SPLIT) {
+        // piece s = tap s / PPT, rows (s % PPT) * CSTEP + (wave_w * 64 + lane) / VPR; its swizzle
+        // bit does not depend on s, so one per-lane offset (opaque: not hoisted as GLN 64-bit
+        // addresses, which spilled) plus a scalar offset per piece
+        constexpr int PPT = BCO * VPR / (64 * NWW), CSTEP = 64 * NWW / VPR;
+        static_assert(GLN % PPT == 0 && CSTEP % (1 << SHW) == 0, "conv1d RS: whole taps per step, swizzle kept");
+        const int p0 = wave_w * 64 + lane, col0 = p0 / VPR;
+        int lane_off = (co_blk + col0) * a.Ci + ((p0 % VPR) ^ ((col0 >> (SHW - 1)) & 2)) * 8;
+        asm volatile("" : "+v"(lane_off));
+#pragma unroll
+        for (int s = 0; s < GLN; ++s) {
+          const int k = min(k0 + s / PPT, a.K - 1);  // taps >= K are skipped by the MFMA loop
+          const TC* src = Wp + (k * tap_stride + (s % PPT) * CSTEP * a.Ci + c0) + lane_off;
+          TC* dst = wt0 + buf * WSTRIDE + (s * NWW + wave_w) * 64 * 8;
+          __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+        }
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < GLN; ++s) {
-        const int k = min(k0 + gl_t[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
-        const TC* src = Wp + k * tap_stride + gl_src[s] + c0;
-        TC* dst = wt0 + buf * WSTRIDE + (s * NW + wave_u) * 64 * 8;
+        int gt, gsrc;
+        {
+          gt = gl_t[s];
+          gsrc = gl_src[s];
+        }
+        const int k = min(k0 + gt, a.K - 1);  // taps >= K are skipped by the MFMA loop
+        const TC* src = Wp + k * tap_stride + gsrc + c0;
+        TC* dst = wt0 + buf * WSTRIDE + (s * NWW + wave_w) * 64 * 8;
         __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
       }
     }
@@ -346,8 +467,22 @@ conv1d_kernel(ConvArgs a) {
 
   auto load_window = [&](int c) {
     const int c0 = ci_lo + c * KC;
+    if constexpr (SPLIT) {  // NICE: no channel bounds; rows clamped (zeroed by the LDS pass)
+      typedef __attribute__((address_space(3))) void lds_void;
+      typedef const __attribute__((address_space(1))) void g_void;
+      int lrow = lane / VPR;  // opaque per call (see load_w_dma)
+      asm volatile("" : "+v"(lrow));
+      const TIN* xq = X + (lane % VPR) * 8 + c0;
 #pragma unroll
-    for (int s = 0; s < MAXV; ++s) {
+      for (int s = 0; s < XPW; ++s) {
+        const int row = min(max(t0 * S - a.pad + (wave_x * XPW + s) * (64 / VPR) + lrow, 0), a.T_in - 1);
+        __builtin_amdgcn_global_load_lds((g_void*)(xq + (int64_t)row * a.ldx),
+                                         (lds_void*)(xraw + (wave_x * XPW + s) * 64 * 8), 16, 0, 0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < MAXVA; ++s) {
       win_ok[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
       if constexpr (ABL == 1) {
         if (c > 0) { win_r[s].zero(); continue; }
@@ -357,10 +492,29 @@ conv1d_kernel(ConvArgs a) {
   };
   auto store_window = [&](int buf) {
     TC* base = win0 + buf * win_stride;
+    if constexpr (SPLIT) {  // this wave's own DMA pieces (same lanes): no barrier needed first
+      wait_vmcnt<0>();
+#pragma unroll
+      for (int s = 0; s < XPW; ++s) {
+        const int v = (wave_x * XPW + s) * 64 + lane, r = v / VPR, row = t0 * S - a.pad + r;
+        Raw8<TIN> u;
+        u.load(reinterpret_cast<const TIN*>(xraw + v * 8));
+        if (!(row >= 0 && row < a.T_in)) u.zero();
+        float f[8];
+        u.to_f32(f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
+        store8(r < win_rows ? base + Lds<TC>::template off<2>(r, v % VPR) : dummy, f);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < MAXV; ++s) {  // branch-free: idle slots store to the dummy row
-      TC* dst = xl[s] >= 0 ? base + xl[s] : dummy;
-      if (!win_ok[s]) win_r[s].zero();
+      TC* dst;
+      {
+        dst = xl[s] >= 0 ? base + xl[s] : dummy;
+        if (!win_ok[s]) win_r[s].zero();
+      }
       if constexpr (std::is_same<TIN, TC>::value) {
         if (raw_window) {
           lds_put(dst, win_r[s]);
@@ -413,10 +567,10 @@ conv1d_kernel(ConvArgs a) {
   const int brow0 = wave_t0 + lr;
 
   // prologue
-  load_window(0);
+  if (xwave) load_window(0);
   load_w(0, 0);
-  load_w_dma(0, 0, 0);
-  store_window(0);
+  if (wwave) load_w_dma(0, 0, 0);
+  if (xwave) store_window(0);
   store_w(0);
   if constexpr (DMA) wait_vmcnt<0>();
   __syncthreads();
@@ -450,7 +604,26 @@ conv1d_kernel(ConvArgs a) {
   };
 
   int s = 0;
-  for (int c = 0; c < n_chunks; ++c) {
+  if constexpr (SPLIT) {
+    for (int c = 0; c < n_chunks; ++c) {
+      const bool more_chunks = c + 1 < n_chunks;
+      for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
+        if (wwave) load_w_dma(c, (tg + 1) * TPS, (s + 1) & 1);
+        if (xwave && tg == 0) load_window(min(c + 1, n_chunks - 1));
+        mfma_step(c, tg, s);
+        if (wwave) wait_vmcnt<0>();  // this wave's DMA pieces landed
+        lds_barrier();
+      }
+      if (wwave) load_w_dma(min(c + 1, n_chunks - 1), 0, (s + 1) & 1);
+      if (xwave && tsteps == 1) load_window(min(c + 1, n_chunks - 1));
+      mfma_step(c, tsteps - 1, s);
+      if (xwave && more_chunks) store_window((c + 1) & 1);
+      if (wwave) wait_vmcnt<0>();
+      lds_barrier();
+      ++s;
+    }
+  }
+  for (int c = 0; c < (SPLIT ? 0 : n_chunks); ++c) {
     const bool more_chunks = c + 1 < n_chunks;
     if constexpr (!DMA) load_window(min(c + 1, n_chunks - 1));  // a whole chunk of MFMAs ahead of its use
     for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
@@ -560,7 +733,7 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -583,13 +756,17 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   a.cig = d->Ci / groups;
   a.cog = d->Co / groups;
   const int win_rows = (BT - 1) * S + 1 + (d->K - 1) * d->dil;
-  const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO + 1) * Lds<TC>::PITCH * sizeof(TC);
+  const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
+  // role-split kernels (RS): + the raw window staging area of conv1d_kernel (XPW pieces per window wave)
+  constexpr bool SPL = RS && GL && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0 && (WCO * WT) % 2 == 0;
+  constexpr int NWX = WCO * WT / 2;
+  constexpr size_t RAW = SPL ? (size_t)((((BT - 1) * S + 1 + HALO_MAX) * (KC / 8) + 64 * NWX - 1) / (64 * NWX)) * NWX * 1024 : 0;
+  const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO + 1) * Lds<TC>::PITCH * sizeof(TC) + (nice ? RAW : 0);
   if (lds > 160 * 1024) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL>
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS>
                    : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
   a.partial = nullptr;
   a.kcs = 0;
@@ -614,9 +791,9 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
 }
 
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, bool GL = false>
+          int PRIO = 0, int ABL = 0, bool GL = false, bool RS = false>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
-  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL>(d, st);
+  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL, RS>(d, st);
 }
 
 // HiFi-GAN discriminator layers (strided and/or grouped, C5): 64-row tiles so that a stride-4
@@ -767,6 +944,13 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
         if (vo_tune_get("conv_cfg") == 2) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 3) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 4) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 3, 1, 1, 0, true>(d, st);
+        // Round 2: role-split staging (RS: half the waves issue the weight DMA, half copy the window by
+        // LDS-DMA; bare step barriers): k = 7 / 11 0.131 / 0.171 -> 0.127 / 0.165 ms, k = 3 0.082 ->
+        // 0.091 (its two-step chunks leave the window DMA one step) -- k >= 5 only; conv_cfg 5 forces it,
+        // 6 disables it (tools/probes/s0_probe.py, bit-identical)
+        const int cc = vo_tune_get("conv_cfg");
+        if (cc == 5 || (cc != 6 && d->K >= 5))
+          return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true, true>(d, st);
         return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true>(d, st);
       }
       case 2: return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 2>(d, st);

@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
   load_win(tile);
   store_win();
   if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
 
   f32x4 acc[NI][NJ];
   int gcount = 0;  // streamed groups consumed so far (selects the double buffer)
@@ -342,12 +342,12 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
       for (int c = 0; c < NC; ++c)
         for (int k = 0; k < K; ++k) tap(wls + k * TAPE + c * C * 32, win + c * win_rows * 32, brow0 + k * dil);
       if constexpr (IP) {  // T1 overwrites the window: every wave must be past its P1 reads
-        __syncthreads();
+        lds_barrier();
         p1_epilogue();
-        __syncthreads();
+        lds_barrier();
       } else {
         p1_epilogue();
-        __syncthreads();
+        lds_barrier();
         if (has_next) store_win();
       }
       const bf16_t* wb = wls + K * TAPE;
@@ -412,11 +412,11 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
         if (!IP && p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
         if (more) store_group((gcount + 1) & 1);
         if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed
-        __syncthreads();
+        lds_barrier();
         ++gcount;
         if (IP && p1_last) {  // every wave is past its window reads: T1 may overwrite them
           p1_epilogue();
-          __syncthreads();
+          lds_barrier();
         }
       };
       for (int g = 0; g < NG - 1; ++g) group(0, g, false, false);
@@ -503,10 +503,10 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
       for (int h = 0; h < NH; ++h)
         __builtin_amdgcn_raw_buffer_store_b128(yv[j][h], yrs, (r * C + n0 + 8 * h) * (int)sizeof(bf16_t), 0, 0);
     }
-    if constexpr (RES) __syncthreads();
+    if constexpr (RES) lds_barrier();
     if constexpr (IP) {  // P2's T1 reads ended at the last group barrier
       if (has_next) store_win();
-      __syncthreads();
+      lds_barrier();
     }
   }
 }

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
   for (int s = 0; s < MAXW; ++s) load_slot(s, tile);
   store_win();
   if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
 
   f32x4 acc[NI][NJ];
   int gc = 0;  // groups consumed (double-buffer parity)
@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       }
       store_group((gc + 1) & 1);
       if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      lds_barrier();
       ++gc;
     }
 
@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
         for (int i = 0; i < NI; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- P2: c2 over T1; the next tile's window slots [g SPG, (g + 1) SPG) are fetched in groups
     // g < NGW (unrolled: the slot registers need compile-time indices), the rest is a runtime loop
@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
           default: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
         }
       }
-      __syncthreads();
+      lds_barrier();
       ++gc;
     };
 #pragma unroll
@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       epilogue(std::true_type{});
     else
       epilogue(std::false_type{});
-    __syncthreads();  // the next window is visible before the next P1
+    lds_barrier();  // the next window is visible before the next P1
   }
 }
 

@@ -42,6 +42,16 @@ constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six conv
 // wait at a group's end leaves the younger NBUF - 2 groups in flight).
 template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
 __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
+  // streamed-weight blocks: bare LDS barriers (the fence of __syncthreads drains the window
+  // prefetch and the y stores at every group); resident-weight (C = 32) blocks keep
+  // __syncthreads -- without its vmcnt(0) that kernel ran 0.29 -> 0.40 ms (the next tile's loads
+  // queued behind the previous tile's y stores)
+  auto bar = [&]() {
+    if constexpr (RESW)
+      __syncthreads();
+    else
+      lds_barrier();
+  };
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
   constexpr int NC = C / 32;               // 32-channel planes
@@ -162,7 +172,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
   load_win(tile);
   store_win();
   if constexpr (!RESW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  bar();
 
   f32x4 acc[NI][NJ];
 #pragma unroll
@@ -231,13 +241,13 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
           // the next group's DMA (issued D - 1 groups ago) has landed for this wave; younger ones
           // stay in flight; the barrier publishes it and frees this group's buffer
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * GLN) : "memory");
-          __syncthreads();
+          bar();
           ++gcount;
         }
       }
       if (k != 2) continue;
       // ---- end of a conv: every wave is past its reads of the region
-      if constexpr (RESW) __syncthreads();
+      if constexpr (RESW) bar();
       if (s == 2 && ph == 1) break;  // the last conv's epilogue follows the loop (its window
                                      // registers must not be live around the loop)
       float bz[8 * NH];
@@ -297,7 +307,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
       for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (g + 1 < NG) __syncthreads();  // region rewritten: visible before the next conv reads it
+      if (g + 1 < NG) bar();  // region rewritten: visible before the next conv reads it
     }
     {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows
       float bz[8 * NH];
@@ -367,7 +377,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
     // next window (requested in the last epilogue) over the region (P2 of stage 2 ended its
     // region reads at the last barrier)
     if (has_next) store_win();
-    __syncthreads();
+    bar();
   }
 }
 

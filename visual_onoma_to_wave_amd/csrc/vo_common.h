@@ -37,6 +37,13 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 // are identical (a NaN input gives a NaN either way).
 __device__ __forceinline__ float lrelu_max(float v, float s) { return __builtin_elementwise_maximum(v, v * s); }
 
+// Workgroup barrier for LDS hand-offs: this wave's LDS operations drained, then s_barrier.
+// __syncthreads() adds a workgroup-scope release fence, and on gfx950 that fence waits vmcnt(0):
+// every outstanding global load or store of the wave (an epilogue's y stores, a prefetch meant to
+// stay in flight across the barrier) is drained at each barrier.  LDS-DMA destinations still
+// need their own vmcnt wait before this barrier; no global memory is handed between waves.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ---------------------------------------------------------------- 8-element vectors
 // Load 8 consecutive elements (16 B for bf16, 32 B for f32) as floats.
 __device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
