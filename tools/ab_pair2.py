@@ -5,6 +5,7 @@ against pair_cfg 0.
 
     python tools/ab_pair2.py "128:0,20,21" "64:0,20,21"
     python tools/ab_pair2.py "rb3:128,64,32"          # the fused k = 3 ResBlock (vo_resblock3)
+    AB_RB3_CFG=0,4 python tools/ab_pair2.py "rb3:128"  # rb3_cfg values (interleaved)
 
 Set VO_LIB_PATH to time another build of the library (tools/ab_libs.sh runs two builds).
 """
@@ -80,15 +81,18 @@ def rb3(B, C):
     w2 = [ops.pack_conv_weight(torch.randn(C, C, 3, device="cuda", generator=g) / (C * 3) ** 0.5, torch.bfloat16)
           for _ in range(3)]
     b = [torch.randn(C, device="cuda", generator=g) * 0.1 for _ in range(3)]
-    o = acc0.clone()
-    ops.resblock3(x, w1, b, w2, b, (1, 3, 5), 0.1, out=o, out_scale=1.0 / 3, acc=o)
-    chk = float(o.float().abs().sum())
-    y = acc0.clone()
-    fn = lambda: ops.resblock3(x, w1, b, w2, b, (1, 3, 5), 0.1, out=y, out_scale=1.0 / 3, acc=y)  # noqa: E731
-    fn()
-    t = min(timed(fn, 10) for _ in range(3))
     fl = 3 * 2 * 2.0 * B * T * C * C * 3
-    print(f"rb3 C={C}: {t:.4f} ms {fl / t / 1e9:.0f} TF/s checksum {chk:.6e}", flush=True)
+    for cfg in [int(c) for c in os.environ.get("AB_RB3_CFG", "0").split(",")]:
+        _lib.lib().vo_tune(b"rb3_cfg", cfg)
+        o = acc0.clone()
+        ops.resblock3(x, w1, b, w2, b, (1, 3, 5), 0.1, out=o, out_scale=1.0 / 3, acc=o)
+        chk = float(o.float().abs().sum())
+        y = acc0.clone()
+        fn = lambda: ops.resblock3(x, w1, b, w2, b, (1, 3, 5), 0.1, out=y, out_scale=1.0 / 3, acc=y)  # noqa: E731
+        fn()
+        t = min(timed(fn, 10) for _ in range(3))
+        print(f"rb3 C={C} [{cfg}]: {t:.4f} ms {fl / t / 1e9:.0f} TF/s checksum {chk:.6e}", flush=True)
+    _lib.lib().vo_tune(b"rb3_cfg", 0)
 
 
 if __name__ == "__main__":

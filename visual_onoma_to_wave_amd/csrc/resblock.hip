@@ -574,7 +574,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
   // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
   // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.
-  if ((C == 64 && cfg != 9 && cfg < 20) || cfg == 30 || cfg == 31) {
+  if ((C == 64 && cfg != 9 && (cfg < 20 || cfg == 32)) || cfg == 30 || cfg == 31) {
     int handled = 0;
     const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;

@@ -422,6 +422,11 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, true, 2>(a, B, st);
     return pair2_launch<64, 1, 8, 4, 11, true, 2>(a, B, st);
   }
+  if (cfg == 32) {  // two 4-wave workgroups of 256-row tiles per CU, register-staged weights:
+                    // 7-18 % slower (the doubled window registers per thread spill), round 2
+    if (K == 7) return pair2_launch<64, 1, 4, 4, 7, false, 2>(a, B, st);
+    return pair2_launch<64, 1, 4, 4, 11, false, 2>(a, B, st);
+  }
   if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2>(a, B, st);
   return pair2_launch<64, 1, 8, 4, 11, false, 2>(a, B, st);
 }

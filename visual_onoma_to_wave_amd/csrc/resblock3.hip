@@ -40,8 +40,10 @@ constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six conv
 // Streamed weights: a group is 1 / SPLIT of a tap (NC / SPLIT planes); NBUF group buffers form
 // a ring and each group's LDS-DMA is issued NBUF - 1 groups ahead (vmcnt is in-order, so the
 // wait at a group's end leaves the younger NBUF - 2 groups in flight).
+// 4-wave workgroups (WC * WT = 4) are sized for two per CU: one workgroup's epilogues, window
+// fetch and barriers overlap the other's MFMAs
 template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
-__global__ void __launch_bounds__(WC * WT * 64, 1) mrf_rb3_kernel(Rb3Args a) {
+__global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_kernel(Rb3Args a) {
   // streamed-weight blocks: bare LDS barriers (the fence of __syncthreads drains the window
   // prefetch and the y stores at every group); resident-weight (C = 32) blocks keep
   // __syncthreads -- without its vmcnt(0) that kernel ran 0.29 -> 0.40 ms (the next tile's loads
@@ -449,6 +451,12 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   if (C == 64) {
     if (cfg == 1) return rb3_launch<64, 1, 8, 2, false>(a, B, st);
     if (cfg == 4) return rb3_launch<64, 1, 8, 4, false, 1, 4>(a, B, st);
+    if (cfg == 5) return rb3_launch<64, 1, 4, 4, false>(a, B, st);
+    if (cfg == 7) return rb3_launch<64, 1, 4, 4, false, 1, 4>(a, B, st);
+    // cfg 6 / 7: two 4-wave workgroups of 256-row frames per CU with a 3- / 4-deep weight ring
+    // (round 2, bare LDS barriers): 0.53 -> 0.50 ms alone with the MRF accumulator
+    // (tools/ab_pair2.py), the same 12.40 / 12.46 ms bench step (s2 within noise) -- not default
+    if (cfg == 6) return rb3_launch<64, 1, 4, 4, false, 1, 3>(a, B, st);
     return rb3_launch<64, 1, 8, 4, false>(a, B, st);
   }
   if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
