@@ -465,7 +465,12 @@ conv1d_kernel(ConvArgs a) {
     }
   };
 
-  auto load_window = [&](int c) {
+  // SPLIT: two raw areas -- chunk c + 2's window is fetched while chunk c computes and chunk c + 1's
+  // lands; the pass at chunk c's end waits only for chunk c + 1 (vmcnt(XPW): the younger pieces of
+  // chunk c + 2 stay in flight), so each window DMA has a whole chunk or more to land
+  constexpr int XRAW = (NT / 128) * XPW * 64 * 8;  // elements per raw area
+  static_assert(!SPLIT || XPW <= 8, "conv1d RS: wait_vmcnt<XPW>");
+  auto load_window = [&](int c, int rb = 0) {
     const int c0 = ci_lo + c * KC;
     if constexpr (SPLIT) {  // NICE: no channel bounds; rows clamped (zeroed by the LDS pass)
       typedef __attribute__((address_space(3))) void lds_void;
@@ -477,7 +482,7 @@ conv1d_kernel(ConvArgs a) {
       for (int s = 0; s < XPW; ++s) {
         const int row = min(max(t0 * S - a.pad + (wave_x * XPW + s) * (64 / VPR) + lrow, 0), a.T_in - 1);
         __builtin_amdgcn_global_load_lds((g_void*)(xq + (int64_t)row * a.ldx),
-                                         (lds_void*)(xraw + (wave_x * XPW + s) * 64 * 8), 16, 0, 0);
+                                         (lds_void*)(xraw + rb * XRAW + (wave_x * XPW + s) * 64 * 8), 16, 0, 0);
       }
       return;
     }
@@ -490,15 +495,18 @@ conv1d_kernel(ConvArgs a) {
       win_r[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
     }
   };
-  auto store_window = [&](int buf) {
+  auto store_window = [&](int buf, int rb = 0, bool young = false) {
     TC* base = win0 + buf * win_stride;
     if constexpr (SPLIT) {  // this wave's own DMA pieces (same lanes): no barrier needed first
-      wait_vmcnt<0>();
+      if (young)
+        wait_vmcnt<XPW>();  // the next chunk's pieces (issued after these) may stay in flight
+      else
+        wait_vmcnt<0>();
 #pragma unroll
       for (int s = 0; s < XPW; ++s) {
         const int v = (wave_x * XPW + s) * 64 + lane, r = v / VPR, row = t0 * S - a.pad + r;
         Raw8<TIN> u;
-        u.load(reinterpret_cast<const TIN*>(xraw + v * 8));
+        u.load(reinterpret_cast<const TIN*>(xraw + rb * XRAW + v * 8));
         if (!(row >= 0 && row < a.T_in)) u.zero();
         float f[8];
         u.to_f32(f);
@@ -607,21 +615,24 @@ conv1d_kernel(ConvArgs a) {
   if constexpr (SPLIT) {
     for (int c = 0; c < n_chunks; ++c) {
       const bool more_chunks = c + 1 < n_chunks;
+      if (xwave) {  // chunk c's raw area was consumed at chunk c - 1's end
+        if (c == 0) load_window(min(1, n_chunks - 1), 1);
+        load_window(min(c + 2, n_chunks - 1), c & 1);
+      }
       for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
         if (wwave) load_w_dma(c, (tg + 1) * TPS, (s + 1) & 1);
-        if (xwave && tg == 0) load_window(min(c + 1, n_chunks - 1));
         mfma_step(c, tg, s);
         if (wwave) wait_vmcnt<0>();  // this wave's DMA pieces landed
         lds_barrier();
       }
       if (wwave) load_w_dma(min(c + 1, n_chunks - 1), 0, (s + 1) & 1);
-      if (xwave && tsteps == 1) load_window(min(c + 1, n_chunks - 1));
       mfma_step(c, tsteps - 1, s);
-      if (xwave && more_chunks) store_window((c + 1) & 1);
+      if (xwave && more_chunks) store_window((c + 1) & 1, (c + 1) & 1, true);
       if (wwave) wait_vmcnt<0>();
       lds_barrier();
       ++s;
     }
+    if (xwave) wait_vmcnt<0>();  // the clamped re-fetches of the last chunks land before the epilogue
   }
   for (int c = 0; c < (SPLIT ? 0 : n_chunks); ++c) {
     const bool more_chunks = c + 1 < n_chunks;
@@ -760,7 +771,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   // role-split kernels (RS): + the raw window staging area of conv1d_kernel (XPW pieces per window wave)
   constexpr bool SPL = RS && GL && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0 && (WCO * WT) % 2 == 0;
   constexpr int NWX = WCO * WT / 2;
-  constexpr size_t RAW = SPL ? (size_t)((((BT - 1) * S + 1 + HALO_MAX) * (KC / 8) + 64 * NWX - 1) / (64 * NWX)) * NWX * 1024 : 0;
+  constexpr size_t RAW = SPL ? 2 * (size_t)((((BT - 1) * S + 1 + HALO_MAX) * (KC / 8) + 64 * NWX - 1) / (64 * NWX)) * NWX * 1024 : 0;
   const size_t lds = (size_t)(2 * win_rows + 2 * TPS * BCO + 1) * Lds<TC>::PITCH * sizeof(TC) + (nice ? RAW : 0);
   if (lds > 160 * 1024) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
@@ -854,6 +865,8 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       // 256 x 256 for the wide convs.  In isolation (tools/probes/wide_convs.py,
       // profiles/r01j/wide_convs.txt) 256 co x 128 rows looked 11 % faster on FFN w_1, but in the
       // bench step its 12 decoder launches took 818 us against 584 (profiles/r01k/): kept out.
+      // ups0 (polyphase 512 -> 8 x 256, K = 2) on the role-split staging was 11-20 % slower (its
+      // one-step chunks: 8 weight-DMA pieces per weight wave per 2-tap step; tools/probes/ups0_probe.py)
       if (d->Co >= 768 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
     }
@@ -945,9 +958,10 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
         if (vo_tune_get("conv_cfg") == 3) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 4) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 3, 1, 1, 0, true>(d, st);
         // Round 2: role-split staging (RS: half the waves issue the weight DMA, half copy the window by
-        // LDS-DMA; bare step barriers): k = 7 / 11 0.131 / 0.171 -> 0.127 / 0.165 ms, k = 3 0.082 ->
-        // 0.091 (its two-step chunks leave the window DMA one step) -- k >= 5 only; conv_cfg 5 forces it,
-        // 6 disables it (tools/probes/s0_probe.py, bit-identical)
+        // LDS-DMA two chunks ahead; bare step barriers): k = 7 / 11 0.137 / 0.175 -> 0.130 / 0.168 ms,
+        // k = 3 0.084 -> 0.096 (two-step chunks: the weight waves' 8 DMA pieces per step, not the
+        // window, bind) -- k >= 5 only; conv_cfg 5 forces it, 6 disables it (tools/probes/s0_probe.py,
+        // bit-identical)
         const int cc = vo_tune_get("conv_cfg");
         if (cc == 5 || (cc != 6 && d->K >= 5))
           return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true, true>(d, st);
