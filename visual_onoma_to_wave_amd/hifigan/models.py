@@ -23,6 +23,18 @@ from .._base import HipModule
 LRELU_SLOPE = 0.1
 # K = 3 ResBlocks as one vo_resblock3 launch (VO_RB3=0: three vo_resblock_pair launches, for A/B)
 RB3_ENABLED = os.environ.get("VO_RB3", "1") != "0"
+# Conv-path MRF stages (C = 256: two conv launches per ResBlock iteration) run their ResBlock
+# chains on concurrent streams (VO_MRF_STREAMS=0: one after another, for A/B)
+MRF_STREAMS = os.environ.get("VO_MRF_STREAMS", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def _side_streams(device, n):
+    """n cached side streams of ``device`` (created once: stream creation is not free)."""
+    key = (str(device), n)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _SIDE_STREAMS[key]
 
 with warnings.catch_warnings():
     warnings.simplefilter("ignore")
@@ -81,9 +93,15 @@ class ResBlock(HipModule):
     def _build(self, device, dtype):
         return [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
 
-    def run(self, x, out=None, out_scale=1.0, accumulate=None, stage=None):
+    def fused(self, x):
+        """True when this ResBlock runs as fused pair / block launches (else two convs per pair)."""
+        return self.channels in self.fused_pair_channels and x.dtype == self.compute_dtype == torch.bfloat16
+
+    def run(self, x, out=None, out_scale=1.0, accumulate=None, stage=None, before_last=None):
         """x (B, T, C) channels-last -> ResBlock(x) * out_scale (+ accumulate), written to out.
-        ``stage`` (0..3) selects the MRF stage's own kernel instantiation and timer tag."""
+        ``stage`` (0..3) selects the MRF stage's own kernel instantiation and timer tag.
+        ``before_last`` (conv path only) is called right before the launch that reads
+        ``accumulate`` -- the MRF's concurrent chains order their accumulations there."""
         var = 0 if stage is None else stage + 1
         tag = None if stage is None else f"mrf_s{stage}"
         packs = self._packed(x.device, self._build)
@@ -109,6 +127,8 @@ class ResBlock(HipModule):
                            pre_slope=LRELU_SLOPE, post_act=ops.ACT_LRELU, post_slope=LRELU_SLOPE,
                            compute_dtype=self.compute_dtype, out_dtype=x.dtype, variant=var, tag=tag)
             last = n == len(self.dilation) - 1
+            if last and before_last is not None:
+                before_last()
             cur = ops.conv1d(t, w2, b2, Co=C, K=k, pad=get_padding(k, 1), res1=cur,
                              out=out if last else None, out_scale=out_scale if last else 1.0,
                              res2=accumulate if last else None, compute_dtype=self.compute_dtype,
@@ -182,13 +202,43 @@ class Generator(HipModule):
         # the stage's ResBlock launches are consecutive: one event pair for all of them
         grp = timer.group(tag) if (stage is not None and timer is not None and timer.watching(tag)) \
             else contextlib.nullcontext()
+        rbs = list(self.resblocks[i * self.num_kernels:(i + 1) * self.num_kernels])
+        for rb in rbs:
+            rb.compute_dtype = self.compute_dtype
         with grp:
-            for j in range(self.num_kernels):
-                rb = self.resblocks[i * self.num_kernels + j]
-                rb.compute_dtype = self.compute_dtype
-                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
-                       stage=stage)
+            if MRF_STREAMS and x.is_cuda and len(rbs) > 1 and not any(rb.fused(x) for rb in rbs):
+                self._mrf_concurrent(rbs, x, xs, stage)
+            else:
+                for j, rb in enumerate(rbs):
+                    rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
+                           stage=stage)
         return xs
+
+    def _mrf_concurrent(self, rbs, x, xs, stage):
+        """The MRF's ResBlock chains are independent until their sum: chain j runs on its own
+        stream, and only its last launch (the one that adds into ``xs``) waits for chain j - 1's
+        last launch, so the sum is formed in the same order as the sequential loop (bit-identical
+        output).  The C = 256 stage's convs are non-persistent two-round launches whose
+        residual / accumulator epilogues load HBM all at once; overlapping the chains lets one
+        chain's epilogue traffic run under another's MFMA work."""
+        main = torch.cuda.current_stream(x.device)
+        side = _side_streams(x.device, len(rbs) - 1)
+        chain_streams = [main] + side
+        for s in side:
+            s.wait_stream(main)  # x (and xs's allocation) are ordered on main
+            x.record_stream(s)
+            xs.record_stream(s)
+        done = [None] * len(rbs)
+        for j, (rb, s) in enumerate(zip(rbs, chain_streams)):
+            def before_last(j=j, s=s):
+                if j > 0:
+                    s.wait_event(done[j - 1])
+            with torch.cuda.stream(s):
+                rb.run(x, out=xs, out_scale=1.0 / self.num_kernels, accumulate=xs if j > 0 else None,
+                       stage=stage, before_last=before_last)
+                done[j] = torch.cuda.Event()
+                done[j].record(s)
+        main.wait_event(done[-1])  # chain j's completion implies chains < j (their last launches)
 
     def train_forward(self, mel_cl):
         """Differentiable forward for HiFi-GAN training (config C5): mel_cl (B, T, 80)
