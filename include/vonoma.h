@@ -315,6 +315,17 @@ int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);
 int vo_period_fold_bwd(const void* g, int dtype, int B, int T, int P, float* gwav, void* stream);
 int vo_wav_cl8_bwd(const void* g, int dtype, int64_t n, float* gwav, void* stream);
 int vo_avgpool_wav_bwd(const float* g, int B, int T, float* gx, void* stream);
+
+/* Weight normalisation over n layers per call (torch.nn.utils.weight_norm, dim = 0; the HiFi-GAN
+ * generator's and discriminators' weight-normed convs in C5 training -- replaces PyTorch's
+ * per-layer torch._weight_norm forward / backward kernels, hifigan/models.py:96-103,124-132 and
+ * the HiFi-GAN V1 discriminators).  Layer k: fp32 v[k] (rows[k] x len[k], contiguous), g[k]
+ * (rows[k]); forward w[k] = v * g / ||v_row||; backward from dw[k]: dv[k], dg[k].  The pointer
+ * and size tables are host arrays (copied into the kernel arguments, 24 layers per launch). */
+int vo_weight_norm(int n, const void* const* v, const void* const* g, void* const* w, const int* rows,
+                   const int* len, void* stream);
+int vo_weight_norm_bwd(int n, const void* const* v, const void* const* g, const void* const* dw, void* const* dv,
+                       void* const* dg, const int* rows, const int* len, void* stream);
 int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
                   int dtype, float* out, float* workspace, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,

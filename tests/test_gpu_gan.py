@@ -100,21 +100,28 @@ def test_gan_reductions_and_grads():
         assert rel_l2(ac.grad.cpu(), ar.grad) < 1e-6
 
 
-def _disc_params_mpd(mpd):
+def _ref_weight(m):
+    """The reference parameterisation on the CPU copy: torch's weight norm (the HIP path's
+    vo_weight_norm is GPU only), torch's spectral-norm hook."""
     from visual_onoma_to_wave_amd.hifigan.discriminators import effective_weight
+    if hasattr(m, "weight_g"):
+        return torch._weight_norm(m.weight_v, m.weight_g, 0)
+    return effective_weight(m)
+
+
+def _disc_params_mpd(mpd):
     out = []
     for d in mpd.discriminators:
         ms = list(d.convs) + [d.conv_post]
-        out.append(([effective_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
+        out.append(([_ref_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
     return out
 
 
 def _disc_params_msd(msd):
-    from visual_onoma_to_wave_amd.hifigan.discriminators import effective_weight
     out = []
     for d in msd.discriminators:
         ms = list(d.convs) + [d.conv_post]
-        out.append(([effective_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
+        out.append(([_ref_weight(m).detach().cpu() for m in ms], [m.bias.detach().cpu() for m in ms]))
     return out
 
 

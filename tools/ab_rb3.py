@@ -46,10 +46,15 @@ def main():
                                         out_scale=1.0 / 3 if s == 2 else 1.0, acc=acc if s == 2 else None)
         fl = 3 * 2 * 2.0 * B * T * C * C * 3
         line = f"C={C} T={T}: 3 pairs {t_ms(pairs):.4f} ms"
+        ref = None
         for c in cfgs:
             _lib.lib().vo_tune(b"rb3_cfg", c)
+            ops.resblock3(x, p1, b1, p2, b2, dils, 0.1, out=y, out_scale=1.0 / 3, acc=acc)
+            if ref is None:
+                ref = y.clone()
+            same = "==" if torch.equal(y, ref) else "DIFF"
             ms = t_ms(lambda: ops.resblock3(x, p1, b1, p2, b2, dils, 0.1, out=y, out_scale=1.0 / 3, acc=acc))
-            line += f" | rb3[{c}] {ms:.4f} ms {fl / ms / 1e9:.0f} TF/s {4 * x.numel() * 2 / ms / 1e6:.0f} GB/s(4 passes)"
+            line += f" | rb3[{c}]{same} {ms:.4f} ms {fl / ms / 1e9:.0f} TF/s {4 * x.numel() * 2 / ms / 1e6:.0f} GB/s(4 passes)"
         _lib.lib().vo_tune(b"rb3_cfg", 0)
         print(line, flush=True)
 

@@ -47,7 +47,9 @@ def effective_weight(m):
     """The weight a weight-normed / spectral-normed conv would use in this forward (torch
     parameterisation math: w = g v / ||v||, or the power-iteration sigma in training mode)."""
     if hasattr(m, "weight_g"):
-        return torch._weight_norm(m.weight_v, m.weight_g, 0)
+        # the same kernel as the batched training path (vo_weight_norm): the packed-weight cache is
+        # keyed on parameter versions only, so every path must derive bit-identical weights
+        return G.weight_norm_all([m])[m]
     for hook in m._forward_pre_hooks.values():
         if isinstance(hook, SpectralNorm):
             hook(m, None)
@@ -64,6 +66,20 @@ def _weight(m):
     if wkey is None or (torch.is_grad_enabled() and p.requires_grad):
         return effective_weight(m)
     return G._cached(wkey, "w_eff", lambda: effective_weight(m).detach())
+
+
+def _batched_weights(root):
+    """Effective weights of every weight-normed conv under ``root`` in one batched call while the
+    discriminator is being trained (autograd records and its parameters require grad); {} otherwise
+    (the frozen G-step path keeps the per-module cache of ``_weight``)."""
+    mods = [m for m in root.modules() if hasattr(m, "weight_g")]
+    if not (torch.is_grad_enabled() and any(m.weight_v.requires_grad for m in mods)):
+        return {}
+    return G.weight_norm_all(mods)
+
+
+def _w(m, W):
+    return W[m] if W and m in W else _weight(m)
 
 
 class _DiscBase(nn.Module):
@@ -100,17 +116,20 @@ class DiscriminatorP(_DiscBase):
         specs.append(G.ConvSpec(K=k, pad=2, post="lrelu", post_slope=LRELU_SLOPE))
         return specs, G.ConvSpec(K=3, pad=1, co_pad=4)
 
-    def forward(self, wav):
-        """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)])."""
+    def forward(self, wav, W=None):
+        """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)]).  ``W``: effective
+        weights batched by the caller (``_batched_weights``)."""
         cdt, adt = self.compute_dtype, self._act_dtype()
+        if W is None:
+            W = _batched_weights(self)
         x = G.PeriodFoldFn.apply(wav, self.period, adt)
         specs, post = self._specs()
         fmap = []
         for m, sp in zip(self.convs, specs):
-            x = G.conv(x, _weight(m)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
+            x = G.conv(x, _w(m, W)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, _weight(m)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
+        y = G.conv(x, _w(m, W)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap
@@ -126,10 +145,11 @@ class MultiPeriodDiscriminator(_DiscBase):
         batch (one launch per layer for both)."""
         B = y.shape[0]
         both = torch.cat([y, y_hat], 0)
+        W = _batched_weights(self)
         rs, gs, frs, fgs = [], [], [], []
         for d in self.discriminators:
             p = d.period
-            s, fm = d(both)
+            s, fm = d(both, W)
             rs.append(s[: B * p])
             gs.append(s[B * p:])
             frs.append([f[: B * p] for f in fm])
@@ -149,18 +169,20 @@ class DiscriminatorS(_DiscBase):
             self.convs = nn.ModuleList(norm_f(Conv1d(ci, co, k, s, groups=g, padding=p)) for ci, co, k, s, g, p in cfg)
             self.conv_post = norm_f(Conv1d(1024, 1, 3, 1, padding=1))
 
-    def forward(self, wav):
+    def forward(self, wav, W=None):
         """wav (B, T) fp32 -> (score (B, T'), fmaps [(B, T_l, C_l)])."""
         cdt, adt = self.compute_dtype, self._act_dtype()
+        if W is None:
+            W = _batched_weights(self)
         x = G.WavCl8Fn.apply(wav, adt)
         fmap = []
         for m, (ci, co, k, s, g, p) in zip(self.convs, self.cfg):
             sp = G.ConvSpec(K=k, pad=p, stride=s, groups=g, post="lrelu", post_slope=LRELU_SLOPE,
                             ci_pad=8 if ci == 1 else None)
-            x = G.conv(x, _weight(m), m.bias, sp, cdt, wkey=G.weight_key(m))
+            x = G.conv(x, _w(m, W), m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
         m = self.conv_post
-        y = G.conv(x, _weight(m), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
+        y = G.conv(x, _w(m, W), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
         score = y[..., 0].contiguous()
         fmap.append(score)
         return score, fmap
@@ -175,11 +197,12 @@ class MultiScaleDiscriminator(_DiscBase):
     def forward(self, y, y_hat):
         B = y.shape[0]
         x = torch.cat([y, y_hat], 0)
+        W = _batched_weights(self)
         rs, gs, frs, fgs = [], [], [], []
         for i, d in enumerate(self.discriminators):
             if i != 0:
                 x = G.AvgPoolFn.apply(x)
-            s, fm = d(x)
+            s, fm = d(x, W)
             rs.append(s[:B])
             gs.append(s[B:])
             frs.append([f[:B] for f in fm])

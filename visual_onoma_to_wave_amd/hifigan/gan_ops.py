@@ -26,6 +26,7 @@ Backward, per op:
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
+import os
 import weakref
 
 import torch
@@ -338,6 +339,48 @@ class ConvFn(torch.autograd.Function):
 def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None):
     """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged."""
     return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey)
+
+
+class WeightNormFn(torch.autograd.Function):
+    """w_k = g_k v_k / ||v_k|| (torch._weight_norm(v, g, 0)) for n layers in one launch per 24 layers,
+    forward and backward (vo_weight_norm / vo_weight_norm_bwd): the per-layer PyTorch kernels were
+    ~270 launches per C5 step.  apply(n, v_1..v_n, g_1..g_n) -> (w_1..w_n)."""
+
+    @staticmethod
+    def forward(ctx, n, *vg):
+        vs, gs = [t.detach() for t in vg[:n]], [t.detach() for t in vg[n:]]
+        ctx.n = n
+        ctx.save_for_backward(*vg)
+        return tuple(ops.weight_norm(vs, gs))
+
+    @staticmethod
+    def backward(ctx, *dws):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        vs, gs = [t.detach() for t in saved[:n]], [t.detach() for t in saved[n:]]
+        dws = [torch.zeros_like(v) if d is None else d.float().contiguous() for d, v in zip(dws, vs)]
+        dvs, dgs = ops.weight_norm_bwd(vs, gs, dws)
+        return (None, *dvs, *dgs)
+
+
+# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)
+BATCHED_WN = os.environ.get("VO_BATCHED_WN", "1") != "0"
+
+
+def weight_norm_all(mods):
+    """{module: effective weight} of weight-normed convs (``weight_v`` / ``weight_g``), batched:
+    differentiable through WeightNormFn while autograd records, a plain vo_weight_norm otherwise."""
+    mods = [m for m in mods if hasattr(m, "weight_g")]
+    if not mods:
+        return {}
+    if not BATCHED_WN:
+        return {m: torch._weight_norm(m.weight_v, m.weight_g, 0) for m in mods}
+    vs, gs = [m.weight_v for m in mods], [m.weight_g for m in mods]
+    if torch.is_grad_enabled() and any(p.requires_grad for p in vs + gs):
+        ws = WeightNormFn.apply(len(mods), *vs, *gs)
+    else:
+        ws = ops.weight_norm([v.detach() for v in vs], [g.detach() for g in gs])
+    return dict(zip(mods, ws))
 
 
 class PeriodFoldFn(torch.autograd.Function):

@@ -245,13 +245,17 @@ class Generator(HipModule):
         channels-last -> wav (B, 256 T) fp32.  Same HIP conv kernels as ``run`` (pre-lrelu while
         staging, residual and MRF sum in the epilogue), one launch per conv (the fused pair
         kernel has no backward), gradients through ``gan_ops.ConvFn``; the weight-norm
-        reparameterisation w = g v / ||v|| is differentiated by torch."""
+        reparameterisation w = g v / ||v|| of every conv runs as one batched HIP launch
+        (``gan_ops.WeightNormFn``, forward and backward)."""
         from . import gan_ops as G
         dt = self.compute_dtype
         adt = torch.float32 if dt == torch.float32 else torch.bfloat16
 
+        # every weight-normed conv's w = g v / ||v|| in one batched launch (and one in the backward)
+        W = G.weight_norm_all(list(self.modules()))
+
         def wgt(m):
-            return torch._weight_norm(m.weight_v, m.weight_g, 0) if hasattr(m, "weight_g") else m.weight
+            return W[m] if m in W else m.weight
 
         x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, G.ConvSpec(K=7, pad=3), dt,
                    wkey=G.weight_key(self.conv_pre))

@@ -682,6 +682,54 @@ def period_fold_bwd(g, B, T, period):
     return gw
 
 
+def _ptr_table(ts):
+    return ctypes.cast((ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts]), ctypes.c_void_p)
+
+
+def _wn_check(vs, gs):
+    if len(vs) != len(gs):
+        raise ValueError("weight_norm: as many g as v")
+    for v, g in zip(vs, gs):
+        _contig(v, "v")
+        _contig(g, "g")
+        if v.dtype != torch.float32 or g.dtype != torch.float32:
+            raise ValueError("weight_norm: fp32 v and g")
+        if g.numel() != v.shape[0] or v.device != vs[0].device:
+            raise ValueError(f"weight_norm: g {tuple(g.shape)} vs v {tuple(v.shape)} (one gain per row of dim 0)")
+    rows = [v.shape[0] for v in vs]
+    lens = [v.numel() // v.shape[0] for v in vs]
+    return (ctypes.c_int * len(vs))(*rows), (ctypes.c_int * len(vs))(*lens)
+
+
+def weight_norm(vs, gs):
+    """w_k = g_k * v_k / ||v_k||, norms over every dim but 0 (torch._weight_norm(v, g, 0)), for a list
+    of layers in one launch per 24 layers (vo_weight_norm) -> list of w."""
+    if not vs:
+        return []
+    rows, lens = _wn_check(vs, gs)
+    ws = [torch.empty_like(v) for v in vs]
+    _lib.check(_lib.lib().vo_weight_norm(len(vs), _ptr_table(vs), _ptr_table(gs), _ptr_table(ws), rows, lens,
+                                          _stream(vs[0])), "vo_weight_norm")
+    return ws
+
+
+def weight_norm_bwd(vs, gs, dws):
+    """Backward of ``weight_norm``: lists of dL/dw -> (dL/dv list, dL/dg list)."""
+    if not vs:
+        return [], []
+    rows, lens = _wn_check(vs, gs)
+    for v, d in zip(vs, dws):
+        _contig(d, "dw")
+        if d.shape != v.shape or d.dtype != torch.float32:
+            raise ValueError("weight_norm_bwd: dw must match v (fp32)")
+    dvs = [torch.empty_like(v) for v in vs]
+    dgs = [torch.empty_like(g) for g in gs]
+    _lib.check(_lib.lib().vo_weight_norm_bwd(len(vs), _ptr_table(vs), _ptr_table(gs), _ptr_table(dws),
+                                              _ptr_table(dvs), _ptr_table(dgs), rows, lens, _stream(vs[0])),
+               "vo_weight_norm_bwd")
+    return dvs, dgs
+
+
 def wav_cl8_bwd(g):
     """Adjoint of ``wav_cl8``: g (B, T, 8) -> (B, T) fp32 (channel 0)."""
     _contig(g, "g")
