@@ -307,6 +307,12 @@ int vo_pack_grouped(const float* src, int Co, int Ci, int K, int groups, int Ci_
                     int dst_dtype, void* stream);
 int vo_pack_grouped_blocks(const float* src, int Co, int Ci, int K, int groups, int Ci_pad, void* dst,
                            int dst_dtype, void* stream);
+/* Input-gradient weights of one stride phase r of a strided / grouped conv: w (Co, Ci/groups, K) fp32
+ * -> dst [J][ci_out][co_in], dst[t][ci][co] = w[co][ci mod cig][k_r + S (J - 1 - t)] within a group,
+ * 0 elsewhere (blocks_only: the diagonal blocks only, other entries left as they are).  Replaces
+ * the transpose / flip / pack chain of the HiFi-GAN discriminators' backward (C5). */
+int vo_pack_dgrad_phase(const float* w, int Co, int cig, int K, int groups, int S, int k_r, int J, int ci_out,
+                        int co_in, int blocks_only, void* dst, int dst_dtype, void* stream);
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
 int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
 int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);

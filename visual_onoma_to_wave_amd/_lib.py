@@ -128,6 +128,8 @@ _SIGNATURES = {
     "vo_period_fold_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "vo_wav_cl8_bwd": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "vo_avgpool_wav_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "vo_pack_dgrad_phase": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_void_p, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_weight_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),

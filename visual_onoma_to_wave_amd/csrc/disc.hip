@@ -51,6 +51,36 @@ __global__ void __launch_bounds__(256) pack_grouped_blocks_kernel(const float* _
   }
 }
 
+// Input-gradient weights of one stride phase of a strided / grouped conv (hifigan/gan_ops._dgrad):
+// from w (Co, cig, K) fp32 straight to the packed [J][Ci_out][Co_in] layout of the stride-1 grouped
+// conv over dY -- tap t <- k_r + S (J - 1 - t) (the phase's taps reversed), channel roles swapped
+// per group -- replacing a transpose copy, a zero-row concat, a flip and the grouped pack.
+// BLOCKS: write only the diagonal blocks (a persistent buffer zeroed once); else every entry.
+template <typename TD, bool BLOCKS>
+__global__ void __launch_bounds__(256) pack_dgrad_phase_kernel(const float* __restrict__ w, int Co, int cig, int K,
+                                                               int groups, int S, int k_r, int J, int ci_out,
+                                                               int co_in, TD* __restrict__ dst) {
+  const int Ci = cig * groups, cog = Co / groups;
+  const int64_t n = BLOCKS ? (int64_t)J * Ci * cog : (int64_t)J * ci_out * co_in;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int t, ci, cc;
+    if constexpr (BLOCKS) {
+      const int c = (int)(i % cog);
+      const int64_t r = i / cog;
+      ci = (int)(r % Ci); t = (int)(r / Ci);
+      cc = (ci / cig) * cog + c;
+    } else {
+      cc = (int)(i % co_in);
+      const int64_t r = i / co_in;
+      ci = (int)(r % ci_out); t = (int)(r / ci_out);
+    }
+    float v = 0.f;
+    if (BLOCKS || (ci < Ci && cc < Co && cc / cog == ci / cig))
+      v = w[((int64_t)cc * cig + (ci - (ci / cig) * cig)) * K + k_r + S * (J - 1 - t)];
+    dst[((int64_t)t * ci_out + ci) * co_in + cc] = from_f32<TD>(v);
+  }
+}
+
 // wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
 // reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
 template <typename TD>
@@ -355,6 +385,28 @@ extern "C" int vo_pack_grouped_blocks(const float* src, int Co, int Ci, int K, i
   else
     hipLaunchKernelGGL(pack_grouped_blocks_kernel<float>, dim3(g), dim3(256), 0, st, src, Co, cig, cog, K, Ci_pad,
                        (float*)dst);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_pack_dgrad_phase(const float* w, int Co, int cig, int K, int groups, int S, int k_r, int J,
+                                   int ci_out, int co_in, int blocks_only, void* dst, int dst_dtype, void* stream) {
+  VO_CHECK_ARG(w && dst, "pack_dgrad_phase: null pointer");
+  VO_CHECK_ARG(groups >= 1 && Co % groups == 0 && cig >= 1 && K >= 1 && S >= 1 && k_r >= 0 && J >= 1 &&
+                   k_r + S * (J - 1) < K && ci_out >= cig * groups && co_in >= Co,
+               "pack_dgrad_phase: bad sizes Co=%d cig=%d K=%d groups=%d S=%d k_r=%d J=%d ci_out=%d co_in=%d", Co, cig,
+               K, groups, S, k_r, J, ci_out, co_in);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = blocks_only ? (int64_t)J * cig * groups * (Co / groups) : (int64_t)J * ci_out * co_in;
+  const int g = grid_for(n);
+#define VO_PDP(TD, B)                                                                                          \
+  hipLaunchKernelGGL((pack_dgrad_phase_kernel<TD, B>), dim3(g), dim3(256), 0, st, w, Co, cig, K, groups, S, k_r, \
+                     J, ci_out, co_in, (TD*)dst)
+  if (dst_dtype == VO_BF16) {
+    if (blocks_only) VO_PDP(bf16_t, true); else VO_PDP(bf16_t, false);
+  } else {
+    if (blocks_only) VO_PDP(float, true); else VO_PDP(float, false);
+  }
+#undef VO_PDP
   VO_RETURN_LAUNCH();
 }
 

@@ -179,15 +179,8 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
     cog, Ci = Co // g, cig * g
     # dgrad conv weight (Ci, Co / g, K): per group the (cog x cig) blocks transposed
     ci_out = x.shape[-1]  # >= Ci (1-channel inputs padded to 8)
-    wt_box = []
-
-    def wt_get():
-        if not wt_box:
-            wt = w.detach().float().reshape(g, cog, cig, K).transpose(1, 2).reshape(Ci, cog, K)
-            if ci_out > Ci:
-                wt = torch.cat([wt, wt.new_zeros((ci_out - Ci, cog, K))])
-            wt_box.append(wt)
-        return wt_box[0]
+    if ci_out > Ci and g != 1:
+        raise NotImplementedError("strided / grouped input gradient: padded input channels with groups")
     gzp = _pad_channels(gz.to(cdt))
     co_in = gzp.shape[-1]  # >= Co (Co = 1 padded to 8); extra channels multiply zero weights
     B, T_in = x.shape[0], x.shape[1]
@@ -206,11 +199,11 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
         c_r = (r + pad - k_r) // S
         tag = (spec, cdt, "dgrad", r, ci_out, co_in)
 
-        def build(k_r=k_r, tag=tag):
-            # tap t <- k_r + S (J - 1 - t); a strided slice + flip (list indexing would copy the
-            # index list host -> device, which a HIP-graph capture refuses)
-            wsel = wt_get()[:, :, k_r::S].flip(-1).contiguous()
-            return _pack_grouped(wsel, cdt, g if ci_out == Ci else 1, co_in, _slot_fn(wkey, tag))
+        def build(k_r=k_r, tag=tag, J=J):
+            # tap t <- k_r + S (J - 1 - t), channel roles swapped per group: one packing launch
+            slot = _slot_fn(wkey, tag)
+            out = None if slot is None else slot((J, ci_out, co_in), cdt, w.device)
+            return ops.pack_dgrad_phase(w, g, S, k_r, J, ci_out, co_in, cdt, out=out)
         wp = _cached(wkey, tag, build)
         ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,
                    groups=g if ci_out == Ci else 1)

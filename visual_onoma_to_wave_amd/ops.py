@@ -641,6 +641,23 @@ def pack_grouped_weight(w, dtype, groups=1, ci_pad=None, out=None):
     return out
 
 
+def pack_dgrad_phase(w, groups, S, k_r, J, ci_out, co_in, dtype, out=None):
+    """Stride phase k_r of a strided / grouped conv's input gradient: w (Co, Ci/groups, K) -> packed
+    [J][ci_out][co_in] (taps k_r + S (J - 1 - t), channel roles swapped per group, zero padding).
+    ``out``: a persistent buffer of that shape, zero outside the diagonal blocks (only they are written)."""
+    w = w.detach().float().contiguous()
+    Co, cig, K = w.shape
+    shape = (J, ci_out, co_in)
+    if out is not None:
+        if tuple(out.shape) != shape or out.dtype != dtype or not out.is_contiguous():
+            raise ValueError(f"pack_dgrad_phase: out {tuple(out.shape)} {out.dtype}, expected contiguous {shape} {dtype}")
+    dst = out if out is not None else torch.empty(shape, dtype=dtype, device=w.device)
+    _lib.check(_lib.lib().vo_pack_dgrad_phase(_ptr(w), Co, cig, K, groups, S, k_r, J, ci_out, co_in,
+                                              1 if out is not None else 0, _ptr(dst), vo_dtype(dtype), _stream(w)),
+               "vo_pack_dgrad_phase")
+    return dst
+
+
 def period_fold(wav, period, dtype):
     """wav (B, T) fp32 -> (B * period, ceil(T / period), 8) channels-last (MPD input)."""
     _contig(wav, "wav")
