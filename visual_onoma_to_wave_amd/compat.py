@@ -8,9 +8,24 @@ internally ``import transformer``, ``import hifigan``).  ``install()`` registers
 package's modules under all of those names, so the callers run unchanged:
 
     import visual_onoma_to_wave_amd.compat as c; c.install()
+
+The hot-path names of ``utils.tools`` / ``utils.model`` (``to_device``,
+``get_mask_from_lengths``, ``pad``, ``expand``, ``get_model``, ``vocoder_infer`` ...) are this
+package's.  The callers also import helpers that are not on the path and are not built here --
+``log`` / ``synth_one_sample`` (``scripts/04_train.py:12``, ``scripts/evaluate.py:10``) and
+``plot_mel`` (``prediction.ipynb:215``), TensorBoard logging and matplotlib plotting.  Those
+resolve to the CALLER'S OWN definitions: a name the build's module lacks is looked up in the
+caller's ``scripts/utils/<module>.py``, executed once as a private module
+(``utils._caller_tools``) whose relative imports (``from .model import vocoder_infer``,
+``tools.py:224``) land on this package again.  The caller's tree is found from
+``install(caller_root=...)``, ``$VO_CALLER_ROOT``, the working directory (the reference runs
+from its repo root: ``scripts/hifigan/config.json`` is cwd-relative, ``utils/model.py:57``) or a
+``.../scripts`` entry of ``sys.path`` (``04_train.py`` runs with its own directory first).
 """
 
 import importlib
+import importlib.util
+import os
 import sys
 
 _PKG = __name__.rsplit(".", 1)[0]
@@ -38,9 +53,19 @@ _MAP = {
     "dataset": "dataset",
 }
 
+_caller_root = None          # set by install(caller_root=...)
+_caller_mods = {}            # "utils.tools" -> the caller's module (executed once)
 
-def install(prefixes=("", "scripts.")):
-    """Alias ``<prefix><name>`` -> ``visual_onoma_to_wave_amd.<name>`` in sys.modules."""
+
+def install(prefixes=("", "scripts."), caller_root=None):
+    """Alias ``<prefix><name>`` -> ``visual_onoma_to_wave_amd.<name>`` in sys.modules.
+
+    ``caller_root``: the reference checkout whose ``scripts/`` tree supplies the non-path
+    helpers (default: ``$VO_CALLER_ROOT``, the cwd, or a ``scripts`` dir on ``sys.path``)."""
+    global _caller_root
+    if caller_root is not None:
+        _caller_root = os.fspath(caller_root)
+    _caller_mods.clear()
     if "scripts." in prefixes and "scripts" not in sys.modules:
         import types
         pkg = types.ModuleType("scripts")
@@ -57,3 +82,60 @@ def install(prefixes=("", "scripts.")):
             if parent and parent in sys.modules:
                 setattr(sys.modules[parent], leaf, mod)
     return sys.modules[_PKG]
+
+
+def _scripts_dirs():
+    """Candidate ``scripts/`` directories of the caller's checkout, in priority order."""
+    roots = [r for r in (_caller_root, os.environ.get("VO_CALLER_ROOT"), os.getcwd()) if r]
+    out = [os.path.join(r, "scripts") for r in roots]
+    out += [p for p in sys.path if p and os.path.basename(os.path.normpath(p)) == "scripts"]
+    pkg_dir = os.path.dirname(os.path.abspath(__file__))
+    seen, res = set(), []
+    for d in out:
+        d = os.path.abspath(d)
+        if d not in seen and not d.startswith(pkg_dir):
+            seen.add(d)
+            res.append(d)
+    return res
+
+
+def _load_caller(modname):
+    """Execute the caller's own ``scripts/<modname>.py`` once as ``<pkg>._caller_<leaf>``."""
+    if modname in _caller_mods:
+        return _caller_mods[modname]
+    rel = modname.replace(".", os.sep) + ".py"
+    path = next((os.path.join(d, rel) for d in _scripts_dirs()
+                 if os.path.isfile(os.path.join(d, rel))), None)
+    mod = None
+    if path is not None:
+        pkg, _, leaf = modname.rpartition(".")
+        # relative imports of the caller's file ("from .model import vocoder_infer") resolve
+        # against the aliased package, i.e. back onto this build
+        if pkg and pkg not in sys.modules and f"scripts.{pkg}" in sys.modules:
+            pkg = f"scripts.{pkg}"
+        name = f"{pkg}._caller_{leaf}" if pkg else f"_caller_{leaf}"
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        try:
+            spec.loader.exec_module(mod)
+        except BaseException:
+            del sys.modules[name]
+            raise
+    _caller_mods[modname] = mod
+    return mod
+
+
+def caller_attr(modname, name):
+    """``name`` from the caller's own ``scripts/<modname>.py`` (module ``__getattr__`` hook of
+    ``utils.tools`` / ``utils.model``); AttributeError when the caller's tree lacks it."""
+    if name.startswith("__"):
+        raise AttributeError(name)
+    mod = _load_caller(modname)
+    if mod is None or not hasattr(mod, name):
+        raise AttributeError(
+            f"module '{modname}' has no attribute '{name}': it is not on the synthesis path "
+            f"(not built by {_PKG}) and no caller tree provides it (looked in "
+            f"{[os.path.join(d, modname.replace('.', os.sep) + '.py') for d in _scripts_dirs()]}; "
+            f"pass compat.install(caller_root=...) or set VO_CALLER_ROOT)")
+    return getattr(mod, name)

@@ -86,3 +86,10 @@ def vocoder_infer(mels, vocoder, model_config, preprocess_config, lengths=None, 
         for i in range(len(mels)):
             wavs[i] = wavs[i][: lengths[i]]
     return wavs
+
+
+def __getattr__(name):
+    """Names the build does not provide come from the caller's own ``scripts/utils/model.py``
+    (see ``compat``)."""
+    from .. import compat
+    return compat.caller_attr("utils.model", name)

@@ -119,3 +119,11 @@ def pad(input_ele, mel_max_length=None):
         y[: min(n, max_len)] = x[: min(n, max_len)]
         out.append(y)
     return torch.stack(out)
+
+
+def __getattr__(name):
+    """Names off the synthesis path (``log``, ``synth_one_sample``, ``plot_mel`` ...,
+    ``tools.py:140-241,541-582``) come from the caller's own ``scripts/utils/tools.py``
+    (see ``compat``)."""
+    from .. import compat
+    return compat.caller_attr("utils.tools", name)
