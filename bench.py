@@ -66,6 +66,9 @@ def parse():
                     help="gan: weight of the auxiliary multi-resolution STFT loss (0 = HiFi-GAN V1 losses only)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="train / gan under torchrun: gradient all-reduce dtype")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group, the ranks are "
+                         "all-gathered and rank 0 prints them (no model, no CUDA call)")
     ap.add_argument("--mode", default="infer", choices=["infer", "c2", "c3", "train", "gan"],
                     help="infer: end-to-end synthesis (headline, with C2 / C3 sub-lines); c2: acoustic model "
                          "only; c3: HiFi-GAN generator only (B=64); train: C4 training step (DDP); "
@@ -326,7 +329,8 @@ def bench_train(a, dev, rank, world, dist):
     if rank == 0:
         print(json.dumps({
             "metric": "C4 training mel-frames/sec (FastSpeech2 + variance loss, DDP)", "value": round(frames / elapsed, 1),
-            "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "unit": "mel-frames/s", "n_gpus": world, "ranks_seen": a.ranks_seen, "steps": a.steps,
+            "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
             "final_loss": round(float(losses[0].detach()) if torch.is_tensor(losses[0]) else float(losses[0]), 5), "hip_graph": graphed,
@@ -370,7 +374,8 @@ def bench_gan(a, dev, rank, world, dist):
     if rank == 0:
         print(json.dumps({
             "metric": "C5 HiFi-GAN training audio samples/sec (G + MPD + MSD, DDP)", "value": round(samples / elapsed, 1),
-            "unit": "audio samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "unit": "audio samples/s", "n_gpus": world, "ranks_seen": a.ranks_seen, "steps": a.steps,
+            "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16" if a.precision != "fp32" else "f32",
             "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
@@ -382,10 +387,89 @@ def bench_gan(a, dev, rank, world, dist):
                        "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D, {a.comm_dtype})"}}))
 
 
+# ----------------------------------------------------------------------------------- launch
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``--gpus N`` without a torchrun environment: start N rank processes of this script (one
+    per GPU, LOCAL_RANK = rank, rendezvous on 127.0.0.1) and exit with the worst exit code.
+    Runs before anything touches the GPU; the ranks are children, never an exec of this
+    process.  Rank 0's stdout carries the JSON line."""
+    import signal
+    import subprocess
+    if "--dry-run" not in sys.argv:
+        n_dev = torch.cuda.device_count()  # does not initialise the HIP runtime on this image
+        if n > n_dev:
+            sys.exit(f"bench.py: --gpus {n} but only {n_dev} GPU(s) visible")
+    env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for r in range(n):
+        env_r = dict(env, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env_r))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:          # one rank failed: the others would hang in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        raise
+    return rc
+
+
+def rank_census(dist, world, rank, local, dev):
+    """All-gather (rank, local_rank) of every process: the ranks the collective layer saw."""
+    if dist is None:
+        return [0]
+    t = torch.tensor([rank, local], dtype=torch.int64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [int(p[0]) for p in parts]
+
+
+def dry_run(a):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    try:
+        seen = rank_census(dist, world, rank, local, "cpu")
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "mode": a.mode, "gpus_requested": a.gpus,
+                              "n_gpus": dist.get_world_size() if dist else 1, "ranks_seen": seen}))
+    finally:
+        if dist:
+            dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------------------------- main
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    if a.dry_run:
+        return dry_run(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -395,6 +479,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
+    a.ranks_seen = rank_census(dist, world, rank, local, dev)
 
     try:
         if a.mode == "gan":
@@ -404,7 +490,7 @@ def main():
         elif a.mode in ("c2", "c3"):
             res = (measure_c2 if a.mode == "c2" else measure_c3)(a, dev, dist)
             if rank == 0:
-                res.update({"n_gpus": world, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                res.update({"n_gpus": world, "ranks_seen": a.ranks_seen, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
                             "scaling": "weak", "vs_baseline": None,
                             "dtype": {"mixed": "bf16 (encoder+variance adaptor fp32)", "bf16": "bf16",
                                       "fp32": "f32"}[a.precision] if a.mode == "c2" else
@@ -468,7 +554,8 @@ def infer(a, dev, rank, world, dist):
     if rank == 0:
         line = {
             "metric": "end-to-end audio samples/sec (22.05 kHz) + mel-frames/sec, batch 32, 1->8 GPU",
-            "value": round(value, 1), "unit": "audio samples/s", "n_gpus": world, "steps": a.steps,
+            "value": round(value, 1), "unit": "audio samples/s", "n_gpus": world, "ranks_seen": a.ranks_seen,
+            "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": {"mixed": "bf16 (encoder+variance adaptor fp32)", "bf16": "bf16", "fp32": "f32"}[a.precision],
