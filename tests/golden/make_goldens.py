@@ -267,10 +267,53 @@ def long_goldens():
         save("generator_long", mel=mel, wav=t2n(gen(torch.from_numpy(mel))))
 
 
+def stft_goldens():
+    """Round 3: the reference's own Tacotron STFT front end (scripts/audio/stft.py:52-81 STFT.transform,
+    :159-178 TacotronSTFT.mel_spectrogram, audio_processing.py:85-91 dynamic_range_compression) run
+    on CPU: ``Tensor.cuda`` is patched to the identity for the call (stft.py:68-69 hard-codes
+    ``.cuda()``), ``pad_center`` is the identity (win_length == filter_length, stft.py:41-42), and
+    the window is scipy's ``get_window("hann", 1024, fftbins=True)`` as the reference computes it.
+    librosa is absent, so the mel basis fed to ``mel_spectrogram`` is the oracle's restatement of
+    ``librosa.filters.mel`` (slaney): the basis itself stays parity-unpinned, everything around it
+    -- DFT-basis magnitude, basis product, log compression, energy -- is the reference's code.
+    Two wav lengths (one full second, one ragged), B = 2, signals in [-1, 1]."""
+    import torch
+    import audio.stft as ref_stft
+    from oracle.mel import librosa_mel
+    ref_stft.pad_center = lambda w, size: w if len(w) == size else np.pad(
+        w, ((size - len(w)) // 2, size - len(w) - (size - len(w)) // 2))
+    ref_stft.librosa_mel_fn = lambda sr, n_fft, n_mels, fmin, fmax: librosa_mel(sr, n_fft, n_mels, fmin, fmax)
+    tac = ref_stft.TacotronSTFT(1024, 256, 1024, 80, 22050, 0.0, 8000.0)
+    rng = np.random.default_rng(31)
+    real_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        for name, N in (("stft_ref_22050", 22050), ("stft_ref_9001", 9001)):
+            t = np.arange(N) / 22050.0
+            f0 = rng.uniform(80, 2000, size=(2, 1))
+            wav = (0.5 * np.sin(2 * np.pi * f0 * t) + 0.2 * np.sin(2 * np.pi * 3.1 * f0 * t)
+                   + 0.1 * rng.standard_normal((2, N)))
+            wav = np.clip(wav, -1, 1).astype(np.float32)
+            with torch.no_grad():
+                mag, _ = tac._stft_fn.transform(torch.from_numpy(wav))
+                mel, energy = tac.mel_spectrogram(torch.from_numpy(wav))
+                drc = ref_stft.dynamic_range_compression(mag)
+            save(name, wav=wav, window=np.asarray(ref_stft.get_window("hann", 1024, fftbins=True), np.float32),
+                 mel_basis=t2n(tac.mel_basis), magnitude=t2n(mag), log_magnitude=t2n(drc), mel=t2n(mel),
+                 energy=t2n(energy))
+    finally:
+        torch.Tensor.cuda = real_cuda
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["long"]:
         import_reference()
         long_goldens()
+    elif sys.argv[1:] == ["stft"]:
+        import_reference()
+        import utils.tools  # noqa: F401  (imports the reference's audio package as main() does)
+        stft_goldens()
     else:
         main()
         long_goldens()
+        stft_goldens()

@@ -210,3 +210,38 @@ def test_synthesis_pipeline_matches_sequential(vtts, gen):
     assert pipe.pending() == 0
     for r, g in zip(ref, got):
         assert torch.equal(r, g.cpu())
+
+
+def test_synthesis_pipeline_inputs_straight_from_to_device(vtts, gen, device):
+    """The serving path as a caller writes it: ``to_device`` lays each glyph batch out with a kernel
+    on the caller's stream (vo_glyph_batch) right before ``submit`` -- with the caller's stream kept
+    busy, so that kernel is still queued when the acoustic stream starts -- and the caller drops its
+    input tensors at once.  Batch for batch bit-identical to the sequential path."""
+    from visual_onoma_to_wave_amd import synth
+    from visual_onoma_to_wave_amd.pipeline import SynthesisPipeline
+    from visual_onoma_to_wave_amd.utils.tools import to_device
+    vtts.set_precision("mixed")
+    gen.set_compute_dtype(torch.bfloat16)
+    datas = []
+    for seed in (21, 22, 23):
+        b = synth.acoustic_batch(seed, 32, 12, 512, ragged=True)
+        strips = [np.round(im[0] * 255.0).astype(np.uint8) for im in b["images"]]   # padded 'L' strips
+        datas.append((None, b["audiotypes"], b["texts"], b["src_lens"], b["max_src_len"], b["mels"],
+                      b["mel_lens"], b["max_mel_len"], None, None, b["d_targets"], strips, None))
+    with torch.no_grad():
+        ref = []
+        for d in datas:
+            t = to_device(d, device)
+            torch.cuda.synchronize()
+            ref.append(gen.run(vtts(*(t[1:]), True)[1]).cpu())
+        pipe = SynthesisPipeline(vtts, gen)
+        got = []
+        for i, d in enumerate(datas):
+            torch.cuda._sleep(40_000_000)          # ~20 ms of spinning ahead of to_device's kernel
+            pipe.submit(*(to_device(d, device)[1:]), True)   # inputs dropped right after submit
+            if i:
+                got.append(pipe.next_wav()[1])
+        got.append(pipe.next_wav()[1])
+        torch.cuda.synchronize()
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g.cpu())

@@ -66,3 +66,26 @@ def test_weight_norm_rejects_bad_tables(device):
         ops.weight_norm([v], [torch.ones(3, device="cuda")])  # one gain per row of dim 0
     with pytest.raises(ValueError):
         ops.weight_norm([v.transpose(1, 2)], [torch.ones(4, device="cuda")])  # contiguous only
+
+
+def test_weight_norm_unaligned_outputs(device):
+    """The public C ABI takes any fp32 pointers: outputs offset by one float (not 16-byte aligned)
+    must take the scalar path (the float4 predicate covers w, dw and dv too)."""
+    from visual_onoma_to_wave_amd import _lib, ops
+    v, g = _layers(3, 2)[1]                             # (128, 32, 5, 1): 160-float rows
+    rows, lens = ops._wn_check([v], [g])
+    wbuf = torch.full((v.numel() + 1,), float("nan"), device="cuda")
+    w = wbuf[1:].view_as(v)
+    _lib.check(_lib.lib().vo_weight_norm(1, ops._ptr_table([v]), ops._ptr_table([g]), ops._ptr_table([w]), rows,
+                                          lens, ops._stream(v)), "vo_weight_norm")
+    assert rel(w, torch._weight_norm(v, g, 0)) < 1e-6
+    dw = torch.randn_like(v)
+    dvbuf = torch.full((v.numel() + 1,), float("nan"), device="cuda")
+    dv = dvbuf[1:].view_as(v)
+    dg = torch.empty_like(g)
+    _lib.check(_lib.lib().vo_weight_norm_bwd(1, ops._ptr_table([v]), ops._ptr_table([g]), ops._ptr_table([dw]),
+                                              ops._ptr_table([dv]), ops._ptr_table([dg]), rows, lens, ops._stream(v)),
+               "vo_weight_norm_bwd")
+    vr, gr = v.clone().requires_grad_(True), g.clone().requires_grad_(True)
+    torch._weight_norm(vr, gr, 0).backward(dw)
+    assert rel(dv, vr.grad) < 1e-5 and rel(dg, gr.grad) < 1e-5

@@ -1,5 +1,13 @@
-"""Mel / STFT front-end (row a21).  PARITY-UNPINNED against the reference's own libraries
-(torchaudio / librosa are not installed and no reference file holds their outputs): the
+"""Mel / STFT front-end (row a21).
+
+Pinned (round 3): the STFT magnitude, its log compression and the Tacotron mel composition
+(basis product, ``dynamic_range_compression``, energy) against the reference's OWN code --
+``scripts/audio/stft.py:52-81`` ``STFT.transform`` and ``:159-178`` ``TacotronSTFT.mel_spectrogram``,
+``audio_processing.py:85-91`` -- run on CPU by ``tests/golden/make_goldens.py stft``
+(goldens ``stft_ref_22050`` / ``stft_ref_9001``): the oracle (CPU) and the HIP kernels (GPU)
+are both checked against them, magnitude rel-L2 <= 1e-5 (fp32).
+PARITY-UNPINNED: the mel filterbanks themselves (torchaudio ``MelScale`` and
+``librosa.filters.mel`` are not installed and no reference file holds their outputs): the
 oracle restates their published algorithms and is cross-checked here against an independent
 float64 DFT; the HIP kernel is checked against the oracle.
 
@@ -78,3 +86,62 @@ def test_tacotron_stft_vs_oracle():
     ref = [M.tacotron_mel(torch.from_numpy(w)) for w in wav]
     _check(mel, energy, torch.stack([r[0] for r in ref]), torch.stack([r[1] for r in ref]))
     assert mel.shape == (2, 80, 51)
+
+
+# ------------------------------------------------------------- pinned to the reference's STFT code
+
+REF_STFT = ["stft_ref_22050", "stft_ref_9001"]
+
+
+def _ref(name):
+    from helpers import golden
+    return golden(name)
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.mark.parametrize("name", REF_STFT)
+def test_oracle_pinned_to_reference_stft(name):
+    """Oracle |STFT| (torch.stft, periodic Hann) == the reference's DFT-basis conv magnitude."""
+    g = _ref(name)
+    np.testing.assert_allclose(g["window"], torch.hann_window(1024, periodic=True).numpy(), atol=5e-7)
+    mag = M.magnitude(torch.from_numpy(g["wav"])).numpy()
+    assert mag.shape == g["magnitude"].shape
+    assert _rel(mag, g["magnitude"]) < 1e-5
+    mel = np.log(np.maximum(np.einsum("mk,bkf->bmf", g["mel_basis"].astype(np.float64), mag), 1e-5))
+    ok = g["mel"] > np.log(1e-3)
+    assert np.abs(mel - g["mel"])[ok].max() < 2e-3
+    np.testing.assert_allclose(np.linalg.norm(mag, axis=1), g["energy"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", REF_STFT)
+def test_stft_magnitude_vs_reference(name):
+    """vo_stft_mag (LDS FFT) against STFT.transform's magnitude, and its log compression against
+    dynamic_range_compression's."""
+    from visual_onoma_to_wave_amd import ops
+    g = _ref(name)
+    wav = torch.from_numpy(g["wav"]).cuda()
+    mag = ops.stft_mag(wav, torch.from_numpy(g["window"]).cuda(), 1024, 256, eps=0.0)
+    mag = mag.transpose(1, 2).cpu().numpy()                      # (B, bins, frames) as the reference
+    assert mag.shape == g["magnitude"].shape
+    assert _rel(mag, g["magnitude"]) < 1e-5
+    drc = np.log(np.maximum(mag, 1e-5))
+    ok = g["magnitude"] > 1e-3
+    assert np.abs(drc - g["log_magnitude"])[ok].max() < 2e-3
+    assert np.abs(drc - g["log_magnitude"]).max() < 5e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", REF_STFT)
+def test_tacotron_mel_vs_reference(name):
+    """The HIP mel front end with the reference's composition: TacotronSTFT.mel_spectrogram on the
+    same mel basis (the basis itself is the oracle's librosa restatement, unpinned)."""
+    from visual_onoma_to_wave_amd.audio import MelSpectrogram
+    g = _ref(name)
+    m = MelSpectrogram(1024, 256, 80, fb=torch.from_numpy(g["mel_basis"]).t().contiguous())
+    mel, energy = m(torch.from_numpy(g["wav"]).cuda())
+    _check(mel, energy, torch.from_numpy(g["mel"]), torch.from_numpy(g["energy"]))

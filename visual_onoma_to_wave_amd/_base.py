@@ -21,11 +21,19 @@ import torch.nn as nn
 _GENERATION = [0]
 
 
-def invalidate_packs():
-    """Drop every module's packed-weight cache.  HIP-graph replays of a training step update
-    parameters in place without bumping their version counters, so the graphed steps call this
-    after each replay (and after capture)."""
-    _GENERATION[0] += 1
+def invalidate_packs(*modules):
+    """Drop the packed-weight caches of ``modules`` (and their HIP submodules); with no argument,
+    of every module in the process.  HIP-graph replays of a training step update parameters in
+    place without bumping their version counters, so the graphed steps call this for the modules
+    they train after each replay (and after capture) -- inference modules living in the same
+    process (a vocoder, a SynthesisPipeline) keep their packs."""
+    if not modules:
+        _GENERATION[0] += 1
+        return
+    for root in modules:
+        for m in root.modules():
+            if isinstance(m, HipModule):
+                m.__dict__["_pack_gen"] = m.__dict__.get("_pack_gen", 0) + 1
 
 
 class HipModule(nn.Module):
@@ -37,7 +45,7 @@ class HipModule(nn.Module):
 
     def _packed(self, device, builder, dtype=None):
         dtype = dtype or self.compute_dtype
-        key = (str(device), dtype, _GENERATION[0], self._params_version())
+        key = (str(device), dtype, _GENERATION[0], self.__dict__.get("_pack_gen", 0), self._params_version())
         cache = self.__dict__.setdefault("_pack_cache", {})
         hit = cache.get("key")
         if hit != key:

@@ -43,8 +43,10 @@ __global__ void __launch_bounds__(256) weight_norm_kernel(WnArgs a) {
   const int64_t base = (int64_t)r * len;
   const float* v = L.v + base;
   // 16-byte vectors when the row allows it (row starts stay 16-byte aligned iff len % 4 == 0)
+  // (every pointer the vector path reads or writes: v and w forward; v, dw and dv backward)
   const bool vec = (len & 3) == 0 && (reinterpret_cast<uintptr_t>(L.v) & 15) == 0 &&
-                   (!BWD || (reinterpret_cast<uintptr_t>(L.dw) & 15) == 0);
+                   (BWD ? ((reinterpret_cast<uintptr_t>(L.dw) | reinterpret_cast<uintptr_t>(L.dv)) & 15) == 0
+                        : (reinterpret_cast<uintptr_t>(L.w) & 15) == 0);
   float ss = 0.f, dot = 0.f;
   const float* dw = BWD ? L.dw + base : nullptr;
   if (vec) {

@@ -21,7 +21,7 @@ import itertools
 import torch
 
 from .. import _base
-from ..train import GradBucketer, TrainState, _check_graph_runtime, quiesce_collectives
+from ..train import GradBucketer, TrainState, _capture_ctx, _check_graph_runtime, _warmup_ctx
 from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiResolutionSTFTLoss, MultiScaleDiscriminator,
                              discriminator_loss, feature_loss, generator_loss)
 
@@ -159,25 +159,23 @@ class HifiGanTrainer:
             snap = TrainState([self.generator, self.mpd, self.msd], [self.optim_g, self.optim_d])
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(side), _warmup_ctx([self.bk_g, self.bk_d]):
                 for _ in range(warmup):
                     self.step(self._x, self._y)
             torch.cuda.current_stream().wait_stream(side)
-            if self.bk_g is not None:
-                quiesce_collectives()
             gan_ops.reset_pack_cache()
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with _capture_ctx([self.bk_g, self.bk_d]), torch.cuda.graph(graph):
                 self._out = self.step(self._x, self._y)
             snap.restore()
             gan_ops.reset_pack_cache()
-            _base.invalidate_packs()
+            _base.invalidate_packs(self.generator, self.mpd, self.msd)
             self._graph = graph
         self._x.copy_(x_mel_cl)
         self._y.copy_(y)
         self._graph.replay()
         gan_ops.reset_pack_cache()  # replays move the parameters without bumping their versions
-        _base.invalidate_packs()
+        _base.invalidate_packs(self.generator, self.mpd, self.msd)
         return self._out
 
     def end_epoch(self):

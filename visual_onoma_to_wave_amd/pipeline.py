@@ -5,9 +5,15 @@ runs on the caller's stream.
 The acoustic model (``scripts/model/vtts.py:47-119``) is a chain of small, latency-bound kernels
 at T_src = 12 / T_mel = 512 (2 ms for B = 32 alone, far from filling 256 CUs); the vocoder
 (``scripts/hifigan/models.py:149-165``) fills the chip.  Overlapping them hides part of the
-former behind the latter (bench.py: 13.67 -> 13.06 ms per B = 32 step).  Each submitted batch's
-mel reaches the vocoder through an event; its memory is recorded on the vocoder stream so the
-caching allocator does not hand it out while the vocoder still reads it.
+former behind the latter (bench.py: 13.67 -> 13.06 ms per B = 32 step).
+
+Stream ordering.  ``submit`` first makes the acoustic stream wait for the caller's stream, so
+inputs the caller produced there just before (``utils.tools.to_device`` lays glyph batches out
+with a kernel on the current stream) are complete before the model reads them, and records every
+CUDA input on the acoustic stream, so the caching allocator does not hand an input's memory out
+while the acoustic model still reads it, even if the caller drops it right after ``submit``.
+Each submitted batch's mel reaches the vocoder through an event; its memory is recorded on the
+vocoder stream likewise.
 """
 
 import collections
@@ -26,6 +32,11 @@ class SynthesisPipeline:
         self._pending = collections.deque()
 
     def submit(self, *model_args):
+        caller = torch.cuda.current_stream(self.device)
+        self.acoustic_stream.wait_stream(caller)
+        for a in model_args:
+            if torch.is_tensor(a) and a.is_cuda:
+                a.record_stream(self.acoustic_stream)
         with torch.cuda.stream(self.acoustic_stream):
             out = self.model(*model_args)
             ev = torch.cuda.Event()

@@ -29,8 +29,8 @@ runtime initialises, so import this package -- or export the variable -- before 
 call); ``GraphedTrainStep`` refuses to run when it is not in effect.
 """
 
+import contextlib
 import os
-import time
 
 import torch
 import torch.distributed as dist
@@ -39,7 +39,10 @@ from . import _base
 
 
 def packet_capture_disabled():
-    return os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+    """True when the HIP runtime read DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 at its initialisation: the
+    variable is "0" and it was not first set by this package after torch had initialised CUDA."""
+    import visual_onoma_to_wave_amd as _pkg
+    return os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0" and not _pkg.PACKET_CAPTURE_SET_LATE
 
 
 class GradBucketer:
@@ -83,8 +86,38 @@ class GradBucketer:
         backend = dist.get_backend(group)
         self.avg = backend == "nccl"  # RCCL averages on the wire; gloo sums, then we scale
         self.side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self.device = dev
+        self.local_only = False      # warm-up before a capture: no collective at all
+        self.capture_group = None    # the group the captured collectives run on (see capturing())
         self.hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
         self.reset()
+
+    @contextlib.contextmanager
+    def warmup(self):
+        """Steps run inside skip the collectives (each rank keeps its own gradients): the eager
+        warm-up steps before a HIP-graph capture, whose updates ``TrainState`` undoes anyway.
+        Everything else -- hooks, gathers into the buckets, the side stream -- runs as usual, so
+        the warm-up still exercises the allocator and the pack caches the capture will use."""
+        prev, self.local_only = self.local_only, True
+        try:
+            yield self
+        finally:
+            self.local_only = prev
+
+    @contextlib.contextmanager
+    def capturing(self):
+        """Collectives issued inside go to a process group that only ever carries captured
+        collectives (``graph_group``).  An eager collective still in the watchdog's list of
+        in-flight works when a capture begins has its end event on its group's stream; if the
+        capture joins that stream the watchdog's query of the event aborts the process
+        ("operation not permitted on an event last recorded in a capturing stream").  The graph
+        group never has an eager work, so no such race exists -- whatever the timing."""
+        prev = self.capture_group
+        self.capture_group = graph_group(self.group, self.device)
+        try:
+            yield self
+        finally:
+            self.capture_group = prev
 
     def reset(self):
         self.pending = [len(b) for b in self.buckets]
@@ -128,10 +161,13 @@ class GradBucketer:
         self.launched[i] = True
 
     def _reduce(self, i, buf):
-        if self.avg:
-            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
+        group = self.capture_group if self.capture_group is not None else self.group
+        if self.local_only:
+            pass
+        elif self.avg:
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
         else:
-            dist.all_reduce(buf, group=self.group)
+            dist.all_reduce(buf, group=group)
             buf.div_(self.world)
         if buf is not self.flat[i]:
             self.flat[i].copy_(buf)
@@ -216,19 +252,51 @@ class TrainState:
                             v.zero_()
 
 
-def quiesce_collectives(seconds=0.5):
-    """Before a capture that contains RCCL collectives: wait for the device, then give the
-    process group's watchdog thread (it polls its list of in-flight works every ~100 ms) time to
-    retire the warm-up steps' collectives.  An eager work still listed when the capture starts has
-    its end event on the communicator's stream, which the capture then joins; the watchdog's
-    event query on it fails ("operation not permitted on an event last recorded in a capturing
-    stream") and aborts the process -- a race we met once in the world-size-1 RCCL test."""
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        torch.cuda.synchronize()
-        time.sleep(seconds)
+_GRAPH_GROUPS = {}
+
+
+def graph_group(group, device):
+    """A process group over the same ranks as ``group`` reserved for collectives captured in HIP
+    graphs (created once per (group, device), on every rank at the same point: the first capture).
+    With the default group bound to a device (``init_process_group(..., device_id=dev)``) the new
+    RCCL communicator is split off eagerly, so no communicator is created inside a capture.
+    gloo groups are returned unchanged (gloo collectives cannot be captured)."""
+    if dist.get_backend(group) != "nccl":
+        return group
+    key = (id(group), str(device))
+    if key not in _GRAPH_GROUPS:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        dev = device if getattr(dist.distributed_c10d._get_default_group(), "bound_device_id", None) else None
+        _GRAPH_GROUPS[key] = dist.new_group(ranks=ranks, backend="nccl", device_id=dev,
+                                            group_desc="vo_graph_collectives")
+    return _GRAPH_GROUPS[key]
+
+
+def _warmup_ctx(bucketers):
+    stack = contextlib.ExitStack()
+    for b in bucketers:
+        if b is not None:
+            stack.enter_context(b.warmup())
+    return stack
+
+
+def _capture_ctx(bucketers):
+    stack = contextlib.ExitStack()
+    for b in bucketers:
+        if b is not None:
+            stack.enter_context(b.capturing())
+    return stack
 
 
 def _check_graph_runtime():
+    import visual_onoma_to_wave_amd as _pkg
+    if _pkg.PACKET_CAPTURE_SET_LATE:
+        raise RuntimeError(
+            "HIP-graph training: visual_onoma_to_wave_amd was imported after torch had initialised the HIP "
+            "runtime, so its DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 setting came too late to take effect. Import the "
+            "package (or export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0) before the first CUDA call, e.g. before "
+            "torch.cuda.set_device(local_rank); with the CLR packet-capture launch path replays of the training "
+            "step compute wrong values (DESIGN.md section 7)")
     if not packet_capture_disabled():
         raise RuntimeError(
             "HIP-graph training needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in effect when the HIP runtime "
@@ -271,19 +339,17 @@ class GraphedTrainStep:
         step0 = self.opt.current_step
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), _warmup_ctx([self.bucketer]):
             for _ in range(self.warmup):
                 self.opt._update_learning_rate()
                 self._body(self.static)
         torch.cuda.current_stream().wait_stream(side)
-        if self.bucketer is not None:
-            quiesce_collectives()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with _capture_ctx([self.bucketer]), torch.cuda.graph(self.graph):
             self.out = self._body(self.static)
         snap.restore()  # the warm-up updates are undone: the first replay is the first update
         self.opt.current_step = step0
-        _base.invalidate_packs()
+        _base.invalidate_packs(self.model)
 
     def __call__(self, batch):
         if self.graph is None:
@@ -295,7 +361,7 @@ class GraphedTrainStep:
                 raise ValueError("GraphedTrainStep: non-tensor batch entries are fixed at capture")
         self.opt._update_learning_rate()
         self.graph.replay()
-        _base.invalidate_packs()  # replays move the parameters without bumping their versions
+        _base.invalidate_packs(self.model)  # replays move the parameters without bumping their versions
         return self.out
 
 
