@@ -22,6 +22,15 @@ PAIRS = {"pair_s1_k3": (128, 32768, 3, 1), "pair_s1_k7": (128, 32768, 7, 3), "pa
 def main(names, iters=5, B=32):
     dev = torch.device("cuda")
     for name in names:
+        if name == "dec_ffn_w1":  # C2 decoder FFN w_1 (transformer/SubLayers.py:85-93): 256 -> 1024, k 9, relu
+            x = torch.randn(B, 512, 256, device=dev).to(torch.bfloat16)
+            w = ops.pack_conv_weight(torch.randn(1024, 256, 9, device=dev) / (256 * 9) ** 0.5, torch.bfloat16)
+            bias = torch.zeros(1024, device=dev)
+            y = torch.empty(B, 512, 1024, device=dev, dtype=torch.bfloat16)
+            for _ in range(iters):
+                ops.conv1d(x, w, bias, Co=1024, K=9, pad=4, post_act=ops.ACT_RELU, out=y, compute_dtype=torch.bfloat16)
+            torch.cuda.synchronize()
+            continue
         if name in PAIRS:
             C, T, k, d = PAIRS[name]
             x = torch.randn(B, T, C, device=dev).to(torch.bfloat16)

@@ -7,7 +7,7 @@ pass).  Per MI355X_MICROARCH.md section HBM: both are KB; on gfx950 FETCH_SIZE r
 half the bytes of a wide coalesced streaming read, so it is doubled.  Result:
 {"mrf_s<i>": {"hbm_bytes_per_launch", "fetch_bytes", "write_bytes", "launches"}}.
 
-    python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json [FETCH2.csv WRITE2.csv ...]
 """
 import csv
 import json
@@ -24,6 +24,9 @@ def load(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
+        if name.startswith("dec_ffn_w1 "):  # tools/conv_probe.py dec_ffn_w1 (the C2 dominant conv alone)
+            acc["dec_ffn_w1"].append(float(r["Counter_Value"]))
+            continue
         m = re.search(r"conv1d_kernel<[^>]*?(?:true|false),\s*(\d+)", name)  # ROLE follows the NICE flag
         if m and m.group(1) != "0":
             acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
@@ -42,9 +45,14 @@ def load(path, counter):
     return acc
 
 
-def main(fetch_csv, write_csv, out):
+def main(fetch_csv, write_csv, out, *extra):
     f = load(fetch_csv, "FETCH_SIZE")
     w = load(write_csv, "WRITE_SIZE")
+    for fx, wx in zip(extra[0::2], extra[1::2]):  # further (FETCH, WRITE) csv pairs, e.g. the C2 probe
+        for k, v in load(fx, "FETCH_SIZE").items():
+            f[k] += v
+        for k, v in load(wx, "WRITE_SIZE").items():
+            w[k] += v
     res = {}
     for tag in sorted(set(f) | set(w)):
         fb = 2.0 * 1024 * sum(f[tag]) / max(1, len(f[tag]))
@@ -58,4 +66,4 @@ def main(fetch_csv, write_csv, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:])
