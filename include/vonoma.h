@@ -206,6 +206,16 @@ typedef struct vo_head_desc {
 } vo_head_desc;
 int vo_variance_head(const vo_head_desc* d, void* stream);
 
+/* Training-side energy embedding (config C4, teacher-forced): idx = bucketize(target, bins)
+ * (right=False), out = x + table[idx] (out of place), rows = B*T, table (n_bins + 1, D) fp32;
+ * vo_embed_bwd: dtable[e] = sum of dy rows with idx == e, added in row order (deterministic).
+ * Replaces: energy_embedding(torch.bucketize(e_target, energy_bins)) and its autograd
+ * (scripts/model/modules.py:53-64,101-104). */
+int vo_bucket_embed(const void* x, int x_dtype, const float* target, const float* bins, int n_bins,
+                    const float* table, int64_t rows, int D, void* out, int32_t* idx_out, void* stream);
+int vo_embed_bwd(const void* dy, int dy_dtype, const int32_t* idx, int64_t rows, int D, int n_table, float* dtable,
+                 void* stream);
+
 /* ------------------------------------------------------------------ encoder glue
  * Visual feature extractor front: for every 24 x W_s slice (b, i) of images (B, 1, 24, W),
  * 3 x [Conv2d 3x3 pad 1 (1 -> 1 ch) -> BatchNorm2d(eval, folded scale/shift) -> ReLU],
@@ -444,6 +454,18 @@ int vo_stft_loss_grad(const float* xm, const float* ym, int64_t n, const float* 
 int vo_glyph_batch(const uint8_t* px, const int64_t* img_off, const int32_t* img_w,
                    const int32_t* char_off, const int32_t* char_start, const int32_t* char_len,
                    int B, int H, int cell, int margin, int W_out, float* out, void* stream);
+
+/* ------------------------------------------------------------------ optimizer
+ * Multi-tensor Adam (decoupled = 0: L2 weight decay on the gradient) / AdamW (decoupled = 1) step over
+ * nt fp32 tensors (tables of device pointers and element counts, host memory), torch's
+ * single-tensor update order; lr and step (the steps taken so far) are device scalars read by the
+ * kernels, so the update is graph-capturable.  vo_opt_step_increment(step) advances the counter
+ * (after every vo_adam_multi call of a step).  Replaces torch.optim.Adam behind ScheduledOptim
+ * (scripts/model/optimizer.py:9-15) and the HiFi-GAN V1 recipe's AdamW. */
+int vo_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                  const int64_t* numel, const float* lr, const float* step, float beta1, float beta2, float eps,
+                  float weight_decay, int decoupled, void* stream);
+int vo_opt_step_increment(float* step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,122 @@
+"""The multi-tensor HIP Adam / AdamW (visual_onoma_to_wave_amd.optim.FusedAdam, vo_adam_multi) against
+torch.optim.Adam / AdamW (the reference's optimizer, scripts/model/optimizer.py:9-15, and the HiFi-GAN V1
+recipe's AdamW) over several steps: parameters within rel-L2 1e-6, moments within 1e-5 (fp32, the same
+update order; fused multiply-adds and powf vs Python-double bias corrections differ in the last bits).  Also: unaligned gradient views
+(bucket slices), more tensors than one launch holds, a state_dict round trip with torch's Adam, and a
+HIP-graph replay equal to eager steps bit for bit."""
+
+import pytest
+import torch
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1,), (3,), (5, 7), (256, 256), (513,), (1024, 64, 3), (2, 3, 5, 7), (4097,)]
+
+
+def _params(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(SHAPES[i % len(SHAPES)], generator=g) for i in range(n)]
+
+
+def _grads(seed, ps, steps):
+    g = torch.Generator().manual_seed(seed)
+    return [[torch.randn(p.shape, generator=g) * (0.1 + i) for i, p in enumerate(ps)] for _ in range(steps)]
+
+
+@pytest.mark.parametrize("decoupled,wd,n", [(False, 0.0, 8), (False, 0.01, 70), (True, 0.01, 9), (True, 0.0, 130)])
+def test_fused_adam_vs_torch(decoupled, wd, n):
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    init = _params(n, n)
+    grads = _grads(n + 1, init, 5)
+    kw = dict(lr=2e-3, betas=(0.8, 0.99), eps=1e-8, weight_decay=wd)
+    pr = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    pf = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    ref = (torch.optim.AdamW if decoupled else torch.optim.Adam)(pr, foreach=False, **kw)
+    got = FusedAdam(pf, decoupled=decoupled, **kw)
+    # gradients as views into one flat buffer at a 1-float offset (GradBucketer slices are not aligned)
+    flat = torch.empty(1 + sum(p.numel() for p in init), device="cuda")
+    for gs in grads:
+        off = 1
+        for a, b, g in zip(pr, pf, gs):
+            a.grad = g.cuda()
+            v = flat[off: off + g.numel()].view_as(g)
+            v.copy_(g.cuda())
+            b.grad = v
+            off += g.numel()
+        ref.step()
+        got.step()
+    for a, b in zip(pr, pf):
+        assert rel_l2(b.detach().cpu(), a.detach().cpu()) < 1e-6
+        sa, sb = ref.state[a], got.state[b]
+        assert rel_l2(sb["exp_avg"].cpu(), sa["exp_avg"].cpu()) < 1e-5
+        assert rel_l2(sb["exp_avg_sq"].cpu(), sa["exp_avg_sq"].cpu()) < 1e-5
+        assert float(sb["step"]) == float(sa["step"]) == 5.0
+
+
+def test_fused_adam_state_dict_interchange():
+    """A torch Adam state (the reference checkpoint's "optimizer" entry) loads into FusedAdam and the
+    next steps continue as torch's would; FusedAdam's state_dict loads back into torch Adam."""
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    init = _params(3, 6)
+    grads = _grads(4, init, 6)
+    kw = dict(lr=1e-3, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.0)
+    pr = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    ref = torch.optim.Adam(pr, foreach=False, **kw)
+    for gs in grads[:3]:
+        for a, g in zip(pr, gs):
+            a.grad = g.cuda()
+        ref.step()
+    pf = [torch.nn.Parameter(a.detach().clone()) for a in pr]
+    got = FusedAdam(pf, **kw)
+    got.load_state_dict(ref.state_dict())
+    for gs in grads[3:]:
+        for a, b, g in zip(pr, pf, gs):
+            a.grad = g.cuda()
+            b.grad = g.cuda()
+        ref.step()
+        got.step()
+    for a, b in zip(pr, pf):
+        assert rel_l2(b.detach().cpu(), a.detach().cpu()) < 1e-5  # eps 1e-9: tiny denominators
+    back = torch.optim.Adam([torch.nn.Parameter(b.detach().clone()) for b in pf], **kw)
+    back.load_state_dict(got.state_dict())
+    assert float(back.state_dict()["state"][0]["step"]) == 6.0
+    assert set(got.state_dict()["param_groups"][0]) == set(ref.state_dict()["param_groups"][0])
+
+
+def test_fused_adam_graph_replay_matches_eager():
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    init = _params(9, 12)
+    grads = _grads(10, init, 4)
+    outs = []
+    for graphed in (False, True):
+        ps = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+        lr = torch.tensor(1e-3, device="cuda")
+        opt = FusedAdam(ps, lr=lr, betas=(0.8, 0.99), weight_decay=0.01, decoupled=True, capturable=True)
+        static = [g.cuda() for g in grads[0]]
+        for p, g in zip(ps, static):
+            p.grad = g
+        if graphed:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                opt.step()  # warm-up: creates the state
+            torch.cuda.current_stream().wait_stream(s)
+            with torch.no_grad():
+                for p, q in zip(ps, init):
+                    p.copy_(q.cuda())
+                for st in opt.state.values():
+                    for k in ("exp_avg", "exp_avg_sq", "step"):
+                        st[k].zero_()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                opt.step()
+        for i, gs in enumerate(grads):
+            for s_, g in zip(static, gs):
+                s_.copy_(g.cuda())
+            lr.fill_(1e-3 * (i + 1))
+            graph.replay() if graphed else opt.step()
+        torch.cuda.synchronize()
+        outs.append(torch.cat([p.detach().flatten().cpu() for p in ps]))
+    assert torch.equal(outs[0], outs[1])

@@ -418,7 +418,7 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 9, 30, 31])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 9, 30, 31, 40, 41])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
                                      # several tiles per persistent workgroup (pipelined window/weights)

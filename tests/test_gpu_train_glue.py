@@ -220,3 +220,36 @@ def test_multi_resolution_stft_loss_vs_oracle():
     # deterministic: the same call again gives the same bits
     sc2, mag2 = loss(xg.detach(), y.float().cuda())
     assert torch.equal(sc2, sc.detach()) and torch.equal(mag2, mag.detach())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bucket_embed_vs_torch(dt):
+    """Training-side energy embedding (vo_bucket_embed / vo_embed_bwd, modules.py:53-64,101-104):
+    bucket indices exact (targets on and next to every bin edge), out = x + table[idx], dx = dy, and
+    the table gradient against nn.Embedding's autograd."""
+    from visual_onoma_to_wave_amd import autograd as AG
+    g = torch.Generator().manual_seed(3)
+    B, T, D = 32, 12, 256
+    bins = torch.linspace(-1.06798, 5.10888, 255)
+    tgt = torch.randn(B, T, generator=g) * 2 + 1
+    tgt[0, :6] = bins[torch.tensor([0, 1, 100, 200, 253, 254])]          # exactly on edges (right=False)
+    tgt[1, :4] = torch.tensor([-5.0, 9.0, float(bins[7]) - 1e-6, float(bins[7]) + 1e-6])
+    emb = torch.nn.Embedding(256, D)
+    x = torch.randn(B, T, D, generator=g)
+    xg = x.to(dt).cuda().requires_grad_(True)
+    e_h = torch.nn.Embedding(256, D).cuda()
+    e_h.weight.data.copy_(emb.weight.data)
+    out = AG.bucket_embed(xg, e_h, tgt.cuda(), bins.cuda())
+    idx_ref = torch.bucketize(tgt, bins)
+    xr = x.to(dt).float().requires_grad_(True)
+    ref = xr + emb(idx_ref)
+    if dt == torch.float32:
+        assert torch.equal(out.detach().cpu(), ref.detach())
+    else:
+        assert torch.equal(out.detach().cpu(), ref.detach().to(dt))
+    dy = torch.randn(B, T, D, generator=g)
+    out.backward(dy.to(dt).cuda())
+    ref.backward(dy.to(dt).float())
+    assert torch.equal(xg.grad.cpu(), dy.to(dt))
+    err = float((e_h.weight.grad.cpu() - emb.weight.grad).norm() / emb.weight.grad.norm())
+    assert err < 1e-6, err

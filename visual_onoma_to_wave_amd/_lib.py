@@ -93,6 +93,12 @@ _SIGNATURES = {
                                        c_void_p]),
     "vo_lr_lengths": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_variance_head": (c_int, [ctypes.POINTER(HeadDesc), c_void_p]),
+    "vo_bucket_embed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, ctypes.c_int64, c_int,
+                                c_void_p, c_void_p, c_void_p]),
+    "vo_adam_multi": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                              c_float, c_float, c_float, c_int, c_void_p]),
+    "vo_opt_step_increment": (c_int, [c_void_p, c_void_p]),
+    "vo_embed_bwd": (c_int, [c_void_p, c_int, c_void_p, ctypes.c_int64, c_int, c_int, c_void_p, c_void_p]),
     "vo_vfe_stencil": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_int, c_void_p, c_int, c_void_p]),
     "vo_add_pos_class": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

@@ -203,3 +203,29 @@ def vfe_conv(x, conv):
 
 def length_regulate(x, dur, max_len, out_dtype=None):
     return LengthRegulateFn.apply(x, dur, max_len, out_dtype or x.dtype)
+
+
+class BucketEmbedFn(torch.autograd.Function):
+    """x + Embedding(table)[bucketize(target, bins)] (scripts/model/modules.py:53-64,101-104, teacher
+    forced): forward vo_bucket_embed, backward dx = dy and dtable by vo_embed_bwd (row-ordered sums)."""
+
+    @staticmethod
+    def forward(ctx, x, table, target, bins):
+        out, idx = ops.bucket_embed(x.contiguous(), target, bins.detach().float().contiguous(),
+                                    table.detach().float().contiguous())
+        ctx.save_for_backward(idx)
+        ctx.n_table = table.shape[0]
+        ctx.table_dtype = table.dtype
+        ctx.mark_non_differentiable(idx)
+        return out, idx
+
+    @staticmethod
+    def backward(ctx, go, _gi):
+        (idx,) = ctx.saved_tensors
+        dt = ops.embed_bwd(go.contiguous(), idx, ctx.n_table) if ctx.needs_input_grad[1] else None
+        return go, (dt.to(ctx.table_dtype) if dt is not None else None), None, None
+
+
+def bucket_embed(x, embedding, target, bins):
+    """``x + embedding(torch.bucketize(target, bins))`` on HIP, differentiable in x and the table."""
+    return BucketEmbedFn.apply(x, embedding.weight, target, bins)[0]

@@ -549,6 +549,9 @@ using namespace vo;
 int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                  const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                  hipStream_t st, int* handled);  // resblock2.hip
+int vo_pair3_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                 const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
+                 hipStream_t st, int* handled);  // resblock4.hip
 
 extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                                 void* y, const void* acc, int B, int T, int C, int K, int dil, float slope,
@@ -571,6 +574,11 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
+  if (cfg == 40 || cfg == 41) {  // round 3: two 4-wave workgroups per CU, LDS-DMA windows (resblock4.hip)
+    int handled = 0;
+    const int rc = vo_pair3_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
   // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
   // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
   // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.

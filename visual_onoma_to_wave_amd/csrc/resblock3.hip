@@ -42,7 +42,11 @@ constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six conv
 // wait at a group's end leaves the younger NBUF - 2 groups in flight).
 // 4-wave workgroups (WC * WT = 4) are sized for two per CU: one workgroup's epilogues, window
 // fetch and barriers overlap the other's MFMAs
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
+// VD (round 3, "VALU diet"; the round-2 epilogues ran 6-9 VALU instructions per MFMA): each conv's
+// bias enters as the C operand of its first MFMA (no accumulator zeroing, no bias adds), leaky ReLU
+// and the residual update in packed fp32 (v_pk_mul / v_pk_add), x_{s+1}'s lrelu'd copy taken from
+// the fp32 sum instead of re-unpacking the rounded bf16, boundary masks only in boundary tiles.
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true>
 __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_kernel(Rb3Args a) {
   // streamed-weight blocks: bare LDS barriers (the fence of __syncthreads drains the window
   // prefetch and the y stores at every group); resident-weight (C = 32) blocks keep
@@ -160,7 +164,7 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   auto store_win = [&]() {
 #pragma unroll
     for (int s = 0; s < MAXW; ++s) {
-      const u32x4 v = lrelu8(xw[s], slope);
+      const u32x4 v = VD ? lrelu8_pk(xw[s], slope) : lrelu8(xw[s], slope);
       *reinterpret_cast<u32x4*>(xr0 + s * RSTEP < RR ? reg + xl0 + s * RSTEP * 32 : spare) =
           xw_ok[s] ? v : u32x4{0u, 0u, 0u, 0u};
     }
@@ -198,9 +202,12 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
     const bool has_next = tile + 1 < tile_end;
     u32x4 xres[NJ][NH];  // x_s of the lane's frame rows (bf16), the next stage's residual
 
-    for (int g = 0; g < NG; ++g) {
-      const int s = g / 6, ph = (g / 3) & 1, k = g % 3;
+    for (int cv = 0; cv < 6; ++cv) {  // conv cv: stage cv / 2, c1 (even) or c2 (odd)
+      const int s = cv >> 1, ph = cv & 1;
       const int step = ph ? 1 : a.dil[s];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {  // taps (compile-time: the conv's first step is known statically)
+      const int g = cv * 3 + k;
       const int row = brow0 + (k - 1) * step;
 #pragma unroll
       for (int part = 0; part < (RESW ? 1 : SPLIT); ++part) {
@@ -234,10 +241,19 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
           const int boff = c * RR * 32 + rb_off(row, lq, 2);
 #pragma unroll
           for (int j = 0; j < NJ; ++j) bfr[j].load(reg + boff + 16 * j * 32);
+          if (VD && k == 0 && part == 0 && cl == 0) {  // the conv's first step: its bias is the C operand
 #pragma unroll
-          for (int i = 0; i < NI; ++i)
+            for (int i = 0; i < NI; ++i) {
+              const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + cv * C + n0 + 4 * i);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+              for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], bv);
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+          }
         }
         if constexpr (!RESW) {
           // the next group's DMA (issued D - 1 groups ago) has landed for this wave; younger ones
@@ -247,16 +263,71 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
           ++gcount;
         }
       }
-      if (k != 2) continue;
+      }  // taps
       // ---- end of a conv: every wave is past its reads of the region
       if constexpr (RESW) bar();
       if (s == 2 && ph == 1) break;  // the last conv's epilogue follows the loop (its window
                                      // registers must not be live around the loop)
       float bz[8 * NH];
-      lane_bias(2 * s + ph, bz);
+      if constexpr (VD) {
+#pragma unroll
+        for (int u = 0; u < 8 * NH; ++u) bz[u] = 0.f;  // the bias is in the accumulators
+      } else {
+        lane_bias(2 * s + ph, bz);
+      }
       // frame rows outside [0, T) exist only in an utterance's first / last tile
       const bool interior = p0 >= 0 && p0 + F <= T;
-      if (ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
+      if (VD && ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = p0 + r;
+          const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            uint32_t w[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const int e = 2 * e2;
+              w[e2] = lrelu_pk(acc[2 * h + e / 4][j][e & 3], acc[2 * h + (e + 1) / 4][j][(e + 1) & 3], slope);
+            }
+            if (!interior) {
+#pragma unroll
+              for (int e2 = 0; e2 < 4; ++e2) w[e2] &= km;
+            }
+            const int ch = n0 + 8 * h;
+            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
+          }
+        }
+      } else if (VD && s < 2) {  // x_{s+1} = x_s + c2 + b2 (bf16) and lrelu(x_{s+1}) from the fp32 sum
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = p0 + r;
+          const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            float xf[8];
+            unpack8(xres[j][h], xf);
+            uint32_t w[4], l[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const int e = 2 * e2;
+              const f32x2v v = f32x2v{acc[2 * h + e / 4][j][e & 3], acc[2 * h + (e + 1) / 4][j][(e + 1) & 3]} +
+                               f32x2v{xf[e], xf[e + 1]};
+              w[e2] = pk_bf16(v.x, v.y);
+              l[e2] = lrelu_pk(v.x, v.y, slope);
+            }
+            if (!interior) {
+#pragma unroll
+              for (int e2 = 0; e2 < 4; ++e2) l[e2] &= km;
+            }
+            xres[j][h] = u32x4{w[0], w[1], w[2], w[3]};
+            const int ch = n0 + 8 * h;
+            *reinterpret_cast<u32x4*>(reg + (ch >> 5) * RR * 32 + rb_off(r + RB3_HPC, (ch & 31) >> 3, 2)) = u32x4{l[0], l[1], l[2], l[3]};
+          }
+        }
+      } else if (ph == 0) {  // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's zero padding)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int r = wt * 16 * NJ + 16 * j + lr;
@@ -305,15 +376,22 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
           }
         }
       }
+      if constexpr (!VD) {
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (g + 1 < NG) bar();  // region rewritten: visible before the next conv reads it
+          for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (cv < 5) bar();  // region rewritten: visible before the next conv reads it
     }
     {  // y = (x2 + c2 + b2) * out_scale (+ acc) on the valid rows
       float bz[8 * NH];
-      lane_bias(5, bz);
+      if constexpr (VD) {
+#pragma unroll
+        for (int u = 0; u < 8 * NH; ++u) bz[u] = 0.f;  // the bias is in the accumulators
+      } else {
+        lane_bias(5, bz);
+      }
       // the accumulator rows for every (j, h) at once (clamped, unconditional: without acc the
       // x rows are read and not added) instead of one dependent load per store; the y values
       // are packed, the next tile's window is requested (before the y stores: vmcnt retires in
@@ -372,10 +450,12 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
           __builtin_amdgcn_raw_buffer_store_b128(yv[j][h], yrs, roff + (n0 + 8 * h) * (int)sizeof(bf16_t), 0, 0);
       }
     }
+    if constexpr (!VD) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     // next window (requested in the last epilogue) over the region (P2 of stage 2 ended its
     // region reads at the last barrier)
     if (has_next) store_win();
@@ -383,7 +463,7 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2>
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true>
 static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int F = WT * 16 * NJ;
@@ -397,7 +477,7 @@ static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
     vo_set_error("resblock3: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF>;
+  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF, VD>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -444,6 +524,11 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
+  if (cfg == 20) {  // the round-2 kernels (epilogues without the VALU diet), for A/B
+    if (C == 32) return rb3_launch<32, 1, 8, 2, true, 1, 2, false>(a, B, st);
+    if (C == 64) return rb3_launch<64, 1, 8, 4, false, 1, 2, false>(a, B, st);
+    return rb3_launch<128, 2, 4, 4, false, 1, 2, false>(a, B, st);
+  }
   if (C == 32) {  // 256-row frames, all weights resident: 2 workgroups (4 waves / SIMD) per CU
     if (cfg == 1) return rb3_launch<32, 1, 8, 4, true>(a, B, st);
     return rb3_launch<32, 1, 8, 2, true>(a, B, st);

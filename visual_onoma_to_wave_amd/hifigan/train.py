@@ -20,7 +20,7 @@ import itertools
 
 import torch
 
-from .. import _base
+from .. import _base, optim
 from ..train import GradBucketer, TrainState, _capture_ctx, _check_graph_runtime, _warmup_ctx
 from .discriminators import (MelLoss, MultiPeriodDiscriminator, MultiResolutionSTFTLoss, MultiScaleDiscriminator,
                              discriminator_loss, feature_loss, generator_loss)
@@ -67,10 +67,11 @@ class HifiGanTrainer:
         if graphed and not cap:
             raise ValueError("graphed training needs the capturable optimizer")
         lr = (lambda: torch.tensor(float(h.learning_rate), device=device)) if cap else (lambda: h.learning_rate)
-        self.optim_g = torch.optim.AdamW(generator.parameters(), lr(), betas=[h.adam_b1, h.adam_b2],
-                                         capturable=cap)
-        self.optim_d = torch.optim.AdamW(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
-                                         lr(), betas=[h.adam_b1, h.adam_b2], capturable=cap)
+        # AdamW (torch's defaults: weight decay 0.01, eps 1e-8) as multi-tensor HIP launches on the GPU
+        adamw = optim.AdamW if torch.device(device).type == "cuda" else torch.optim.AdamW
+        self.optim_g = adamw(generator.parameters(), lr(), betas=[h.adam_b1, h.adam_b2], capturable=cap)
+        self.optim_d = adamw(itertools.chain(self.msd.parameters(), self.mpd.parameters()),
+                             lr(), betas=[h.adam_b1, h.adam_b2], capturable=cap)
         self.sched_g = torch.optim.lr_scheduler.ExponentialLR(self.optim_g, gamma=h.lr_decay)
         self.sched_d = torch.optim.lr_scheduler.ExponentialLR(self.optim_d, gamma=h.lr_decay)
         self.mel_loss = MelLoss(h.n_fft, h.num_mels, h.sampling_rate, h.hop_size, h.win_size, h.fmin,

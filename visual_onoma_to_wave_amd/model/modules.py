@@ -184,10 +184,10 @@ class VarianceAdaptor(HipModule):
         e_pred = k_pred = None
         if self.is_energy:
             e_pred = self.energy_predictor.train_run(x, src_mask)
-            x = x + self.energy_embedding(torch.bucketize(e_target, self.energy_bins)).to(x.dtype)
+            x = AG.bucket_embed(x, self.energy_embedding, e_target, self.energy_bins)
         if self.is_kurtosis:
             k_pred = self.kurtosis_predictor.train_run(x, src_mask)
-            x = x + self.kurt_embedding(torch.bucketize(k_target, self.kurt_bins)).to(x.dtype)
+            x = AG.bucket_embed(x, self.kurt_embedding, k_target, self.kurt_bins)
         if max_len is None:
             mel_len, _ = ops.lr_lengths(d_target)
             max_len = int(mel_len.cpu().max())

@@ -2,11 +2,13 @@
 
 lr(step) = init_lr * min(step^-0.5, warmup^-1.5 * step) * anneal_rate^#{anneal steps < step},
 evaluated after the step counter is incremented; Adam(betas, eps, weight_decay) from the
-train config.  ``fused=True`` runs Adam as one multi-tensor kernel per step on the GPU.
+train config.  On the GPU the update runs as multi-tensor HIP launches (``optim.FusedAdam``).
 """
 
 import numpy as np
 import torch
+
+from ..optim import FusedAdam
 
 
 class ScheduledOptim:
@@ -20,11 +22,14 @@ class ScheduledOptim:
         # the param group then matches a reference checkpoint's optimizer state on resume
         params = list(model.parameters())
         kw = dict(betas=o["betas"], eps=o["eps"], weight_decay=o["weight_decay"])
-        if params and params[0].is_cuda:
-            kw["fused"] = True
         if capturable:
             kw.update(capturable=True, lr=torch.tensor(0.0, device=params[0].device))
-        self._optimizer = torch.optim.Adam(params, **kw)
+        if params and params[0].is_cuda:
+            # the update as multi-tensor HIP launches (visual_onoma_to_wave_amd.optim), torch Adam's
+            # arithmetic and state layout (checkpoints interchange with the reference's Adam)
+            self._optimizer = FusedAdam(params, decoupled=False, **kw)
+        else:
+            self._optimizer = torch.optim.Adam(params, **kw)
         self.n_warmup_steps = o["warm_up_step"]
         self.anneal_steps = o["anneal_steps"]
         self.anneal_rate = o["anneal_rate"]

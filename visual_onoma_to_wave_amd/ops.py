@@ -324,6 +324,32 @@ def energy_head(h, w, b, lens, x, bins, table, target=None, mean=0.0, std=1.0, c
     return pred, idx
 
 
+def bucket_embed(x, target, bins, table):
+    """Training-side energy embedding: out = x + table[bucketize(target, bins)] (out of place) ->
+    (out, idx int32) (vo_bucket_embed; reference modules.py:53-64,101-104 with a target)."""
+    _contig(x, "x")
+    B, T, D = x.shape
+    tgt = _contig(target.float(), "target")
+    if tgt.shape != (B, T):
+        raise ValueError(f"bucket_embed: target {tuple(tgt.shape)} vs x {tuple(x.shape)}")
+    out = torch.empty_like(x)
+    idx = torch.empty((B, T), dtype=torch.int32, device=x.device)
+    _lib.check(_lib.lib().vo_bucket_embed(_ptr(x), vo_dtype(x), _ptr(tgt), _ptr(bins), bins.numel(), _ptr(table),
+                                          B * T, D, _ptr(out), _ptr(idx), _stream(x)), "vo_bucket_embed")
+    return out, idx
+
+
+def embed_bwd(dy, idx, n_table):
+    """dtable (n_table, D) fp32 = per-row sums of dy over the tokens of each index (row order)."""
+    _contig(dy, "dy")
+    D = dy.shape[-1]
+    rows = dy.numel() // D
+    dt = torch.empty((n_table, D), dtype=torch.float32, device=dy.device)
+    _lib.check(_lib.lib().vo_embed_bwd(_ptr(dy), vo_dtype(dy), _ptr(idx), rows, D, n_table, _ptr(dt), _stream(dy)),
+               "vo_embed_bwd")
+    return dt
+
+
 # ----------------------------------------------------------------------------- encoder glue
 
 def vfe_stencil(images, conv_params, bn_params, slice_w, out_dtype):
