@@ -48,8 +48,10 @@ struct PairArgs {
 // from window + T1 to max(window, T1), so the C = 128 tile can grow to 256 rows and each
 // streamed weight tap feeds twice the MFMAs.  Costs two barriers per tile and a window store
 // after P2 instead of during it.
+// VD (round 3, "VALU diet"): each conv's bias is the C operand of its first MFMAs (no accumulator
+// zeroing, no bias adds), leaky ReLU in packed fp32, the T1 mask only in boundary tiles.
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false, bool HP = false, bool LATE = HP>
+          bool IP = false, bool HP = false, bool LATE = HP, bool VD = true>
 __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {  // >= 2 waves per SIMD
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -248,18 +250,28 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
   f32x4 acc[NI][NJ];
   int gcount = 0;  // streamed groups consumed so far (selects the double buffer)
 
-  // one tap of one plane: NI x NJ MFMAs
-  auto tap = [&](const bf16_t* wt, const bf16_t* src, int row) {
+  // one tap of one plane: NI x NJ MFMAs; bias_row >= 0 (VD, a conv's first step): that conv's bias
+  // is the C operand
+  auto tap = [&](const bf16_t* wt, const bf16_t* src, int row, int bias_row = -1) {
     Frag<bf16_t> af[NI], bfr[NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i) af[i].load(wt + a_off[i]);
     const int boff = rb_off(row, lq, 2);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) bfr[j].load(src + boff + 16 * j * 32);
+    if (bias_row >= 0) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + bias_row * C + n0 + 4 * i);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], bv);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    }
   };
 
   for (; tile < tile_end; ++tile) {
@@ -293,10 +305,12 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
       load_win(has_next ? tile + 1 : tile);  // unconditional (see load_win)
     }
 
+    if constexpr (!VD) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     // P1 epilogue: T1 = lrelu(acc + b1), zero outside [0, T) (c2's zero padding); clears acc
     // the lane's 8*NH bias values, read (as float4) before the epilogue's LDS stores: read
@@ -310,6 +324,31 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
       }
     };
     auto p1_epilogue = [&]() {
+      if constexpr (VD) {  // the bias is in the accumulators
+        const bool interior = t0 - h2 >= 0 && t0 - h2 + R1 <= T;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int r = wt * 16 * NJ + 16 * j + lr;
+          const int pos = t0 - h2 + r;
+          const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            uint32_t w[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const int e = 2 * e2;
+              w[e2] = lrelu_pk(acc[2 * h + e / 4][j][e & 3], acc[2 * h + (e + 1) / 4][j][(e + 1) & 3], slope);
+            }
+            if (!interior) {
+#pragma unroll
+              for (int e2 = 0; e2 < 4; ++e2) w[e2] &= km;
+            }
+            const int ch = n0 + 8 * h;
+            *reinterpret_cast<u32x4*>(t1 + (ch >> 5) * T1R * 32 + rb_off(r, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
+          }
+        }
+        return;
+      }
       float bz[8 * NH];
       lane_bias(0, bz);
       // rows outside [0, T) exist only in the first / last tile of an utterance
@@ -339,8 +378,9 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
     };
 
     if constexpr (RES) {
+      tap(wls, win, brow0, VD ? 0 : -1);  // c = 0, k = 0: the conv's first step
       for (int c = 0; c < NC; ++c)
-        for (int k = 0; k < K; ++k) tap(wls + k * TAPE + c * C * 32, win + c * win_rows * 32, brow0 + k * dil);
+        for (int k = c == 0 ? 1 : 0; k < K; ++k) tap(wls + k * TAPE + c * C * 32, win + c * win_rows * 32, brow0 + k * dil);
       if constexpr (IP) {  // T1 overwrites the window: every wave must be past its P1 reads
         lds_barrier();
         p1_epilogue();
@@ -351,8 +391,9 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
         if (has_next) store_win();
       }
       const bf16_t* wb = wls + K * TAPE;
+      tap(wb, t1, brow0, VD ? 1 : -1);
       for (int c = 0; c < NC; ++c)
-        for (int k = 0; k < K; ++k) tap(wb + k * TAPE + c * C * 32, t1 + c * T1R * 32, brow0 + k);
+        for (int k = c == 0 ? 1 : 0; k < K; ++k) tap(wb + k * TAPE + c * C * 32, t1 + c * T1R * 32, brow0 + k);
     } else {
       // peeled per phase so the P1 epilogue / window store sit on straight-line paths
       auto group = [&](int ph, int g, bool p1_last, bool p2_first) {
@@ -374,12 +415,13 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
         if constexpr (!SB) {  // plain steps: hipcc schedules the reads (fewer live fragments)
 #pragma unroll
           for (int st = 0; st < S; ++st) {
+            const int brow_first = VD && g == 0 && st == 0 ? ph : -1;  // a conv's first step: bias as C
             if constexpr (HP) {  // half tap g & 1 of tap g >> 1: planes (g & 1) * S + st
               const int c = (g & 1) * S + st;
-              tap(wb + st * C * 32, src + c * plane, brow0 + (g >> 1) * step);
+              tap(wb + st * C * 32, src + c * plane, brow0 + (g >> 1) * step, brow_first);
             } else if (TG == 1 || g * TG + st / NC < K) {
               const int t = st / NC, c = st - t * NC;
-              tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + (g * TG + t) * step);
+              tap(wb + t * TAPE + c * C * 32, src + c * plane, brow0 + (g * TG + t) * step, brow_first);
             }
           }
         }
@@ -419,8 +461,9 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
           lds_barrier();
         }
       };
-      for (int g = 0; g < NG - 1; ++g) group(0, g, false, false);
-      group(0, NG - 1, true, false);
+      group(0, 0, NG == 1, false);  // peeled: the conv's first step is known statically
+      for (int g = 1; g < NG - 1; ++g) group(0, g, false, false);
+      if (NG > 1) group(0, NG - 1, true, false);
       group(1, 0, false, true);
       for (int g = 1; g < NG; ++g) group(1, g, false, false);
     }
@@ -456,7 +499,12 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
       }
     }
     float b2z[8 * NH];
-    lane_bias(1, b2z);
+    if constexpr (VD) {
+#pragma unroll
+      for (int u = 0; u < 8 * NH; ++u) b2z[u] = 0.f;  // the bias is in the accumulators
+    } else {
+      lane_bias(1, b2z);
+    }
     // y rows through a buffer resource covering exactly this tile's valid rows: the rows past
     // it (r >= BT, or past T) fall outside the resource and their stores are dropped by the
     // hardware -- no per-lane branch, and a fixed number of stores per wave
@@ -512,7 +560,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
 }
 
 template <int C, int WC, int WT, int NJ, bool RES, int TG, int ABL = 0, int PRIO = 0, bool SB = false, bool GL = false,
-          bool IP = false, bool HP = false, bool LATE = HP>
+          bool IP = false, bool HP = false, bool LATE = HP, bool VD = true>
 static int pair_launch(PairArgs a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -528,7 +576,7 @@ static int pair_launch(PairArgs a, int B, hipStream_t st) {
     vo_set_error("resblock_pair: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP, HP, LATE>;
+  auto kern = mrf_pair_kernel<C, WC, WT, NJ, RES, TG, ABL, PRIO, SB, GL, IP, HP, LATE, VD>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -552,6 +600,9 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
 int vo_pair3_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                  const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                  hipStream_t st, int* handled);  // resblock4.hip
+int vo_pair_wave_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                     const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
+                     hipStream_t st, int* handled);  // resblock5.hip
 
 extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                                 void* y, const void* acc, int B, int T, int C, int K, int dil, float slope,
@@ -574,6 +625,11 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
+  if (cfg == 50) {  // round 3: C = 32 with wave-private frames (resblock5.hip)
+    int handled = 0;
+    const int rc = vo_pair_wave_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
   if (cfg == 40 || cfg == 41) {  // round 3: two 4-wave workgroups per CU, LDS-DMA windows (resblock4.hip)
     int handled = 0;
     const int rc = vo_pair3_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
@@ -582,10 +638,18 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
   // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
   // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.
-  if ((C == 64 && cfg != 9 && (cfg < 20 || cfg == 32)) || cfg == 30 || cfg == 31) {
+  if ((C == 64 && cfg != 9 && (cfg < 20 || cfg == 32 || cfg == 33)) || cfg == 30 || cfg == 31) {
     int handled = 0;
     const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;
+  }
+  // VALU diet (VD): C = 128 -2..4 % (0.682 -> 0.668 ms at k = 11, 0.505 -> 0.485 at k = 7); C = 32
+  // +2..3 % (0.201 -> 0.205, 0.234 -> 0.240): C = 32 ships without it (tools/mrf_bench.py --tune
+  // pair_cfg=8,0, round 3).  cfg 8 swaps the C = 32 / 128 epilogues, for A/B
+  if (cfg == 8) {
+    if (C == 32) return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true, true>(a, B, st);
+    if (C == 128 && K <= 3) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true, true, false>(a, B, st);
+    if (C == 128) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true, false>(a, B, st);
   }
   if (C == 32) {
     if (cfg == 3) return pair_launch<32, 1, 4, 8, true, 1>(a, B, st);
@@ -597,7 +661,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     }
     // 512-row in-place tiles, window / residual fetched after P2: k = 11 -13 %, k = 7 -3 %
     // (k = 3 is HBM-bound at ~5 TB/s either way; tools/ab_sb.py pair32 9 5)
-    return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true>(a, B, st);
+    return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true, false>(a, B, st);
   }
   if (C == 128) {
     // 2 x 4 waves of 64 channels (2 waves/SIMD), weights by LDS-DMA.  k = 3: 128-row tiles;

@@ -33,7 +33,9 @@ struct Pair2Args {
 
 constexpr int PAIR2_DMAX = 5;
 
-template <int C, int WC, int WT, int NJ, int K, bool GL, int TG>
+// VD (round 3, "VALU diet"): each conv's bias is the C operand of its first MFMAs (no accumulator
+// zeroing, no bias adds), leaky ReLU in packed fp32, the T1 mask only in boundary tiles.
+template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true>
 __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a) {
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -191,18 +193,28 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
     }
   };
 
-  // one (tap, plane) step: NI x NJ MFMAs
-  auto tap = [&](const bf16_t* wt_, const bf16_t* src, int row) {
+  // one (tap, plane) step: NI x NJ MFMAs; bias_row >= 0 (VD, a conv's first step): the bias of that
+  // conv is the C operand
+  auto tap = [&](const bf16_t* wt_, const bf16_t* src, int row, int bias_row = -1) {
     Frag<bf16_t> af[NI], bfr[NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i) af[i].load(wt_ + a_off[i]);
     const int boff = rb_off(row, lq, 2);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) bfr[j].load(src + boff + 16 * j * 32);
+    if (bias_row >= 0) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + bias_row * C + n0 + 4 * i);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], bv);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    }
     // keep the unrolled straight-line steps apart: hoisting the next steps' fragment reads
     // above these MFMAs blew the register budget (spills)
     __builtin_amdgcn_sched_barrier(0);
@@ -217,30 +229,60 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
     int brow0 = brow0_;
     asm volatile("" : "+v"(brow0));
 
+    if constexpr (!VD) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
-    // ---- P1: c1 over the lrelu'd window (a runtime loop: unrolled, both phases spilled)
-#pragma unroll 1
-    for (int g = 0; g < NG; ++g) {
+    // ---- P1: c1 over the lrelu'd window (a runtime loop: unrolled, both phases spilled); the first
+    // group is peeled so that its first step (bias as the C operand) is known statically
+    auto p1_group = [&](int g, bool first) {
       load_group(g + 1, (gc + 1) & 1);  // g = NG - 1: P2's first group
       const bf16_t* wb = wls + (gc & 1) * GE;
 #pragma unroll
       for (int t = 0; t < TG; ++t) {
         if (g * TG + t >= K) continue;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) tap(wb + t * TAPE + c * C * 32, reg + c * WR * 32, brow0 + (g * TG + t) * dil);
+        for (int c = 0; c < NC; ++c)
+          tap(wb + t * TAPE + c * C * 32, reg + c * WR * 32, brow0 + (g * TG + t) * dil,
+              VD && first && t == 0 && c == 0 ? 0 : -1);
       }
       store_group((gc + 1) & 1);
       if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
       ++gc;
-    }
+    };
+    p1_group(0, true);
+#pragma unroll 1
+    for (int g = 1; g < NG; ++g) p1_group(g, false);
 
     // ---- P1 epilogue: T1 = lrelu(acc + b1) over the (dead) window; zero outside [0, T)
-    {
+    if constexpr (VD) {  // the bias is in the accumulators
+      const bool interior = t0 - H2 >= 0 && t0 - H2 + R1 <= T;  // uniform
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int r = wt * 16 * NJ + 16 * j + lr;
+        const int pos = t0 - H2 + r;
+        const uint32_t km = (interior || (pos >= 0 && pos < T)) ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          uint32_t w[4];
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const int e = 2 * e2;
+            w[e2] = lrelu_pk(acc[2 * h + e / 4][j][e & 3], acc[2 * h + (e + 1) / 4][j][(e + 1) & 3], slope);
+          }
+          if (!interior) {
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) w[e2] &= km;
+          }
+          const int ch = n0 + 8 * h;
+          *reinterpret_cast<u32x4*>(reg + (ch >> 5) * WR * 32 + rb_off(r, (ch & 31) >> 3, 2)) = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    } else {
       float bz[8 * NH];
       lane_bias(0, bz);
       const bool interior = t0 - H2 >= 0 && t0 - H2 + R1 <= T;  // uniform
@@ -284,7 +326,8 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       for (int t = 0; t < TG; ++t) {
         if (g * TG + t >= K) continue;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) tap(wb + t * TAPE + c * C * 32, reg + c * WR * 32, brow0 + g * TG + t);
+        for (int c = 0; c < NC; ++c)
+          tap(wb + t * TAPE + c * C * 32, reg + c * WR * 32, brow0 + g * TG + t, VD && g == 0 && t == 0 && c == 0 ? 1 : -1);
       }
       store_group((gc + 1) & 1);
       if constexpr (GL) {
@@ -327,7 +370,12 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       for (int h = 0; h < NH; ++h) ares[j][h] = *reinterpret_cast<const u32x4*>(accp + off + 8 * h);
     }
     float b2z[8 * NH];
-    lane_bias(1, b2z);
+    if constexpr (VD) {
+#pragma unroll
+      for (int u = 0; u < 8 * NH; ++u) b2z[u] = 0.f;  // the bias is in the accumulators
+    } else {
+      lane_bias(1, b2z);
+    }
     const int valid = min(BT, T - t0);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
@@ -365,7 +413,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
   }
 }
 
-template <int C, int WC, int WT, int NJ, int K, bool GL, int TG>
+template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true>
 static int pair2_launch(Pair2Args a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -380,7 +428,7 @@ static int pair2_launch(Pair2Args a, int B, hipStream_t st) {
     vo_set_error("resblock_pair (v2): LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair2_kernel<C, WC, WT, NJ, K, GL, TG>;
+  auto kern = mrf_pair2_kernel<C, WC, WT, NJ, K, GL, TG, VD>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -418,6 +466,12 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
   // C = 64: 8 waves of 64 rows, 512-row tiles, 2-tap register-staged groups (cfg 31: LDS-DMA).
   // Measured and dropped: two 4-wave workgroups of 256-row tiles per CU (LDS-DMA weights): 4-8 %
   // faster alone (tools/ab_pair2.py), but s2 -3.6 % / s3 +4 % and the same 13.75 ms in the bench step
+  // VALU diet (VD) at C = 64: k = 11 0.408 -> 0.398 ms, k = 7 0.311 -> 0.318 (tools/mrf_bench.py
+  // --tune pair_cfg=33,0, round 3): k = 11 ships with it, k = 7 without; cfg 33 swaps both, for A/B
+  if (cfg == 33) {
+    if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, true>(a, B, st);
+    return pair2_launch<64, 1, 8, 4, 11, false, 2, false>(a, B, st);
+  }
   if (cfg == 31) {
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, true, 2>(a, B, st);
     return pair2_launch<64, 1, 8, 4, 11, true, 2>(a, B, st);
@@ -427,6 +481,6 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
     if (K == 7) return pair2_launch<64, 1, 4, 4, 7, false, 2>(a, B, st);
     return pair2_launch<64, 1, 4, 4, 11, false, 2>(a, B, st);
   }
-  if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2>(a, B, st);
-  return pair2_launch<64, 1, 8, 4, 11, false, 2>(a, B, st);
+  if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, false>(a, B, st);
+  return pair2_launch<64, 1, 8, 4, 11, false, 2, true>(a, B, st);
 }

@@ -495,6 +495,10 @@ static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
 
 using namespace vo;
 
+int vo_rb3_wave_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                    const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
+                    float out_scale, int cfg, hipStream_t st, int* handled);  // resblock5.hip
+
 extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
                             const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C,
                             float slope, float out_scale, void* stream) {
@@ -524,6 +528,11 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
+  if (C == 32 && (cfg == 30 || cfg == 31)) {  // round 3: wave-private frames (resblock5.hip)
+    int handled = 0;
+    const int rc = vo_rb3_wave_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
   if (cfg == 20) {  // the round-2 kernels (epilogues without the VALU diet), for A/B
     if (C == 32) return rb3_launch<32, 1, 8, 2, true, 1, 2, false>(a, B, st);
     if (C == 64) return rb3_launch<64, 1, 8, 4, false, 1, 2, false>(a, B, st);
