@@ -120,3 +120,46 @@ def test_fused_adam_graph_replay_matches_eager():
         torch.cuda.synchronize()
         outs.append(torch.cat([p.detach().flatten().cpu() for p in ps]))
     assert torch.equal(outs[0], outs[1])
+
+
+def test_fused_adam_bumps_parameter_versions():
+    """The HIP update writes the parameters outside autograd; it bumps their version counters as
+    torch's in-place updates do, so caches keyed on them (packed bf16 weights) see every step."""
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    ps = [torch.nn.Parameter(p.cuda()) for p in _params(5, 3)]
+    opt = FusedAdam(ps, lr=1e-3)
+    before = [p._version for p in ps]
+    for p, g in zip(ps, _grads(6, ps, 1)[0]):
+        p.grad = g.cuda()
+    opt.step()
+    assert all(p._version > v for p, v in zip(ps, before))
+
+
+def test_gan_trainer_fused_adamw_matches_torch_adamw(monkeypatch):
+    """Two eager HiFi-GAN V1 steps (fp32 compute) with the fused AdamW against the same steps with
+    torch.optim.AdamW: the generator's packed weights must follow every update (a stale pack would
+    leave the second step's forward on the first step's weights)."""
+    from helpers import hifigan_arrays, hifigan_h
+    from weights import load_into
+    from visual_onoma_to_wave_amd import hifigan, optim
+    mel_g = torch.Generator().manual_seed(2)
+    mel = (torch.randn(2, 32, 80, generator=mel_g) - 4.0).cuda()
+    y = (0.3 * torch.randn(2, 8192, generator=mel_g)).clamp(-1, 1).cuda()
+    finals = []
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(optim, "AdamW", lambda params, *a, **kw: torch.optim.AdamW(params, *a, **kw))
+        torch.manual_seed(1234)
+        g = hifigan.Generator(hifigan.AttrDict(hifigan_h()))
+        load_into(g, hifigan_arrays())
+        tr = hifigan.HifiGanTrainer(g.cuda(), hifigan.AttrDict(hifigan_h()), capturable=True)
+        tr.set_compute_dtype(torch.float32)
+        for _ in range(2):
+            losses = tr.step(mel, y)
+        torch.cuda.synchronize()
+        finals.append(({k: float(v) for k, v in losses.items()},
+                       torch.cat([p.detach().flatten().cpu() for p in g.parameters()])))
+    (lf, gf), (lt, gt) = finals
+    assert rel_l2(gf, gt) < 1e-4
+    for k in lt:
+        assert abs(lf[k] - lt[k]) <= 1e-3 * abs(lt[k]) + 1e-5, (k, lf[k], lt[k])

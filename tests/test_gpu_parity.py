@@ -373,7 +373,7 @@ def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
 @pytest.mark.parametrize("C,T", [(32, 1000), (64, 777), (128, 300), (32, 5), (64, 1), (128, 13), (128, 232),
                                  (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768)])
 @pytest.mark.parametrize("with_acc", [True, False])
-@pytest.mark.parametrize("cfg", [0, 1, 4, 20, 30, 31])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 20, 30, 31, 40, 41])
 def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     """vo_resblock3 (a whole k = 3 ResBlock, dilations 1/3/5, in one launch) against the torch fp32
     ResBlock at tile edges (frame 232 / 488 valid rows), T = 1, and multi-tile persistent runs;

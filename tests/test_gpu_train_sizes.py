@@ -90,7 +90,7 @@ def test_c4_step_full_size_vs_oracle(device):
         if err > 2e-3 * float(gr.norm()) + 1e-5:
             bad.append((k, err, float(gr.norm())))
     assert not bad, bad[:10]
-    assert len(set(subset)) > 60
+    assert len(set(subset)) > 50
 
 
 # ------------------------------------------------------------------------------------------- C5

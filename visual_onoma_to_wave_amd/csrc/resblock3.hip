@@ -46,7 +46,10 @@ constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six conv
 // bias enters as the C operand of its first MFMA (no accumulator zeroing, no bias adds), leaky ReLU
 // and the residual update in packed fp32 (v_pk_mul / v_pk_add), x_{s+1}'s lrelu'd copy taken from
 // the fp32 sum instead of re-unpacking the rounded bf16, boundary masks only in boundary tiles.
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true>
+// TPG (round 3): taps per streamed group -- 3 = a whole conv per group, so the group's wait and
+// barrier coincide with the conv-end barrier the region rewrite needs anyway (6 barriers per tile
+// instead of 24, 96 MFMAs per wave between them at C = 64)
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1>
 __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_kernel(Rb3Args a) {
   // streamed-weight blocks: bare LDS barriers (the fence of __syncthreads drains the window
   // prefetch and the y stores at every group); resident-weight (C = 32) blocks keep
@@ -72,10 +75,11 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   constexpr int NH = NI / 2;               // 8-channel vectors per lane in epilogue layout
   constexpr int NG = 18;                   // taps per tile: 3 stages x 2 convs x 3 taps
   constexpr int D = NBUF - 1;              // DMA prefetch distance in groups
-  constexpr int NGR = NG * SPLIT;          // streamed groups per tile
-  constexpr int GE = TAPE / SPLIT;         // LDS elements per group buffer
-  constexpr int GPL = NC / SPLIT;          // planes per group
-  static_assert(RESW || (NC % SPLIT == 0 && (TAPV / SPLIT) % NT == 0 && NBUF >= 2),
+  static_assert(TPG == 1 || (TPG == 3 && SPLIT == 1 && !RESW), "whole-conv groups: 3 taps, unsplit");
+  constexpr int NGR = TPG > 1 ? NG / TPG : NG * SPLIT;  // streamed groups per tile
+  constexpr int GE = TPG > 1 ? TPG * TAPE : TAPE / SPLIT;  // LDS elements per group buffer
+  constexpr int GPL = NC / SPLIT;          // planes per group tap
+  static_assert(RESW || (NC % SPLIT == 0 && (TPG * TAPV / SPLIT) % NT == 0 && NBUF >= 2),
                 "streamed groups split into whole wave-KiB DMA instructions");
   static_assert(NT % VPR == 0 && (NT / VPR) % 8 == 0, "window slot stride must keep the swizzle");
   constexpr int RSTEP = NT / VPR;
@@ -110,22 +114,23 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
     const int s = g / 6, ph = (g / 3) & 1, k = g % 3;
     return (ph ? a.w2[s] : a.w1[s]) + k * (C * C);
   };
-  constexpr int GLN = RESW ? 1 : TAPV / SPLIT / NT;  // DMA instructions per wave per group
+  constexpr int GLN = RESW ? 1 : TPG * TAPV / SPLIT / NT;  // DMA instructions per wave per group
   int gl_off[GLN];
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   if constexpr (!RESW) {
 #pragma unroll
     for (int s = 0; s < GLN; ++s) {  // LDS slot p holds (plane, co, chunk q ^ swz(co)): swizzle on the source
-      const int p = (s * NW + wave) * 64 + lane;
+      const int p0 = (s * NW + wave) * 64 + lane;
+      const int t = p0 / TAPV, p = p0 - t * TAPV;  // TPG > 1: tap t of the group (contiguous in W)
       const int pl = p / (C * 4), rem = p - pl * C * 4;
       const int co = rem >> 2, q = (rem & 3) ^ ((co >> (SHW - 1)) & 2);
-      gl_off[s] = co * C + pl * 32 + q * 8;
+      gl_off[s] = t * (C * C) + co * C + pl * 32 + q * 8;
     }
   }
   auto load_grp = [&](int h, int buf) {  // LDS-DMA of group h (planes of tap h / SPLIT) into buffer buf
     typedef __attribute__((address_space(3))) void lds_void;
     typedef const __attribute__((address_space(1))) void g_void;
-    const bf16_t* W = tap_src(h / SPLIT) + (h % SPLIT) * GPL * 32;
+    const bf16_t* W = TPG > 1 ? tap_src(h * TPG) : tap_src(h / SPLIT) + (h % SPLIT) * GPL * 32;
 #pragma unroll
     for (int s = 0; s < GLN; ++s)
       __builtin_amdgcn_global_load_lds((g_void*)(W + gl_off[s]),
@@ -214,6 +219,9 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
         const bf16_t* wb;
         if constexpr (RESW) {
           wb = wls + g * TAPE;
+        } else if constexpr (TPG > 1) {  // the conv's group; the next conv's issued at its first tap
+          if (k == 0) load_grp(cv + D < NGR ? cv + D : cv + D - NGR, (gcount + D) % NBUF);
+          wb = wls + (gcount % NBUF) * GE + k * TAPE;
         } else {  // group D ahead (wrapping into the next tile's first groups)
           const int h = g * SPLIT + part;
           load_grp(h + D < NGR ? h + D : h + D - NGR, (gcount + D) % NBUF);
@@ -258,9 +266,11 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
         if constexpr (!RESW) {
           // the next group's DMA (issued D - 1 groups ago) has landed for this wave; younger ones
           // stay in flight; the barrier publishes it and frees this group's buffer
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * GLN) : "memory");
-          bar();
-          ++gcount;
+          if (TPG == 1 || k == TPG - 1) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * GLN) : "memory");
+            bar();
+            ++gcount;
+          }
         }
       }
       }  // taps
@@ -463,7 +473,7 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true>
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1>
 static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int F = WT * 16 * NJ;
@@ -471,13 +481,13 @@ static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
   constexpr int RR = F + 2 * RB3_HPC;
   a.tiles_per_b = (a.T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
-  const size_t wel = RESW ? 18 * (size_t)C * C : (size_t)NBUF * C * C / SPLIT;
+  const size_t wel = RESW ? 18 * (size_t)C * C : (size_t)NBUF * TPG * C * C / SPLIT;
   const size_t lds = ((size_t)RR * C + wel) * sizeof(bf16_t) + 6 * C * sizeof(float) + 16;
   if (lds > 160 * 1024) {
     vo_set_error("resblock3: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF, VD>;
+  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF, VD, TPG>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -551,7 +561,11 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
     // (round 2, bare LDS barriers): 0.53 -> 0.50 ms alone with the MRF accumulator
     // (tools/ab_pair2.py), the same 12.40 / 12.46 ms bench step (s2 within noise) -- not default
     if (cfg == 6) return rb3_launch<64, 1, 4, 4, false, 1, 3>(a, B, st);
-    return rb3_launch<64, 1, 8, 4, false>(a, B, st);
+    if (cfg == 40) return rb3_launch<64, 1, 8, 4, false>(a, B, st);  // one tap per group (round 2 / 3)
+    if (cfg == 41) return rb3_launch<64, 1, 8, 3, false, 1, 2, true, 3>(a, B, st);
+    // a whole conv (3 taps, 24 KB) per streamed group: 6 barriers per tile instead of 24, 0.476 ->
+    // 0.448 ms (tools/mrf_bench.py --stages 2 --tune rb3_cfg=0,40, round 3, bit-identical)
+    return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3>(a, B, st);
   }
   if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
   if (cfg == 4) return rb3_launch<128, 2, 4, 4, false, 2, 4>(a, B, st);

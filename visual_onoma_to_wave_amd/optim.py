@@ -16,6 +16,7 @@ as in the training steps here.  fp32 parameters, gradients and moments on the GP
 import ctypes
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 
@@ -63,8 +64,8 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 st = self.state.get(p, {})
                 for k in ("exp_avg", "exp_avg_sq"):
-                    if k in st:
-                        st[k] = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+                    if k in st:  # own copies: torch's load_state_dict keeps the caller's tensors
+                        st[k] = st[k].to(device=p.device, dtype=torch.float32, copy=True).contiguous()
             self._group_step(group)
         self._tables.clear()
 
@@ -129,6 +130,10 @@ class FusedAdam(torch.optim.Optimizer):
                                        float(group["weight_decay"]), int(bool(group.get("decoupled_weight_decay"))),
                                        stream), "vo_adam_multi")
             _lib.check(L.vo_opt_step_increment(ctypes.c_void_p(step_t.data_ptr()), stream), "vo_opt_step_increment")
+            # the kernel writes the parameters behind autograd's back: bump their version counters as
+            # torch's in-place updates do, so caches keyed on them (the packed bf16 weights,
+            # _base.PackedModule) see the step
+            increment_version(ps)
         return loss
 
 
