@@ -373,7 +373,7 @@ def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
 @pytest.mark.parametrize("C,T", [(32, 1000), (64, 777), (128, 300), (32, 5), (64, 1), (128, 13), (128, 232),
                                  (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768)])
 @pytest.mark.parametrize("with_acc", [True, False])
-@pytest.mark.parametrize("cfg", [0, 1, 4, 20, 30, 31, 40, 41])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 20, 30, 31, 40, 41, 42, 43, 44, 45])
 def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     """vo_resblock3 (a whole k = 3 ResBlock, dilations 1/3/5, in one launch) against the torch fp32
     ResBlock at tile edges (frame 232 / 488 valid rows), T = 1, and multi-tile persistent runs;
@@ -418,7 +418,7 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 30, 31, 33, 40, 41, 50])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 30, 31, 33, 34, 35, 40, 41, 50, 60, 61])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
                                      # several tiles per persistent workgroup (pipelined window/weights)

@@ -435,20 +435,31 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair_kernel(PairArgs a) {
 #pragma unroll
           for (int j = 0; j < NJ; ++j) bq[set][j].load(src + boff + 16 * j * 32);
         };
+        // SB (round 3 form): the next step's reads go out right after the step's first MFMA, so the
+        // wait before that MFMA covers only reads issued a whole step earlier (two sets of 8 reads in
+        // flight exceed the 4-bit lgkmcnt: hipcc then waited for the just-issued ones as well)
+        static_assert(!SB || !HP, "SB: whole-tap groups");
+        f32x4 bz4[NI];
+        if (SB && VD && g == 0) {
+#pragma unroll
+          for (int i = 0; i < NI; ++i) bz4[i] = *reinterpret_cast<const f32x4*>(sbias + ph * C + n0 + 4 * i);
+        }
         if constexpr (SB) ld(0, 0);
 #pragma unroll
         for (int st = 0; st < (SB ? S : 0); ++st) {
-          if (st + 1 < S) ld(st + 1, (st + 1) & 1);
-          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-          if (TG == 1 || g * TG + st / NC < K) {
-            if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+          const bool valid = TG == 1 || g * TG + st / NC < K;
+          const bool first = VD && g == 0 && st == 0;  // the conv's first step: its bias is the C operand
 #pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-              for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[st & 1][i], bq[st & 1][j], acc[i][j]);
-            if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+          for (int q = 0; q < NI * NJ; ++q) {
+            const int i = q / NJ, j = q - i * NJ;
+            if (valid) acc[i][j] = mfma(af[st & 1][i], bq[st & 1][j], first ? bz4[i] : acc[i][j]);
+            if (q == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+              if (st + 1 < S) ld(st + 1, (st + 1) & 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
           }
-          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
         }
         if (!IP && p1_last) p1_epilogue();
         if (!IP && p2_first && has_next) store_win();  // P1 reads of the window ended at the last barrier
@@ -638,7 +649,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
   // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
   // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.
-  if ((C == 64 && cfg != 9 && (cfg < 20 || cfg == 32 || cfg == 33)) || cfg == 30 || cfg == 31) {
+  if ((C == 64 && cfg != 9 && (cfg < 20 || (cfg >= 32 && cfg <= 35))) || cfg == 30 || cfg == 31) {
     int handled = 0;
     const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;
@@ -705,6 +716,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // (k = 11: 0.69 -> 0.83 ms; MFMA busy 46.5 -> 38.6 %, waits on the fragment loads 56 % of wave
     // cycles -- one tap of prefetch does not cover the L1 / L2 latency of 64 KiB of fragment loads
     // per tap per CU, and a deeper ring does not fit the registers)
+    if (cfg == 60) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, true, true, true, false, true>(a, B, st);
     if (cfg == 9) {  // the previous defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
@@ -713,7 +725,10 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // the MFMA loop): k = 3 with half-tap buffers (-10 %), k >= 7 with whole taps (-4..6 %)
     // against the 128 / 192-row kernels (tools/ab_sb.py pair 9 6 7)
     if (K <= 3) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
-    return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
+    // round 3: the software-pipelined steps (SB: the next (tap, plane) step's fragments read right
+    // after the current step's first MFMA) -1..2 % at k = 7 / 11, bit-identical (pair_cfg 61 = without)
+    if (cfg == 61) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
+    return pair_launch<128, 2, 4, 4, false, 1, 0, 0, true, true, true, false, true>(a, B, st);
   }
   // C = 64: k = 3 -> both convs resident in LDS; k >= 7 -> 2-tap groups, register staged.
   // pair_cfg 3 / 4 / 5: 512-row IP + LDS-DMA / 384-row IP + LDS-DMA / 512-row IP (the default)

@@ -35,7 +35,10 @@ constexpr int PAIR2_DMAX = 5;
 
 // VD (round 3, "VALU diet"): each conv's bias is the C operand of its first MFMAs (no accumulator
 // zeroing, no bias adds), leaky ReLU in packed fp32, the T1 mask only in boundary tiles.
-template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true>
+// PIPE (round 3): each group's (tap, plane) steps software-pipelined as in resblock3.hip -- the next
+// step's fragments are read right after the current step's first MFMA (two register sets); bit 0: P1,
+// bit 1: P2 (where the next tile's window slots are live too)
+template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true, int PIPE = 0>
 __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a) {
   constexpr int NW = WC * WT;
   constexpr int NT = NW * 64;
@@ -220,6 +223,43 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // S_c steps; aptr(st) / bptr(st): the step's A (weights) and B (activation rows) base addresses;
+  // valid(st): the step's tap exists; bias_row >= 0 (compile-time after inlining): bias as C
+  auto piped = [&](auto S_c, auto&& aptr, auto&& bptr, auto&& valid, int bias_row) {
+    constexpr int S = decltype(S_c)::value;
+    Frag<bf16_t> fa[2][NI], fb[2][NJ];
+    auto ld = [&](int st, int set) {
+      const bf16_t* pa = aptr(st);
+      const bf16_t* pb = bptr(st);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) fa[set][i].load(pa + a_off[i]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[set][j].load(pb + 16 * j * 32);
+    };
+    f32x4 bz4[NI];
+    if (bias_row >= 0) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) bz4[i] = *reinterpret_cast<const f32x4*>(sbias + bias_row * C + n0 + 4 * i);
+    }
+    ld(0, 0);
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+      const int set = st & 1;
+      const bool ok = valid(st), first = bias_row >= 0 && st == 0;
+#pragma unroll
+      for (int q = 0; q < NI * NJ; ++q) {
+        const int i = q / NJ, j = q - i * NJ;
+        if (ok) acc[i][j] = mfma(fa[set][i], fb[set][j], first ? bz4[i] : acc[i][j]);
+        if (q == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (st + 1 < S) ld(st + 1, (st + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   for (; tile < tile_end; ++tile) {
     const int b = tile / a.tiles_per_b;
     const int t0 = (tile - b * a.tiles_per_b) * BT;
@@ -241,8 +281,14 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
     auto p1_group = [&](int g, bool first) {
       load_group(g + 1, (gc + 1) & 1);  // g = NG - 1: P2's first group
       const bf16_t* wb = wls + (gc & 1) * GE;
+      if constexpr ((PIPE & 1) != 0) {
+        piped(std::integral_constant<int, TG * NC>{},
+              [&](int st) { return wb + (st / NC) * TAPE + (st % NC) * C * 32; },
+              [&](int st) { return reg + (st % NC) * WR * 32 + rb_off(brow0 + (g * TG + st / NC) * dil, lq, 2); },
+              [&](int st) { return TG == 1 || g * TG + st / NC < K; }, VD && first ? 0 : -1);
+      }
 #pragma unroll
-      for (int t = 0; t < TG; ++t) {
+      for (int t = 0; t < ((PIPE & 1) ? 0 : TG); ++t) {
         if (g * TG + t >= K) continue;
 #pragma unroll
         for (int c = 0; c < NC; ++c)
@@ -322,8 +368,14 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
       for (int s = s_lo; s < s_hi; ++s) load_slot(s, has_next ? tile + 1 : tile);
       __builtin_amdgcn_sched_barrier(0);
       const bf16_t* wb = wls + (gc & 1) * GE;
+      if constexpr ((PIPE & 2) != 0) {
+        piped(std::integral_constant<int, TG * NC>{},
+              [&](int st) { return wb + (st / NC) * TAPE + (st % NC) * C * 32; },
+              [&](int st) { return reg + (st % NC) * WR * 32 + rb_off(brow0 + g * TG + st / NC, lq, 2); },
+              [&](int st) { return TG == 1 || g * TG + st / NC < K; }, VD && g == 0 ? 1 : -1);
+      }
 #pragma unroll
-      for (int t = 0; t < TG; ++t) {
+      for (int t = 0; t < ((PIPE & 2) ? 0 : TG); ++t) {
         if (g * TG + t >= K) continue;
 #pragma unroll
         for (int c = 0; c < NC; ++c)
@@ -413,7 +465,7 @@ __global__ void __launch_bounds__(WC * WT * 64, 2) mrf_pair2_kernel(Pair2Args a)
   }
 }
 
-template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true>
+template <int C, int WC, int WT, int NJ, int K, bool GL, int TG, bool VD = true, int PIPE = 0>
 static int pair2_launch(Pair2Args a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int R1 = WT * 16 * NJ;
@@ -428,7 +480,7 @@ static int pair2_launch(Pair2Args a, int B, hipStream_t st) {
     vo_set_error("resblock_pair (v2): LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_pair2_kernel<C, WC, WT, NJ, K, GL, TG, VD>;
+  auto kern = mrf_pair2_kernel<C, WC, WT, NJ, K, GL, TG, VD, PIPE>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -471,6 +523,14 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
   if (cfg == 33) {
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, true>(a, B, st);
     return pair2_launch<64, 1, 8, 4, 11, false, 2, false>(a, B, st);
+  }
+  if (cfg == 34 || cfg == 35) {  // software-pipelined steps (PIPE): 34 = both phases, 35 = P1 only
+    if (cfg == 34) {
+      if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, false, 3>(a, B, st);
+      return pair2_launch<64, 1, 8, 4, 11, false, 2, true, 3>(a, B, st);
+    }
+    if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, false, 1>(a, B, st);
+    return pair2_launch<64, 1, 8, 4, 11, false, 2, true, 1>(a, B, st);
   }
   if (cfg == 31) {
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, true, 2>(a, B, st);

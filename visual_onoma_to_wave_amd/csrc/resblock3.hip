@@ -49,7 +49,11 @@ constexpr int RB3_HALO = 12;  // valid rows lost per side: sum over the six conv
 // TPG (round 3): taps per streamed group -- 3 = a whole conv per group, so the group's wait and
 // barrier coincide with the conv-end barrier the region rewrite needs anyway (6 barriers per tile
 // instead of 24, 96 MFMAs per wave between them at C = 64)
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1>
+// PIPE (round 3, whole-conv groups only): the conv's 3 x NC (tap, plane) steps software-pipelined --
+// the fragments of step st + 1 are read before the MFMAs of step st (two register sets, pinned by
+// sched_barrier; hipcc otherwise issues each A fragment right before its MFMAs and waits for it)
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1,
+          bool PIPE = false>
 __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_kernel(Rb3Args a) {
   // streamed-weight blocks: bare LDS barriers (the fence of __syncthreads drains the window
   // prefetch and the y stores at every group); resident-weight (C = 32) blocks keep
@@ -76,6 +80,7 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   constexpr int NG = 18;                   // taps per tile: 3 stages x 2 convs x 3 taps
   constexpr int D = NBUF - 1;              // DMA prefetch distance in groups
   static_assert(TPG == 1 || (TPG == 3 && SPLIT == 1 && !RESW), "whole-conv groups: 3 taps, unsplit");
+  static_assert(!PIPE || (!RESW && SPLIT == 1), "PIPE: streamed whole taps / convs");
   constexpr int NGR = TPG > 1 ? NG / TPG : NG * SPLIT;  // streamed groups per tile
   constexpr int GE = TPG > 1 ? TPG * TAPE : TAPE / SPLIT;  // LDS elements per group buffer
   constexpr int GPL = NC / SPLIT;          // planes per group tap
@@ -210,8 +215,64 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
     for (int cv = 0; cv < 6; ++cv) {  // conv cv: stage cv / 2, c1 (even) or c2 (odd)
       const int s = cv >> 1, ph = cv & 1;
       const int step = ph ? 1 : a.dil[s];
+      if constexpr (PIPE) {
+        static_assert((TPG == 3 || TPG == 1) && !RESW && SPLIT == 1, "PIPE: streamed whole taps / convs");
+        constexpr int NKG = 3 / TPG;  // groups per conv
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {  // taps (compile-time: the conv's first step is known statically)
+        for (int kg = 0; kg < NKG; ++kg) {
+          const int g = cv * NKG + kg;  // group of the tile
+          load_grp(g + D < NGR ? g + D : g + D - NGR, (gcount + D) % NBUF);
+          const bf16_t* wb0 = wls + (gcount % NBUF) * GE;
+          if (g == 0) {  // the tile's x rows (see below)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int pos = min(max(p0 + wt * 16 * NJ + 16 * j + lr, 0), T - 1);
+              const int64_t off = ((int64_t)b * T + pos) * C + n0;
+#pragma unroll
+              for (int h = 0; h < NH; ++h) xres[j][h] = *reinterpret_cast<const u32x4*>(a.x + off + 8 * h);
+            }
+          }
+          constexpr int S = TPG * NC;
+          Frag<bf16_t> fa[2][NI], fb[2][NJ];
+          auto ld = [&](int st, int set) {
+            const int t = st / NC, c = st - t * NC, k = kg * TPG + t;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) fa[set][i].load(wb0 + t * TAPE + c * C * 32 + a_off[i]);
+            const int boff = c * RR * 32 + rb_off(brow0 + (k - 1) * step, lq, 2);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) fb[set][j].load(reg + boff + 16 * j * 32);
+          };
+          // the next step's reads go out after the step's first MFMA: the wait before it then covers
+          // only reads issued a whole step earlier (16 outstanding reads exceed the 4-bit lgkmcnt, and
+          // with both sets in flight hipcc waited for all of them, the just-issued ones included)
+          f32x4 bz4[NI];
+          if (VD && kg == 0) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) bz4[i] = *reinterpret_cast<const f32x4*>(sbias + cv * C + n0 + 4 * i);
+          }
+          ld(0, 0);
+#pragma unroll
+          for (int st = 0; st < S; ++st) {
+            const int set = st & 1;
+#pragma unroll
+            for (int q = 0; q < NI * NJ; ++q) {
+              const int i = q / NJ, j = q - i * NJ;
+              acc[i][j] = mfma(fa[set][i], fb[set][j], VD && kg == 0 && st == 0 ? bz4[i] : acc[i][j]);
+              if (q == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (st + 1 < S) ld(st + 1, (st + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * GLN) : "memory");
+          bar();
+          ++gcount;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < (PIPE ? 0 : 3); ++k) {  // taps (compile-time: the conv's first step is known statically)
       const int g = cv * 3 + k;
       const int row = brow0 + (k - 1) * step;
 #pragma unroll
@@ -473,7 +534,8 @@ __global__ void __launch_bounds__(WC * WT * 64, WC * WT == 4 ? 2 : 1) mrf_rb3_ke
   }
 }
 
-template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1>
+template <int C, int WC, int WT, int NJ, bool RESW, int SPLIT = 1, int NBUF = 2, bool VD = true, int TPG = 1,
+          bool PIPE = false>
 static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
   constexpr int NW = WC * WT;
   constexpr int F = WT * 16 * NJ;
@@ -487,7 +549,7 @@ static int rb3_launch(Rb3Args a, int B, hipStream_t st) {
     vo_set_error("resblock3: LDS %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF, VD, TPG>;
+  auto kern = mrf_rb3_kernel<C, WC, WT, NJ, RESW, SPLIT, NBUF, VD, TPG, PIPE>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -563,11 +625,18 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
     if (cfg == 6) return rb3_launch<64, 1, 4, 4, false, 1, 3>(a, B, st);
     if (cfg == 40) return rb3_launch<64, 1, 8, 4, false>(a, B, st);  // one tap per group (round 2 / 3)
     if (cfg == 41) return rb3_launch<64, 1, 8, 3, false, 1, 2, true, 3>(a, B, st);
+    if (cfg == 43) return rb3_launch<64, 1, 8, 3, false, 1, 2, true, 3, true>(a, B, st);
+    if (cfg == 44) return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 1, true>(a, B, st);
     // a whole conv (3 taps, 24 KB) per streamed group: 6 barriers per tile instead of 24, 0.476 ->
-    // 0.448 ms (tools/mrf_bench.py --stages 2 --tune rb3_cfg=0,40, round 3, bit-identical)
-    return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3>(a, B, st);
+    // 0.448 ms (tools/mrf_bench.py --stages 2 --tune rb3_cfg=0,40, round 3, bit-identical); with the
+    // software-pipelined steps (PIPE) 0.443 -> 0.437 ms
+    if (cfg == 45) return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3>(a, B, st);
+    return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3, true>(a, B, st);
   }
   if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
   if (cfg == 4) return rb3_launch<128, 2, 4, 4, false, 2, 4>(a, B, st);
-  return rb3_launch<128, 2, 4, 4, false>(a, B, st);
+  // software-pipelined steps (PIPE: the next (tap, plane) step's fragments read during the current
+  // step's MFMAs): 0.720 -> 0.686 ms, bit-identical (tools/mrf_bench.py --tune rb3_cfg=0,42, round 3)
+  if (cfg == 42) return rb3_launch<128, 2, 4, 4, false>(a, B, st);
+  return rb3_launch<128, 2, 4, 4, false, 1, 2, true, 1, true>(a, B, st);
 }
