@@ -112,12 +112,12 @@ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
 // round trip per JG positions instead of one per position: the scalar form waited for each row's
 // load before its store, 8 times per 128-row wave tile), 16-byte loads and stores; the same
 // arithmetic in the same order as the scalar form (bit-identical)
-template <int NI, int NJ>
+template <int NI, int NJ, int EJ = 2>
 __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0, int n0,
                                                   int wave_t0, int lr) {
   static_assert(NI % 2 == 0, "8-channel runs");
   constexpr int NH = NI / 2;
-  constexpr int JG = NJ < 2 ? NJ : 2;
+  constexpr int JG = NJ < EJ ? NJ : EJ;  // position tiles whose rows are requested together
   bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (int64_t)b * a.ybs;
   const bf16_t* R1 = reinterpret_cast<const bf16_t*>(a.res1 ? a.res1 : a.y) + (int64_t)b * a.ybs;
   const bf16_t* R2 = reinterpret_cast<const bf16_t*>(a.res2 ? a.res2 : a.y) + (int64_t)b * a.ybs;
@@ -180,7 +180,7 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc
   }
 }
 
-template <typename TOUT, int NI, int NJ>
+template <typename TOUT, int NI, int NJ, int EJ = 2>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI][NJ], int b, int t0, int co_blk,
                                               int wave_co0, int wave_t0, int lane) {
   const int lr = lane & 15;
@@ -190,7 +190,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
   if constexpr (std::is_same<TOUT, bf16_t>::value && NI % 2 == 0) {
     // uniform per launch: plain conv, 8-element aligned rows, the lane's whole run inside Co
     if (!a.transposed && (a.ldy & 7) == 0 && (a.ybs & 7) == 0 && a.Co % (4 * NI) == 0) {
-      conv_epilogue_vec<NI, NJ>(a, acc, b, t0, n0, wave_t0, lr);
+      conv_epilogue_vec<NI, NJ, EJ>(a, acc, b, t0, n0, wave_t0, lr);
       return;
     }
   }
@@ -312,7 +312,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // (issued one chunk ahead, they got one step to land); and the step barriers are bare s_barrier
 // (LDS writes drained by lgkmcnt): __syncthreads' workgroup release fence waits vmcnt(0) too.
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
   constexpr int NT = WCO * WT * 64;
@@ -671,7 +671,7 @@ conv1d_kernel(ConvArgs a) {
     conv_partial_store<NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
     return;
   }
-  conv_epilogue<TOUT, NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
+  conv_epilogue<TOUT, NI, NJ, EJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
 }
 
 // split reduction, second pass: y = epilogue(sum_z partial[z] + bias) with the partials added
@@ -744,7 +744,7 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -777,7 +777,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS>
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS, EJ>
                    : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
   a.partial = nullptr;
   a.kcs = 0;
@@ -802,9 +802,9 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
 }
 
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, bool GL = false, bool RS = false>
+          int PRIO = 0, int ABL = 0, bool GL = false, bool RS = false, int EJ = 2>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
-  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL, RS>(d, st);
+  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL, RS, EJ>(d, st);
 }
 
 // HiFi-GAN discriminator layers (strided and/or grouped, C5): 64-row tiles so that a stride-4
@@ -963,6 +963,11 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
         // window, bind) -- k >= 5 only; conv_cfg 5 forces it, 6 disables it (tools/probes/s0_probe.py,
         // bit-identical)
         const int cc = vo_tune_get("conv_cfg");
+        // Round 3, measured and dropped (tools/mrf_bench.py --stages 0, conv pairs): 4-wave tiles, two
+        // workgroups per CU (256 co x 128 rows, 1 tap per step, with and without RS; 128 co x 256 rows)
+        // -- 27-45 % slower than the 8-wave 256 x 256 tile at k = 3 / 7 / 11
+        // (EJ, the epilogue's position tiles whose residual / accumulator rows are requested
+        // together: 4 measured within 1 % of 2, 8 spills and runs 10-20 % slower -- kept at 2)
         if (cc == 5 || (cc != 6 && d->K >= 5))
           return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true, true>(d, st);
         return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1, 0, true>(d, st);
