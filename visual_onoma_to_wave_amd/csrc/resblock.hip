@@ -700,7 +700,9 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // around its MFMA clusters (PRIO 1) within noise -- neither kept.
     // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
     // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
-    // SIMD (12 waves, 2 x 6) 15 % slower.
+    // SIMD (12 waves, 2 x 6) 15 % slower  Round 3, remeasured with the pinned fragment pipeline
+    // (SB) and 512 registers per wave (launch bounds 1 workgroup / CU): 20-27 % slower at k = 7 / 11
+    // (tools/mrf_bench.py, profiles/r03/s1_one_wave_per_simd_ab.txt), 2 % faster at k = 3.
     // timing ablations (VO_ABLATIONS builds only): no window / residual loads 0.70 -> 0.58 ms at
     // k = 11, 0.52 -> 0.41 at k = 7 (cfg 17); no weight DMA 0.70 -> 0.63 (cfg 25).  Measured and
     // dropped in round 2 (tools/ab_pair2.py): the next window staged through registers during P2
