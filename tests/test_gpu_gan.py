@@ -349,6 +349,48 @@ def test_conv1d_wgrad_vs_torch(B, T, Ci, Co, K, dil, s, pad, pre, dt, tol):
     assert torch.equal(gb, ops.colsum(gy.cuda().to(dt).contiguous()))
 
 
+@pytest.mark.parametrize("B,T,Ci,Co,K,dil,g,bias,kg", [
+    # MRF shapes (C5 generator stages), the tap run split by the plan or forced (wgrad_kg)
+    (4, 2048, 128, 128, 11, 5, 1, True, 0), (4, 2048, 128, 128, 11, 1, 1, False, 3), (3, 4096, 64, 64, 7, 3, 1, True, 0),
+    (8, 8192, 32, 32, 11, 5, 1, True, 0), (8, 8192, 32, 32, 3, 1, 1, False, 0), (16, 256, 256, 256, 11, 5, 1, True, 0),
+    # ragged T (last chunk of each utterance partial), window at its 128-row limit, K > 10 split into runs
+    (3, 777, 128, 64, 9, 8, 1, True, 0), (2, 1000, 32, 32, 11, 6, 1, False, 11), (2, 64, 1024, 1024, 41, 1, 16, False, 0),
+    # Ci = 1 padded to 8 (MSD's first conv), Linears (K = 1), T shorter than a chunk
+    (4, 4096, 8, 128, 15, 1, 1, True, 0), (2, 777, 1024, 256, 1, 1, 1, True, 0), (5, 12, 256, 256, 3, 1, 1, True, 0)])
+def test_conv1d_wgrad_multitap_vs_per_tap(B, T, Ci, Co, K, dil, g, bias, kg):
+    """The multi-tap weight gradient (stride-1 bf16: one staged dY chunk and x window per run of taps)
+    against the per-tap kernel (vo_tune wgrad_mt 1) on the same bf16 operands -- fp32 sums of the same
+    products in different groupings: <= 1e-6 rel-L2 -- and against torch; deterministic run to run."""
+    from visual_onoma_to_wave_amd import _lib, ops
+    L = _lib.lib()
+    gen = torch.Generator().manual_seed(B * T + K * dil + Ci)
+    pad = dil * (K - 1) // 2
+    x = torch.randn(B, T, Ci, generator=gen).to(torch.bfloat16)
+    T_out = T + 2 * pad - dil * (K - 1)
+    gy = torch.randn(B, T_out, Co, generator=gen).to(torch.bfloat16)
+    xa, gya = x.cuda(), gy.cuda()
+    kw = dict(S=1, dil=dil, pad=pad, pre_b=None if bias else 0.1, groups=g, with_bias=bias)
+    try:
+        assert L.vo_tune(b"wgrad_mt", 1) == 0
+        ref = ops.conv1d_wgrad(gya, xa, K, **kw)
+        assert L.vo_tune(b"wgrad_mt", 0) == 0 and L.vo_tune(b"wgrad_kg", kg) == 0
+        got = ops.conv1d_wgrad(gya, xa, K, **kw)
+        again = ops.conv1d_wgrad(gya, xa, K, **kw)
+    finally:
+        L.vo_tune(b"wgrad_mt", 0)
+        L.vo_tune(b"wgrad_kg", 0)
+    refw, gotw, agw = (ref[0], got[0], again[0]) if bias else (ref, got, again)
+    assert torch.equal(gotw, agw)
+    assert rel_l2(gotw.cpu(), refw.cpu()) < 1e-6, rel_l2(gotw.cpu(), refw.cpu())
+    xt = x.float() if bias else F.leaky_relu(x.float(), 0.1).to(torch.bfloat16).float()  # staged as bf16
+    tw = torch.nn.grad.conv1d_weight(xt.transpose(1, 2), (Co, Ci // g, K), gy.float().transpose(1, 2), padding=pad,
+                                     dilation=dil, groups=g)
+    assert rel_l2(gotw.cpu(), tw) < 1e-5
+    if bias:
+        assert torch.equal(got[1], again[1])
+        assert rel_l2(got[1].cpu(), gy.float().sum((0, 1))) < 1e-5
+
+
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
     (2, 1000, 128, 128, 41, 2, 4, 20), (2, 777, 128, 256, 41, 4, 16, 20), (3, 300, 256, 512, 41, 4, 16, 20),

@@ -31,6 +31,7 @@ def main():
     sys.argv = ["bench.py", "--mode", "gan", "--steps", "1", "--warmup", "1", "--no-graph", "--cpu-seconds", "0"]
     ops.conv1d_wgrad = timed
     a = bench.parse()
+    a.ranks_seen = [0]
     dev = torch.device("cuda")
     bench.bench_gan(a, dev, 0, 1, None)
     tot = sum(v[1] for v in stats.values())

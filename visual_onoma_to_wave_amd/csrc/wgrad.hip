@@ -44,6 +44,7 @@ struct WgradArgs {
   int64_t n_tot;  // n_w + groups * M (with bias) or n_w: floats per split
   bool bias;  // bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
   int abl;  // timing ablation (wgrad_cfg 11): 2 = no loads
+  int gpt;  // groups per tile (grouped convs with narrow groups, per-tap kernel): see wgrad_gpt
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
 // and B columns [g N, (g+1) N) and writes block g of the (groups, K, M, N) result
@@ -67,15 +68,18 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   __shared__ __attribute__((aligned(16))) TC sb[WG_R * P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
-  const int tiles_n = (p.N + WG_T - 1) / WG_T;
+  // gpt > 1: gpt consecutive groups share one tile -- their A columns (gpt M) and B columns (gpt N)
+  // are contiguous, the tile computes the whole gpt M x gpt N product and keeps its diagonal blocks
+  const int Mv = p.M * p.gpt, Nv = p.N * p.gpt;
+  const int tiles_n = (Nv + WG_T - 1) / WG_T;
   const int m0 = (blockIdx.y / tiles_n) * WG_T, n0 = (blockIdx.y % tiles_n) * WG_T;
-  const int k = blockIdx.z % p.K, grp = blockIdx.z / p.K;
+  const int k = blockIdx.z % p.K, grp = (blockIdx.z / p.K) * p.gpt;
   const int64_t rows = (int64_t)p.Bn * p.T_A;
   const int64_t r_begin = (int64_t)blockIdx.x * p.rows_per_split;
   const int64_t r_end = min(rows, r_begin + p.rows_per_split);
   const TC* A = reinterpret_cast<const TC*>(p.a) + (int64_t)grp * p.M;
   const TC* Bs = reinterpret_cast<const TC*>(p.bsrc) + (int64_t)grp * p.N;
-  float* dw = p.part + (int64_t)blockIdx.x * p.n_tot + ((int64_t)grp * p.K + k) * p.M * p.N;
+  float* dw = p.part + (int64_t)blockIdx.x * p.n_tot;
   constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
   constexpr int VPR = WG_T / EV;            // vectors per staged row
   constexpr int NV = WG_R * VPR / 256;      // vectors per thread per operand
@@ -104,15 +108,15 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       const int b = (int)(qq / p.T_A), t = (int)(qq - (int64_t)b * p.T_A);
       const int tb = t * p.S + k * p.dil - p.pad;
       const bool bok = qok && tb >= 0 && tb < p.T_B;
-      const int ma = min(m0 + c, p.M - EV), nb = min(n0 + c, p.N - EV);
+      const int ma = min(m0 + c, Mv - EV), nb = min(n0 + c, Nv - EV);
       if (p.abl & 2) {
         va[s] = vb[s] = u32x4_t{(unsigned)tb, (unsigned)ma, 1u, 1u};
       } else {
         va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + ma);
         vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + min(max(tb, 0), p.T_B - 1)) * p.ldb + nb);
       }
-      if (!qok || m0 + c >= p.M) va[s] = u32x4_t{0u, 0u, 0u, 0u};
-      if (!bok || n0 + c >= p.N) vb[s] = u32x4_t{0u, 0u, 0u, 0u};
+      if (!qok || m0 + c >= Mv) va[s] = u32x4_t{0u, 0u, 0u, 0u};
+      if (!bok || n0 + c >= Nv) vb[s] = u32x4_t{0u, 0u, 0u, 0u};
     }
     __syncthreads();  // previous chunk's fragment reads are done
 #pragma unroll
@@ -200,7 +204,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
     __shared__ float bred[4][64];
     bred[tid >> 6][tid & 63] = bsum;
     __syncthreads();
-    if (tid < 64 && m0 + tid < p.M)
+    if (tid < 64 && m0 + tid < Mv)
       p.part[(int64_t)blockIdx.x * p.n_tot + p.n_w + (int64_t)grp * p.M + m0 + tid] =
           bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
   }
@@ -214,8 +218,192 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
-        if (m < p.M && n < p.N) dw[(int64_t)m * p.N + n] = acc[i][j][e];
+        const int gm = m / p.M;  // group of the row (0 unless gpt > 1); keep the diagonal blocks
+        if (m < Mv && n < Nv && gm == n / p.N)
+          dw[(((int64_t)(grp + gm) * p.K + k) * p.M + (m - gm * p.M)) * p.N + (n - gm * p.N)] = acc[i][j][e];
       }
+}
+
+// Multi-tap weight gradient (round 3; stride-1 convs, bf16): the per-tap kernel above restages
+// both operands for every tap -- a K = 11 conv reads dY and x eleven times and feeds 8 MFMAs per
+// wave per staged 16 KB (C5's MRF weight gradients ran at 0.05-0.18 PF/s).  Here a workgroup owns
+// a TM x TM tile for a run of up to KG taps: per 64-row chunk it stages A (64 rows) and the B WINDOW
+// (64 + (nk - 1) dil rows) once, and every tap reads its B fragments at a row offset k * dil of that
+// window (the transposed LDS reads name their row per lane, so a shift costs nothing) -- nk x the
+// MFMAs per staged byte.  Chunks never cross an utterance (64-row chunks per utterance, the last one
+// zero-padded), so the window of a chunk is one contiguous run of B rows.  The next chunk is loaded
+// into registers during the current chunk's MFMAs.  Partials, their order and the reduce are the
+// per-tap kernel's (tap-major [split][group][k][M][N]; the tap run only changes which workgroup
+// computes a tap), so the result is deterministic run to run; per element the sum over a split's
+// rows runs in the same chunk / k-step order as the per-tap kernel.
+constexpr int WM_R = 64;       // rows per chunk
+constexpr int WM_MAXW = 128;   // window rows: 64 + (nk - 1) * dil <= 128
+
+template <int TM, int KG>
+__global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunks_per_b, int chunks_per_split,
+                                                         int ntg) {
+  constexpr int P = TM == 64 ? 72 : 48;  // pitch (elements): the 4 rows of a transposed read on distinct banks
+  constexpr int WT = TM / 2;             // wave sub-tile (2 x 2 waves)
+  constexpr int MI = WT / 16;            // MFMA tiles per wave and dimension
+  constexpr int VPR = TM / 8;            // 16-byte vectors per staged row
+  constexpr int NVA = WM_R * VPR / 256;  // A vectors per thread
+  constexpr int NVB = WM_MAXW * VPR / 256;  // B window vectors per thread (upper bound)
+  __shared__ __attribute__((aligned(16))) bf16_t sa[WM_R * P];
+  __shared__ __attribute__((aligned(16))) bf16_t sb[WM_MAXW * P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave & 1) * WT, wn = (wave >> 1) * WT;
+  const int tiles_n = (p.N + TM - 1) / TM;
+  const int m0 = (blockIdx.y / tiles_n) * TM, n0 = (blockIdx.y % tiles_n) * TM;
+  const int tg = blockIdx.z % ntg, grp = blockIdx.z / ntg;
+  const int k0 = tg * KG, nk = min(KG, p.K - k0);
+  const int WR = WM_R + (nk - 1) * p.dil;  // window rows of this tap run
+  const int c_begin = blockIdx.x * chunks_per_split;
+  const int c_end = min(p.Bn * chunks_per_b, c_begin + chunks_per_split);
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.a) + (int64_t)grp * p.M;
+  const bf16_t* Bs = reinterpret_cast<const bf16_t*>(p.bsrc) + (int64_t)grp * p.N;
+  float* dw = p.part + (int64_t)blockIdx.x * p.n_tot;
+
+  f32x4 acc[KG][MI][MI];
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < MI; ++j) acc[kk][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = p.bias && tg == 0 && n0 == 0;  // workgroup-uniform
+  float bsum = 0.f;
+
+  // two register sets, alternated by the 2x-unrolled chunk loop: a chunk's loads are issued two
+  // chunks of MFMAs before its LDS store (one chunk was too short to cover the load latency)
+  u32x4_t va0[NVA], vb0[NVB], va1[NVA], vb1[NVB];
+  auto load = [&](int c, u32x4_t (&va)[NVA], u32x4_t (&vb)[NVB]) {  // chunk c -> registers (unconditional
+                                                                   // loads, clamped; zeroed when stored)
+    const int b = c / chunks_per_b, t0 = (c - b * chunks_per_b) * WM_R;
+#pragma unroll
+    for (int s = 0; s < NVA; ++s) {
+      const int v = tid + s * 256, r = v / VPR, col = (v % VPR) * 8;
+      const int t = min(t0 + r, p.T_A - 1);
+      va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + min(m0 + col, p.M - 8));
+    }
+    const int tb0 = t0 - p.pad + k0 * p.dil;
+#pragma unroll
+    for (int s = 0; s < NVB; ++s) {
+      const int v = tid + s * 256, w = v / VPR, col = (v % VPR) * 8;
+      const int tb = min(max(tb0 + w, 0), p.T_B - 1);
+      vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + tb) * p.ldb + min(n0 + col, p.N - 8));
+    }
+  };
+  auto store = [&](int c, const u32x4_t (&va)[NVA], const u32x4_t (&vb)[NVB]) {
+    const int b = c / chunks_per_b, t0 = (c - b * chunks_per_b) * WM_R;
+    (void)b;
+#pragma unroll
+    for (int s = 0; s < NVA; ++s) {
+      const int v = tid + s * 256, r = v / VPR, col = (v % VPR) * 8;
+      u32x4_t x = va[s];
+      if (t0 + r >= p.T_A || m0 + col >= p.M) x = u32x4_t{0u, 0u, 0u, 0u};
+      if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
+      *reinterpret_cast<u32x4_t*>(sa + r * P + col) = x;
+    }
+    const int tb0 = t0 - p.pad + k0 * p.dil;
+#pragma unroll
+    for (int s = 0; s < NVB; ++s) {
+      const int v = tid + s * 256, w = v / VPR, col = (v % VPR) * 8;
+      if (w < WR) {  // uniform per 8-lane row group; rows past the window are never read
+        u32x4_t y = vb[s];
+        const int tb = tb0 + w;
+        if (tb < 0 || tb >= p.T_B || n0 + col >= p.N) y = u32x4_t{0u, 0u, 0u, 0u};
+        if (p.pre_b) y = u32x4_t{lrelu_pack(y.x, p.slope), lrelu_pack(y.y, p.slope), lrelu_pack(y.z, p.slope), lrelu_pack(y.w, p.slope)};
+        *reinterpret_cast<u32x4_t*>(sb + w * P + col) = y;
+      }
+    }
+  };
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  // fragment of 16 channels (c0 + li) x 8 rows (row0 + 8 g ..): two transposed 4-row reads
+  auto frag = [&](const bf16_t* tile, int row0, int c0) {
+    const bf16_t* base = tile + (row0 + 8 * g + q) * P + c0 + 4 * pp;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)base);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + 4 * P));
+    Frag<bf16_t> f;
+    f.v = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return f;
+  };
+
+  auto compute = [&]() {
+    if (do_bias) {
+      const int col = tid & 63, r16 = (tid >> 6) * 16;
+      if (col < TM) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bsum += to_f32(sa[(r16 + i) * P + col]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < WM_R / 32; ++ks) {
+      Frag<bf16_t> fa[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = frag(sa, ks * 32, wm + 16 * i);
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk) {
+        if (kk < nk) {  // uniform
+          Frag<bf16_t> fb[MI];
+#pragma unroll
+          for (int j = 0; j < MI; ++j) fb[j] = frag(sb, ks * 32 + kk * p.dil, wn + 16 * j);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < MI; ++j) acc[kk][i][j] = mfma(fa[i], fb[j], acc[kk][i][j]);
+        }
+      }
+    }
+  };
+  if (c_begin < c_end) {
+    load(c_begin, va0, vb0);
+    store(c_begin, va0, vb0);
+  }
+  __syncthreads();
+  if (c_begin + 1 < c_end) load(c_begin + 1, va0, vb0);
+  for (int c = c_begin; c < c_end; c += 2) {
+    // LDS holds chunk c; set 0 holds chunk c + 1 (in flight)
+    if (c + 2 < c_end) load(c + 2, va1, vb1);
+    compute();
+    __syncthreads();  // every wave is past this chunk's fragment reads
+    if (c + 1 >= c_end) break;
+    store(c + 1, va0, vb0);
+    __syncthreads();
+    if (c + 3 < c_end) load(c + 3, va0, vb0);
+    compute();
+    __syncthreads();
+    if (c + 2 < c_end) {
+      store(c + 2, va1, vb1);
+      __syncthreads();
+    }
+  }
+
+  if (do_bias) {
+    __shared__ float bred[4][64];
+    bred[tid >> 6][tid & 63] = bsum;
+    __syncthreads();
+    if (tid < TM && m0 + tid < p.M)
+      dw[p.n_w + (int64_t)grp * p.M + m0 + tid] = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+  }
+  // D[m][n] (row = m: 4 g + e, col = n: li) -> part[split][grp][k][m][n]
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk) {
+    if (kk < nk) {
+      float* dk = dw + ((int64_t)grp * p.K + k0 + kk) * p.M * p.N;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
+            if (m < p.M && n < p.N) dk[(int64_t)m * p.N + n] = acc[kk][i][j][e];
+          }
+    }
+  }
 }
 
 // dW[((g M + m) N + n) K + k] = sum over splits of part[s][g][k][m][n]; db likewise.
@@ -304,10 +492,22 @@ using namespace vo;
 // row-split plan shared by the workspace query and the launch: enough workgroups to fill 256
 // CUs ~4 deep, at least 4 chunks of 64 rows each, serial row chains of at most 64 chunks (a small
 // tile x tap grid -- the MSD's 32 x 16 groups -- otherwise leaves one workgroup walking every row)
+// groups per tile of the per-tap kernel: narrow groups (the MSD's 16 x 8 .. 64 x 32 per group) are
+// packed side by side up to the 64 x 64 tile (one launch computed a 16 x 8 group in a 64 x 64 tile:
+// 1/32 of its MFMA work useful)
+static int wgrad_gpt(int M, int N, int groups) {
+  if (groups <= 1 || vo_tune_get("wgrad_cfg") == 12) return 1;  // 12: one group per tile (A/B)
+  int gpt = 1;
+  for (int d = 2; d <= groups; ++d)
+    if (groups % d == 0 && d * M <= WG_T && d * N <= WG_T) gpt = d;
+  return gpt;
+}
+
 static void wgrad_plan(int B, int T_A, int M, int N, int K, int groups, int64_t* splits_out, int* rps_out) {
-  const int64_t zk = (int64_t)K * groups;
+  const int gpt = wgrad_gpt(M, N, groups);
+  const int64_t zk = (int64_t)K * (groups / gpt);
   const int64_t rows = (int64_t)B * T_A;
-  const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
+  const int tiles = ((M * gpt + WG_T - 1) / WG_T) * ((N * gpt + WG_T - 1) / WG_T);
   const int wc = vo_tune_get("wgrad_cfg");
   const int64_t target = wc == 1 ? 4096 : wc == 2 ? 8192 : wc == 3 ? 16384 : 1024;
   int64_t splits = std::max<int64_t>(1, (target + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
@@ -319,12 +519,71 @@ static void wgrad_plan(int B, int T_A, int M, int N, int K, int groups, int64_t*
   *rps_out = rps;
 }
 
+// multi-tap plan (wgrad_mt_kernel): the partials of a split cover the whole (K, M, N) output, so
+// splits are capped by their traffic (at most max(operand bytes, 16 MB) of partials); the taps are
+// then cut into runs (ntg per workgroup column) only as far as needed to give ~256 workgroups, the
+// rest of the parallelism comes from splits.  dil bounds a run's window (64 + (KG - 1) dil <= 128
+// rows); the splits never grow with dil, so the plan at dil = 1 sizes the workspace.
+struct MtPlan { int tm, kg, ntg, chunks_per_b, cps, splits; };
+static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int dil, MtPlan* pl) {
+  pl->tm = (M <= 32 && N <= 32) ? 32 : 64;
+  const int64_t tiles = (int64_t)((M + pl->tm - 1) / pl->tm) * ((N + pl->tm - 1) / pl->tm) * groups;
+  pl->chunks_per_b = (T_A + WM_R - 1) / WM_R;
+  const int64_t total = (int64_t)B * pl->chunks_per_b;
+  const int64_t rows = (int64_t)B * T_A;
+  const int64_t operand = rows * ((int64_t)M + N) * groups * 2;
+  const int64_t per_split = ((int64_t)groups * K * M * N + (int64_t)groups * M) * 4;
+  const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(total, std::max<int64_t>(operand, 16 << 20) / per_split));
+  const int kgmax = std::min(pl->tm == 64 ? 8 : 11, 1 + 64 / std::max(dil, 1));  // TM 64 x 9+ taps spill
+  const int forced = vo_tune_get("wgrad_kg");  // A/B: taps per run
+  int ntg = (int)std::max<int64_t>(1, (256 + tiles * smax - 1) / (tiles * smax));
+  int kg = forced > 0 ? forced : (K + ntg - 1) / ntg;
+  kg = std::max(1, std::min(kg, std::min(kgmax, K)));
+  ntg = (K + kg - 1) / kg;
+  pl->kg = kg;
+  pl->ntg = ntg;
+  const int64_t want = std::max<int64_t>(1, (512 + tiles * ntg - 1) / (tiles * ntg));
+  const int64_t splits = std::min(smax, want);
+  pl->cps = (int)((total + splits - 1) / splits);
+  pl->splits = (int)((total + pl->cps - 1) / pl->cps);
+}
+
 extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, int K, int groups) {
   if (B <= 0 || T_A <= 0 || M <= 0 || N <= 0 || K <= 0 || groups <= 0) return 0;
   int64_t splits;
   int rps;
   wgrad_plan(B, T_A, M, N, K, groups, &splits, &rps);
+  MtPlan mt;
+  wgrad_mt_plan(B, T_A, M, N, K, groups, 1, &mt);
+  splits = std::max<int64_t>(splits, mt.splits);
   return splits * ((int64_t)groups * K * M * N + (int64_t)groups * M) * (int64_t)sizeof(float);
+}
+
+template <int TM, int KG>
+static void wgrad_mt_launch(const WgradArgs& p, const MtPlan& pl, int groups, hipStream_t st) {
+  const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
+  hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG>), dim3((unsigned)pl.splits, (unsigned)tiles, (unsigned)(pl.ntg * groups)),
+                     dim3(256), 0, st, p, pl.chunks_per_b, pl.cps, pl.ntg);
+}
+template <int TM>
+static void wgrad_mt_dispatch(const WgradArgs& p, const MtPlan& pl, int groups, hipStream_t st) {
+  switch (pl.kg) {
+    case 1: return wgrad_mt_launch<TM, 1>(p, pl, groups, st);
+    case 2: return wgrad_mt_launch<TM, 2>(p, pl, groups, st);
+    case 3: return wgrad_mt_launch<TM, 3>(p, pl, groups, st);
+    case 4: return wgrad_mt_launch<TM, 4>(p, pl, groups, st);
+    case 5: return wgrad_mt_launch<TM, 5>(p, pl, groups, st);
+    case 6: return wgrad_mt_launch<TM, 6>(p, pl, groups, st);
+    case 7: return wgrad_mt_launch<TM, 7>(p, pl, groups, st);
+    case 8: return wgrad_mt_launch<TM, 8>(p, pl, groups, st);
+  }
+  if constexpr (TM == 32) {  // TM 64 runs at most 8 taps (wgrad_mt_plan)
+    switch (pl.kg) {
+      case 9: return wgrad_mt_launch<32, 9>(p, pl, groups, st);
+      case 10: return wgrad_mt_launch<32, 10>(p, pl, groups, st);
+      default: return wgrad_mt_launch<32, 11>(p, pl, groups, st);
+    }
+  }
 }
 
 extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
@@ -346,12 +605,31 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   p.n_w = (int64_t)groups * K * M * N;
   p.n_tot = p.n_w + (db ? (int64_t)groups * M : 0);
   p.abl = vo_tune_get("wgrad_cfg") == 11 ? 2 : 0;  // 11: no loads (timing)
-  const int64_t zk = (int64_t)K * groups;
-  const int tiles = ((M + WG_T - 1) / WG_T) * ((N + WG_T - 1) / WG_T);
+  p.gpt = 1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // stride-1 bf16 convs: the multi-tap kernel (wgrad_mt 1 = the per-tap kernel, A/B)
+  // (K >= 2 and utterances of >= 8 whole chunks' worth: the per-utterance chunks of short sequences --
+  // the MPD's period columns, T_A = 10-34 -- are mostly padding: 207 us per call against the per-tap
+  // kernel's flattened rows)
+  const int64_t padded = (int64_t)((T_A + WM_R - 1) / WM_R) * WM_R;
+  const bool mt_ok = K >= 2 && 8 * (padded - T_A) <= T_A;
+  if (dtype == VO_BF16 && S == 1 && mt_ok && vo_tune_get("wgrad_mt") != 1 && p.abl == 0) {
+    MtPlan pl;
+    wgrad_mt_plan(B, T_A, M, N, K, groups, dil, &pl);
+    VO_CHECK_ARG(pl.splits < (1 << 30) && pl.ntg * groups < 65536, "conv1d_wgrad: grid too large");
+    if (pl.tm == 32)
+      wgrad_mt_dispatch<32>(p, pl, groups, st);
+    else
+      wgrad_mt_dispatch<64>(p, pl, groups, st);
+    wgrad_reduce_launch(workspace, pl.splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
+    VO_RETURN_LAUNCH();
+  }
+  p.gpt = wgrad_gpt(M, N, groups);
+  const int64_t zk = (int64_t)K * (groups / p.gpt);
+  const int tiles = ((M * p.gpt + WG_T - 1) / WG_T) * ((N * p.gpt + WG_T - 1) / WG_T);
   int64_t splits;
   wgrad_plan(B, T_A, M, N, K, groups, &splits, &p.rows_per_split);
   VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)zk);
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
