@@ -21,7 +21,7 @@ constexpr int KT = 64;  // keys per tile
 
 template <typename TC>
 __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ qkv, const int32_t* __restrict__ lens,
-                                                        int L, int H, float scale, TC* __restrict__ out) {
+                                                        int L, int H, float scale, TC* __restrict__ out, int xcd) {
   constexpr int KP = ATT_DK + 8;  // K tile pitch
   constexpr int VP = KT + 8;      // V^T tile pitch
   constexpr int PP = KT + 8;      // P tile pitch
@@ -30,9 +30,12 @@ __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ q
   __shared__ __attribute__((aligned(16))) TC p_lds[4][16 * PP];
 
   const int D = H * ATT_DK;
-  const int bh = blockIdx.y;
+  // the query tiles of one (b, h) read the same K / V: consecutive logical ids, one XCD's L2
+  const int nq = gridDim.x, wid = blockIdx.x + nq * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nq * gridDim.y) : wid;
+  const int bh = lid / nq;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = blockIdx.x * 64;
+  const int q0 = (lid - bh * nq) * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4, lk = g * 8;
   const int len = lens ? lens[b] : L;
@@ -173,7 +176,8 @@ __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ q
 // tile).
 template <int NONE = 0>
 __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restrict__ qkv, const int32_t* __restrict__ lens,
-                                                         int L, int H, float scale, bf16_t* __restrict__ out) {
+                                                         int L, int H, float scale, bf16_t* __restrict__ out,
+                                                         int xcd) {
   constexpr int P = ATT_DK + 16;  // row pitch (elements): 72 dwords = 8 mod 64 banks
   __shared__ __attribute__((aligned(16))) bf16_t kv_lds[2][2][KT * P];  // [buf][K | V][key][dk]
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -182,9 +186,12 @@ __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restric
   typedef __attribute__((address_space(3))) v4s lds_v4s;
 
   const int D = H * ATT_DK;
-  const int bh = blockIdx.y;
+  // the query tiles of one (b, h) read the same K / V: consecutive logical ids, one XCD's L2
+  const int nq = gridDim.x, wid = blockIdx.x + nq * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nq * gridDim.y) : wid;
+  const int bh = lid / nq;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = blockIdx.x * 64;
+  const int q0 = (lid - bh * nq) * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
   const int len = min(lens ? lens[b] : L, L);
@@ -332,15 +339,16 @@ extern "C" int vo_attention(const void* qkv, int dtype, const int32_t* lens, int
   VO_CHECK_ARG(B > 0 && L > 0 && H > 0, "attention: empty");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)((L + 63) / 64), (unsigned)(B * H));
+  const int xcd = vo_tune_get("att_xcd") != 1;  // att_xcd 1: plain (tile, head) order (A/B)
   if (dtype == VO_BF16 && vo_tune_get("att_cfg") != 1)
     hipLaunchKernelGGL(attention2_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
-                       (bf16_t*)out);
+                       (bf16_t*)out, xcd);
   else if (dtype == VO_BF16)
     hipLaunchKernelGGL(attention_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
-                       (bf16_t*)out);
+                       (bf16_t*)out, xcd);
   else if (dtype == VO_F32)
     hipLaunchKernelGGL(attention_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, lens, L, H, scale,
-                       (float*)out);
+                       (float*)out, xcd);
   else {
     vo_set_error("attention: bad dtype");
     return VO_ERR_INVALID;

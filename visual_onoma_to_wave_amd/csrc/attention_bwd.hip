@@ -53,7 +53,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const TC* __restrict__
                                                           const TC* __restrict__ dout,
                                                           const int32_t* __restrict__ lens, int L, int H,
                                                           float scale, TC* __restrict__ dqkv,
-                                                          float* __restrict__ lse_ws, float* __restrict__ dd_ws) {
+                                                          float* __restrict__ lse_ws, float* __restrict__ dd_ws,
+                                                          int xcd) {
   constexpr int KP = AB_DK + 8;
   constexpr int TP = AB_KT + 8;
   __shared__ __attribute__((aligned(16))) TC k_lds[AB_KT * KP];
@@ -63,9 +64,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const TC* __restrict__
   __shared__ float dd_lds[4][16];
 
   const int D = H * AB_DK;
-  const int bh = blockIdx.y;
+  // the query tiles of one (b, h) read the same K / V: consecutive logical ids, one XCD's L2
+  const int nq = gridDim.x, wid = blockIdx.x + nq * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nq * gridDim.y) : wid;
+  const int bh = lid / nq;
   const int b = bh / H, h = bh - b * H;
-  const int q0 = blockIdx.x * 64;
+  const int q0 = (lid - bh * nq) * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4, lk = g * 8;
   const int len = lens ? min(lens[b], L) : L;
@@ -219,7 +223,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const TC* __restrict
                                                             const int32_t* __restrict__ lens, int L, int H,
                                                             float scale, TC* __restrict__ dqkv,
                                                             const float* __restrict__ lse_ws,
-                                                            const float* __restrict__ dd_ws) {
+                                                            const float* __restrict__ dd_ws, int xcd) {
   constexpr int NT = QT / 16, KS = QT / 32;
   constexpr int QP = AB_DK + 8;
   constexpr int TP = QT + 8;
@@ -232,9 +236,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const TC* __restrict
   __shared__ float lse_s[QT], dd_s[QT];
 
   const int D = H * AB_DK;
-  const int bh = blockIdx.y;
+  // the key tiles of one (b, h) read the same Q / dO: consecutive logical ids, one XCD's L2
+  const int nk = gridDim.x, wid = blockIdx.x + nk * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nk * gridDim.y) : wid;
+  const int bh = lid / nk;
   const int b = bh / H, h = bh - b * H;
-  const int k0 = blockIdx.x * AB_KT;
+  const int k0 = (lid - bh * nk) * AB_KT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4, lk = g * 8;
   const int len = lens ? min(lens[b], L) : L;
@@ -355,16 +362,17 @@ extern "C" int vo_attention_bwd(const void* qkv, const void* out, const void* do
   float* lse = (float*)workspace;
   float* dd = lse + (int64_t)B * H * L;
   dim3 grid((unsigned)((L + 63) / 64), (unsigned)(B * H));
+  const int xcd = vo_tune_get("att_xcd") != 1;  // att_xcd 1: plain (tile, head) order (A/B)
   if (dtype == VO_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)out,
-                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, lse, dd);
+                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, lse, dd, xcd);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<bf16_t, 64>), grid, dim3(256), 0, st, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, (const float*)lse, (const float*)dd);
+                       (const bf16_t*)dout, lens, L, H, scale, (bf16_t*)dqkv, (const float*)lse, (const float*)dd, xcd);
   } else if (dtype == VO_F32) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, (const float*)out,
-                       (const float*)dout, lens, L, H, scale, (float*)dqkv, lse, dd);
+                       (const float*)dout, lens, L, H, scale, (float*)dqkv, lse, dd, xcd);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<float, 32>), grid, dim3(256), 0, st, (const float*)qkv,
-                       (const float*)dout, lens, L, H, scale, (float*)dqkv, (const float*)lse, (const float*)dd);
+                       (const float*)dout, lens, L, H, scale, (float*)dqkv, (const float*)lse, (const float*)dd, xcd);
   } else {
     vo_set_error("attention_bwd: bad dtype");
     return VO_ERR_INVALID;

@@ -42,6 +42,16 @@ __device__ __forceinline__ float lrelu_max(float v, float s) { return __builtin_
 // every outstanding global load or store of the wave (an epilogue's y stores, a prefetch meant to
 // stay in flight across the barrier) is drained at each barrier.  LDS-DMA destinations still
 // need their own vmcnt wait before this barrier; no global memory is handed between waves.
+// Workgroups are dispatched round-robin over the 8 XCDs by linear id (w -> XCD w % 8), and each
+// XCD has its own L2.  xcd_grouped_id(w, n) maps linear id w of an n-workgroup grid to a logical id
+// in [0, n) such that consecutive logical ids run on one XCD: workgroups that read the same bytes
+// (the query tiles of one attention head, ...) take logical ids next to each other and share that
+// XCD's L2 instead of every XCD fetching them.
+__device__ __forceinline__ int xcd_grouped_id(int w, int n) {
+  const int x = w & 7, k = w >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------- 8-element vectors
