@@ -867,7 +867,10 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       // bench step its 12 decoder launches took 818 us against 584 (profiles/r01k/): kept out.
       // ups0 (polyphase 512 -> 8 x 256, K = 2) on the role-split staging was 11-20 % slower (its
       // one-step chunks: 8 weight-DMA pieces per weight wave per 2-tap step; tools/probes/ups0_probe.py)
-      if (d->Co >= 768 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
+      // (unless that leaves fewer than 128 workgroups: the MPD's joined period columns, ~4-5k rows x
+      // 1024 channels, got 68-80 -- there the 128 x 128 tile below)
+      const int64_t t256 = (int64_t)d->B * ((d->T_out + 255) / 256) * (d->Co / 256);
+      if (d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
     }
     // mid-width convs (PostNet 512 -> 512 k5, conv_pre 80 -> 512 k7 at 16384 rows): 128 x 256

@@ -23,7 +23,7 @@ Backward, per op:
     HiFi-GAN V1) -- the fallback SURVEY.md 8(b) sanctions.
 """
 
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import Optional, Tuple
 
 import os
@@ -329,8 +329,31 @@ class ConvFn(torch.autograd.Function):
         return gx, gw, gb, g_res1, g_res2, None, None, None
 
 
+# Many short sequences (the MPD's period columns: 96-352 sequences of 10-51 rows at C5): the conv
+# kernel tiles every sequence on its own -- a 16- to 256-row tile for 10-51 rows, each tile streaming
+# the whole (1024 x 1024 x 5) weight -- so these layers ran at 0.27 PF/s and below.  Laid end to end
+# with their zero padding between them they are ONE sequence that the kernel tiles densely; the
+# outputs that straddle two sequences are computed and dropped (their gradient is zero, so the
+# input and weight gradients over the joined sequence are the per-sequence ones).
+FLAT_T = int(os.environ.get("VO_FLAT_T", "64"))  # join sequences of up to this many output rows (0: off)
+
+
+def _conv_joined(x, w, b, spec, cdt, wkey):
+    N, T, C = x.shape
+    st = spec.stride
+    T_out = out_len(spec, T)
+    S_out = -(-(T + 2 * spec.pad) // st)     # output slots per sequence
+    S_in = st * S_out                         # input rows per sequence: its padding, then zeros
+    xj = F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
+    yj = ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey)  # slot u S_out + t <- rows u S_in + st t + k
+    return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
+
+
 def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None):
     """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged."""
+    if (FLAT_T > 0 and res1 is None and res2 is None and spec.groups == 1 and spec.dil == 1
+            and spec.transposed is None and x.dim() == 3 and x.shape[0] >= 8 and out_len(spec, x.shape[1]) <= FLAT_T):
+        return _conv_joined(x, w, b, spec, cdt, wkey)
     return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey)
 
 
