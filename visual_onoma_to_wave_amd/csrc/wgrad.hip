@@ -540,6 +540,7 @@ static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int d
   int kg = forced > 0 ? forced : (K + ntg - 1) / ntg;
   kg = std::max(1, std::min(kg, std::min(kgmax, K)));
   ntg = (K + kg - 1) / kg;
+  if (forced <= 0) kg = (K + ntg - 1) / ntg;  // balanced runs (K = 9 at 8 taps max: 5 + 4, not 8 + 1)
   pl->kg = kg;
   pl->ntg = ntg;
   const int64_t want = std::max<int64_t>(1, (512 + tiles * ntg - 1) / (tiles * ntg));
