@@ -323,6 +323,21 @@ int vo_pack_grouped_blocks(const float* src, int Co, int Ci, int K, int groups, 
  * the transpose / flip / pack chain of the HiFi-GAN discriminators' backward (C5). */
 int vo_pack_dgrad_phase(const float* w, int Co, int cig, int K, int groups, int S, int k_r, int J, int ci_out,
                         int co_in, int blocks_only, void* dst, int dst_dtype, void* stream);
+/* Many weight packs in one call (hifigan/gan_ops.prepack: the ~270 re-packs after each C5 optimizer
+ * step).  Job: for r < rows, j < width, t < T, with cbase(r) = (r / rpg) * cpg,
+ *   dst[(t * dst_rows + r) * ld + cbase(r) + j] =
+ *     GATHER swap 0: src[r][j][tap0 + tstep t]                    (vo_pack_weight CONV, grouped blocks)
+ *     GATHER swap 1: src[cbase(r) + j][r mod rpg][tap0 + tstep t] (DGRAD, vo_pack_dgrad_phase blocks)
+ *     CONVT:         src[j][r mod cig][r / cig + tap0 (1 - t)]    (vo_pack_weight CONVT, tap0 = s, K = 2s, T = 2)
+ * src (src_rows, cig, K) fp32 contiguous (CONVT: (Ci, Co = cig, K)); other dst entries untouched;
+ * a job's tap range (|tstep| (T - 1) + 1, CONVT: K) is at most 48. */
+enum vo_pack_job_mode { VO_PJ_GATHER = 0, VO_PJ_CONVT = 1 };
+typedef struct vo_pack_job {
+  const float* src;
+  void* dst;
+  int mode, swap, T, rows, width, dst_rows, ld, rpg, cpg, cig, K, tap0, tstep, src_rows;
+} VoPackJob;
+int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* stream);
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
 int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
 int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);

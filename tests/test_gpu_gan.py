@@ -297,6 +297,100 @@ def test_trainer_step_bf16():
     assert not torch.equal(before, g.conv_pre.weight_v.detach())
 
 
+def _pack_cases():
+    """(weight shape, ConvSpec as ConvFn sees it, input channels) of every conv the C5 step packs:
+    the generator's (B = 16 x 32 frames: conv_pre runs joined), the MPD's and the MSD's (16 x 8192)."""
+    from visual_onoma_to_wave_amd import hifigan
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
+                                                                 _conv_w)
+
+    def wshape(m):
+        return tuple(_conv_w(m, m.weight_v if hasattr(m, "weight_g") else m.weight_orig).shape)  # weight norm / spectral
+    cases = [(wshape(m), G.conv_spec(shape, sp, res), shape[-1])
+             for m, sp, shape, res in hifigan.Generator(hifigan.AttrDict(hifigan_h()))._train_plan(16, 32)]
+    for d in MultiPeriodDiscriminator().discriminators:
+        cases += [(wshape(m), G.conv_spec(shape, sp), shape[-1]) for m, sp, shape in d._layers(32, 8192)]
+    T = 8192
+    for i, d in enumerate(MultiScaleDiscriminator().discriminators):
+        T = T // 2 + 1 if i else T
+        cases += [(wshape(m), G.conv_spec(shape, sp), shape[-1]) for m, sp, shape in d._layers(32, T)]
+    return list(dict.fromkeys(cases))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pack_batch_matches_single_packs(dt):
+    """vo_pack_batch (gan_ops.prepack's one launch) == the per-layer packs each conv builds on first
+    use (vo_pack_weight CONV / DGRAD / CONVT, vo_pack_grouped, vo_pack_dgrad_phase), bit for bit,
+    for every HiFi-GAN layer's forward and input-gradient layouts, all in one call (> 32 jobs:
+    several launches), into zeroed buffers; then a second call with new weights into the same
+    buffers."""
+    from visual_onoma_to_wave_amd import ops
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    cases = _pack_cases()
+    assert len(cases) > 40
+    gen = torch.Generator().manual_seed(11)
+    work = []
+    for wshape, spec, ci_out in cases:
+        for tag, dshape, f in G._pack_plan(wshape, spec, dt, ci_out, True):
+            work.append((wshape, spec, tag, torch.zeros(dshape, dtype=dt, device="cuda"), f))
+    assert len(work) > 64
+    kinds = {t[2] for _, _, t, _, _ in work}
+    assert kinds == {"fwd", "dgrad_plain", "dgrad_convt", "dgrad"}, kinds
+
+    def ref(w, spec, tag):
+        if tag[2] == "fwd":
+            return G._pack(w, spec, dt)
+        if tag[2] == "dgrad_plain":
+            return ops.pack_dgrad_weight(w, dt)
+        if tag[2] == "dgrad_convt":
+            return ops.pack_conv_weight(w, dt)
+        r, ci_out, co_in = tag[3:]
+        k_r = (r + spec.pad) % spec.stride
+        J = len(range(k_r, spec.K, spec.stride))
+        return ops.pack_dgrad_phase(w, spec.groups, spec.stride, k_r, J, ci_out, co_in, dt)
+    for _ in range(2):
+        ws = {wshape: torch.randn(wshape, generator=gen).cuda() for wshape, _, _, _, _ in work}
+        ops.pack_batch([(ws[wshape], dst, f) for wshape, _, _, dst, f in work], dt)
+        for wshape, spec, tag, dst, _ in work:
+            assert torch.equal(dst, ref(ws[wshape], spec, tag)), (wshape, spec, tag)
+
+
+def test_trainer_prepack_no_first_use_packs():
+    """gan_ops.prepack: after the batched pre-pack no conv of a C5 step packs its own weights (every
+    tag the plan writes is the one the conv looks up: generator, both discriminators, D step and
+    G step, the joined-sequence convs of B = 8), and the trained parameters equal the
+    pack-on-first-use path's bit for bit (bf16)."""
+    from visual_onoma_to_wave_amd import hifigan
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    h = hifigan.AttrDict(hifigan_h())
+    mel = (torch.randn(8, 32, 80, generator=torch.Generator().manual_seed(7)) - 4).cuda()
+    y = torch.tanh(torch.randn(8, 8192, generator=torch.Generator().manual_seed(8)) * 0.3).cuda()
+    finals, builds = [], []
+    try:
+        for pre in (True, False):
+            G.PREPACK = pre
+            G.reset_pack_cache()
+            torch.manual_seed(1234)
+            g = _gen("cuda")
+            tr = hifigan.HifiGanTrainer(g, h).set_compute_dtype(torch.bfloat16)
+            tr.step(mel, y)
+            n0 = G.STATS["pack_builds"]
+            losses = tr.step(mel, y)
+            torch.cuda.synchronize()
+            builds.append(G.STATS["pack_builds"] - n0)
+            finals.append(({k: float(v) for k, v in losses.items()},
+                           torch.cat([p.detach().flatten().cpu() for p in g.parameters()]),
+                           torch.cat([p.detach().flatten().cpu() for p in tr.mpd.parameters()]),
+                           torch.cat([p.detach().flatten().cpu() for p in tr.msd.parameters()])))
+    finally:
+        G.PREPACK = True
+        G.reset_pack_cache()
+    assert builds[0] == 0 and builds[1] > 200, builds
+    (l1, g1, p1, s1), (l0, g0, p0, s0) = finals
+    assert l1 == l0 and torch.equal(g1, g0) and torch.equal(p1, p0) and torch.equal(s1, s0)
+
+
 def test_trainer_graphed_matches_eager():
     """HIP-graph replays of the training step (HifiGanTrainer.step_graphed, back to back, no host
     wait; the warm-up steps before the capture are undone) against the same number of eager steps

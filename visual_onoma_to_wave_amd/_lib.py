@@ -45,6 +45,13 @@ class Conv1dDesc(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):
+    """VoPackJob (include/vonoma.h, vo_pack_batch)."""
+    _fields_ = [("src", c_void_p), ("dst", c_void_p)] + [
+        (f, c_int) for f in ("mode", "swap", "T", "rows", "width", "dst_rows", "ld", "rpg", "cpg", "cig", "K", "tap0",
+                             "tstep", "src_rows")]
+
+
 class HeadDesc(ctypes.Structure):
     _fields_ = [
         ("kind", c_int),
@@ -136,6 +143,7 @@ _SIGNATURES = {
     "vo_avgpool_wav_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "vo_pack_dgrad_phase": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_void_p, c_int, c_void_p]),
+    "vo_pack_batch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_weight_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),

@@ -81,6 +81,102 @@ __global__ void __launch_bounds__(256) pack_dgrad_phase_kernel(const float* __re
   }
 }
 
+// Every pack above (and vocoder_glue's plain / input-gradient / ConvTranspose1d packs) as one job of
+// a batch: the C5 step re-packs ~270 weights after each optimizer step, 146 + 125 launches of 4-27 us
+// (2.6 ms per step) that move ~0.7 GB in all.  A job writes, for rows r < rows and columns
+// c = cbase(r) + j (j < width, cbase(r) = (r / rpg) * cpg: the diagonal block of a grouped layout),
+// dst[(t * dst_rows + r) * ld + c] for t < T, from src (src_rows, cig, K) fp32:
+//   GATHER, swap 0 (forward packs):        src[r][j][tap0 + tstep t]
+//   GATHER, swap 1 (input-gradient packs): src[cbase(r) + j][r mod rpg][tap0 + tstep t]
+//   CONVT (ConvTranspose1d (Ci, Co = cig, 2s), tap0 = s): src[j][r mod cig][r / cig + s (1 - t)]
+// Entries a job does not name are left as they are (persistent buffers zeroed once).
+// Each (r, j) reads a run of taps that is contiguous in src; a wave takes 64 such runs (64
+// consecutive j of one row, or for narrow rows several whole rows), stages them in its own LDS
+// region with coalesced loads (swap 0: the 64 runs are one contiguous block), and then writes tap
+// after tap, each a contiguous stretch of dst per row.  (One thread per (r, 4 columns) looping over
+// the taps with direct loads ran latency-bound: C5 +0.8 ms against the per-layer kernels.)
+constexpr int PJ_MAX = 32;
+constexpr int PJ_KMAX = 48;  // tap range staged per run
+struct PackBatchArgs {
+  VoPackJob j[PJ_MAX];
+  int blk0[PJ_MAX + 1];  // first workgroup of each job; blk0[n] = grid size
+  int n;
+  int kp;                // LDS floats per staged run (max over the launch's jobs; dynamic LDS)
+};
+
+__host__ __device__ inline int pj_wpow(int width) {  // lanes per row: the power of two >= width, <= 64
+  int w = 1;
+  while (w < width && w < 64) w <<= 1;
+  return w;
+}
+
+template <typename TD>
+__global__ void __launch_bounds__(256) pack_batch_kernel(PackBatchArgs a) {
+  extern __shared__ float lds[];  // 4 waves x (64 runs x a.kp floats), then 4 x 64 run offsets
+  const int b = blockIdx.x;
+  int li = 0;
+  while (li + 1 < a.n && a.blk0[li + 1] <= b) ++li;  // uniform per workgroup
+  // the job by value: its fields are read from the kernel arguments once (through a reference
+  // the compiler re-read them around every load: a scalar-memory round trip per element)
+  const VoPackJob J = a.j[li];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wpow = pj_wpow(J.width), rpw = 64 / wpow;  // rows per wave (narrow rows)
+  const int jchunks = (J.width + 63) / 64;              // 64-column chunks per row (wide rows)
+  const int unit = (b - a.blk0[li]) * 4 + wv;
+  const int r0 = (unit / jchunks) * rpw, j0 = (unit % jchunks) * 64;
+  // staged tap range [k0, k0 + L)
+  int k0, L;
+  if (J.mode == VO_PJ_CONVT) {
+    k0 = 0; L = J.K;
+  } else {
+    const int last = J.tap0 + J.tstep * (J.T - 1);
+    k0 = min(J.tap0, last); L = abs(last - J.tap0) + 1;
+  }
+  const int Kp = L | 1;  // odd LDS row stride: the per-tap reads below hit 64 distinct banks
+  float* my = lds + wv * 64 * a.kp;
+  int* tab = reinterpret_cast<int*>(lds + 4 * 64 * a.kp) + wv * 64;
+  // this lane's run: (r, j) and the source offset of its tap k0 (-1: no such run)
+  const int r = r0 + lane / wpow, j = j0 + lane % wpow;
+  int base = -1;
+  if (r < J.rows && j < J.width) {
+    if (J.mode == VO_PJ_CONVT) base = (j * J.cig + r % J.cig) * J.K + k0;
+    else if (J.swap) base = (((r / J.rpg) * J.cpg + j) * J.cig + r % J.rpg) * J.K + k0;
+    else base = (r * J.cig + j) * J.K + k0;
+  }
+  tab[lane] = base;
+  __syncthreads();
+  // stage the 64 runs: element e = q L + k of the wave's block, 64 consecutive e per load
+  // (swap 0 and wide rows: one contiguous stretch of src)
+  constexpr int NL = 16;  // loads in flight per lane
+  const int n = 64 * L, dq = 64 / L, dk = 64 - dq * L;
+  int q = lane / L, k = lane - q * L;
+  for (int e0 = 0; e0 < n; e0 += NL * 64) {
+    float v[NL];
+    int at[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const bool in = e0 + u * 64 + lane < n;
+      const int o = in ? tab[q] : -1;
+      v[u] = o >= 0 ? J.src[o + k] : 0.f;
+      at[u] = in ? q * Kp + k : -1;
+      q += dq;
+      k += dk;
+      if (k >= L) { k -= L; ++q; }
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u)
+      if (at[u] >= 0) my[at[u]] = v[u];
+  }
+  __syncthreads();
+  if (base < 0) return;
+  TD* dst = reinterpret_cast<TD*>(J.dst) + (int64_t)r * J.ld + (r / J.rpg) * J.cpg + j;
+  const int64_t plane = (int64_t)J.dst_rows * J.ld;
+  const float* row = my + lane * Kp;
+  const int tb = J.mode == VO_PJ_CONVT ? r / J.cig + J.tap0 : J.tap0 - k0;
+  const int ts = J.mode == VO_PJ_CONVT ? -J.tap0 : J.tstep;
+  for (int t = 0; t < J.T; ++t) dst[plane * t] = from_f32<TD>(row[tb + ts * t]);
+}
+
 // wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
 // reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
 template <typename TD>
@@ -408,6 +504,68 @@ extern "C" int vo_pack_dgrad_phase(const float* w, int Co, int cig, int K, int g
   }
 #undef VO_PDP
   VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* stream) {
+  VO_CHECK_ARG(n >= 0 && (n == 0 || jobs), "pack_batch: null job table");
+  VO_CHECK_ARG(dst_dtype == VO_BF16 || dst_dtype == VO_F32, "pack_batch: dst dtype %d", dst_dtype);
+  for (int i = 0; i < n; ++i) {
+    const VoPackJob& J = jobs[i];
+    VO_CHECK_ARG(J.src && J.dst, "pack_batch: job %d: null pointer", i);
+    VO_CHECK_ARG(J.mode == VO_PJ_GATHER || J.mode == VO_PJ_CONVT, "pack_batch: job %d: mode %d", i, J.mode);
+    VO_CHECK_ARG(J.T >= 1 && J.rows >= 1 && J.width >= 1 && J.rpg >= 1 && J.cpg >= 0 && J.cig >= 1 && J.K >= 1 &&
+                     J.src_rows >= 1 && J.dst_rows >= J.rows,
+                 "pack_batch: job %d: bad sizes", i);
+    VO_CHECK_ARG(J.mode == VO_PJ_CONVT ? J.K <= PJ_KMAX : std::abs(J.tstep) * (J.T - 1) + 1 <= PJ_KMAX,
+                 "pack_batch: job %d: tap range over %d", i, PJ_KMAX);
+    VO_CHECK_ARG((int64_t)((J.rows - 1) / J.rpg) * J.cpg + J.width <= J.ld, "pack_batch: job %d: row exceeds ld", i);
+    VO_CHECK_ARG((int64_t)J.src_rows * J.cig * J.K < (1LL << 31) && (int64_t)J.rows * J.width < (1LL << 30),
+                 "pack_batch: job %d too large", i);
+    if (J.mode == VO_PJ_CONVT) {
+      VO_CHECK_ARG(J.T == 2 && J.K == 2 * J.tap0 && J.rows == J.tap0 * J.cig && J.width <= J.src_rows,
+                   "pack_batch: job %d: ConvTranspose1d job needs T = 2, K = 2 s, rows = s Co", i);
+    } else {
+      const int last = J.tap0 + J.tstep * (J.T - 1);
+      VO_CHECK_ARG(J.tap0 >= 0 && J.tap0 < J.K && last >= 0 && last < J.K, "pack_batch: job %d: taps outside [0, K)",
+                   i);
+      if (J.swap)
+        VO_CHECK_ARG(J.rpg <= J.cig && ((J.rows - 1) / J.rpg) * J.cpg + J.width <= J.src_rows,
+                     "pack_batch: job %d: source row / channel out of range", i);
+      else
+        VO_CHECK_ARG(J.rows <= J.src_rows && J.width <= J.cig, "pack_batch: job %d: source row / channel out of range",
+                     i);
+    }
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += PJ_MAX) {
+    PackBatchArgs a;
+    a.n = std::min(PJ_MAX, n - i0);
+    int64_t blocks = 0;
+    a.kp = 1;
+    for (int i = 0; i < a.n; ++i) {
+      a.j[i] = jobs[i0 + i];
+      a.blk0[i] = (int)blocks;
+      const VoPackJob& J = a.j[i];
+      const int rpw = 64 / pj_wpow(J.width);
+      const int64_t units = (int64_t)((J.rows + rpw - 1) / rpw) * ((J.width + 63) / 64);  // one wave each
+      blocks += (units + 3) / 4;
+      const int L = J.mode == VO_PJ_CONVT ? J.K : std::abs(J.tstep) * (J.T - 1) + 1;
+      a.kp = std::max(a.kp, L | 1);
+    }
+    VO_CHECK_ARG(blocks < (1LL << 31), "pack_batch: grid too large");
+    const size_t lds = (size_t)4 * 64 * (a.kp + 1) * sizeof(float);
+    a.blk0[a.n] = (int)blocks;
+    if (dst_dtype == VO_BF16)
+      hipLaunchKernelGGL(pack_batch_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+    else
+      hipLaunchKernelGGL(pack_batch_kernel<float>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      vo_set_error("pack_batch: launch failed: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+  }
+  return VO_OK;
 }
 
 extern "C" int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream) {

@@ -63,19 +63,35 @@ def _weight(m):
     runs each discriminator twice: real half without graph, generated half)."""
     wkey = G.weight_key(m)
     p = m.weight_v if hasattr(m, "weight_v") else m.weight
-    if wkey is None or (torch.is_grad_enabled() and p.requires_grad):
+    if G.volatile(wkey) or (torch.is_grad_enabled() and p.requires_grad):
         return effective_weight(m)
     return G._cached(wkey, "w_eff", lambda: effective_weight(m).detach())
 
 
-def _batched_weights(root):
-    """Effective weights of every weight-normed conv under ``root`` in one batched call while the
-    discriminator is being trained (autograd records and its parameters require grad); {} otherwise
-    (the frozen G-step path keeps the per-module cache of ``_weight``)."""
+def _conv_w(m, w):
+    return w[..., 0] if w.dim() == 4 else w  # Conv2d (k, 1) weights as Conv1d
+
+
+def _prepare(root, layers, dgrad_first):
+    """Effective weights ``W`` of every weight-normed conv under ``root`` -- one batched launch,
+    differentiable while the discriminator trains (autograd records and its parameters require
+    grad), else cached at the parameters' versions (the frozen G step runs D twice) -- and every
+    packed weight the convs in ``layers`` (per discriminator: [(module, spec, input shape)] in
+    forward order) will look up, written by one ``gan_ops.prepack`` launch (input-gradient layouts
+    for all but each discriminator's first conv, and for those too with ``dgrad_first``)."""
     mods = [m for m in root.modules() if hasattr(m, "weight_g")]
-    if not (torch.is_grad_enabled() and any(m.weight_v.requires_grad for m in mods)):
-        return {}
-    return G.weight_norm_all(mods)
+    if not mods:
+        W = {}
+    elif torch.is_grad_enabled() and any(m.weight_v.requires_grad for m in mods):
+        W = G.weight_norm_all(mods)
+    else:
+        key = (root,) + tuple(v for m in mods for v in (m.weight_v._version, m.weight_g._version))
+        W = G._cached(key, "W_frozen", lambda: dict(zip(mods, ops.weight_norm(
+            [m.weight_v.detach() for m in mods], [m.weight_g.detach() for m in mods]))))
+    cdt = root.compute_dtype
+    G.prepack([(G.weight_key(m), _conv_w(m, W[m]), sp, shape, dgrad_first or i > 0)
+               for d in layers for i, (m, sp, shape) in enumerate(d) if m in W], cdt)
+    return W
 
 
 def _w(m, W):
@@ -116,22 +132,30 @@ class DiscriminatorP(_DiscBase):
         specs.append(G.ConvSpec(K=k, pad=2, post="lrelu", post_slope=LRELU_SLOPE))
         return specs, G.ConvSpec(K=3, pad=1, co_pad=4)
 
+    def _layers(self, B, T):
+        """[(module, spec, input shape (N, T, C))] of ``forward``'s convs for a (B, T) wav batch."""
+        N, H, C = B * self.period, -(-T // self.period), 8
+        specs, post = self._specs()
+        out = []
+        for m, sp in zip(list(self.convs) + [self.conv_post], specs + [post]):
+            out.append((m, sp, (N, H, C)))
+            H, C = G.out_len(sp, H), m.out_channels
+        return out
+
     def forward(self, wav, W=None):
         """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)]).  ``W``: effective
-        weights batched by the caller (``_batched_weights``)."""
+        weights batched (and the convs' weights packed) by the caller (``_prepare``)."""
         cdt, adt = self.compute_dtype, self._act_dtype()
+        layers = self._layers(*wav.shape)
         if W is None:
-            W = _batched_weights(self)
+            W = _prepare(self, [layers], wav.requires_grad)
         x = G.PeriodFoldFn.apply(wav, self.period, adt)
-        specs, post = self._specs()
         fmap = []
-        for m, sp in zip(self.convs, specs):
+        for m, sp, _ in layers:
             x = G.conv(x, _w(m, W)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
-        m = self.conv_post
-        y = G.conv(x, _w(m, W)[..., 0], m.bias, post, cdt, wkey=G.weight_key(m))
-        score = y[..., 0].contiguous()
-        fmap.append(score)
+        score = x[..., 0].contiguous()
+        fmap[-1] = score
         return score, fmap
 
 
@@ -140,12 +164,17 @@ class MultiPeriodDiscriminator(_DiscBase):
         super().__init__()
         self.discriminators = nn.ModuleList(DiscriminatorP(p) for p in periods)
 
+    def prepare(self, wav, dgrad_first=None):
+        """``_prepare`` over every period's convs for a (B, T) wav batch -> W."""
+        layers = [d._layers(*wav.shape) for d in self.discriminators]
+        return _prepare(self, layers, wav.requires_grad if dgrad_first is None else dgrad_first)
+
     def forward(self, y, y_hat):
         """Reference call convention: (y_d_rs, y_d_gs, fmap_rs, fmap_gs).  y and y_hat run as one
         batch (one launch per layer for both)."""
         B = y.shape[0]
         both = torch.cat([y, y_hat], 0)
-        W = _batched_weights(self)
+        W = self.prepare(both)
         rs, gs, frs, fgs = [], [], [], []
         for d in self.discriminators:
             p = d.period
@@ -169,22 +198,30 @@ class DiscriminatorS(_DiscBase):
             self.convs = nn.ModuleList(norm_f(Conv1d(ci, co, k, s, groups=g, padding=p)) for ci, co, k, s, g, p in cfg)
             self.conv_post = norm_f(Conv1d(1024, 1, 3, 1, padding=1))
 
-    def forward(self, wav, W=None):
-        """wav (B, T) fp32 -> (score (B, T'), fmaps [(B, T_l, C_l)])."""
-        cdt, adt = self.compute_dtype, self._act_dtype()
-        if W is None:
-            W = _batched_weights(self)
-        x = G.WavCl8Fn.apply(wav, adt)
-        fmap = []
+    def _layers(self, B, T):
+        """[(module, spec, input shape (N, T, C))] of ``forward``'s convs for a (B, T) wav batch."""
+        out, C = [], 8
         for m, (ci, co, k, s, g, p) in zip(self.convs, self.cfg):
             sp = G.ConvSpec(K=k, pad=p, stride=s, groups=g, post="lrelu", post_slope=LRELU_SLOPE,
                             ci_pad=8 if ci == 1 else None)
+            out.append((m, sp, (B, T, C)))
+            T, C = G.out_len(sp, T), co
+        out.append((self.conv_post, G.ConvSpec(K=3, pad=1, co_pad=4), (B, T, C)))
+        return out
+
+    def forward(self, wav, W=None):
+        """wav (B, T) fp32 -> (score (B, T'), fmaps [(B, T_l, C_l)])."""
+        cdt, adt = self.compute_dtype, self._act_dtype()
+        layers = self._layers(*wav.shape)
+        if W is None:
+            W = _prepare(self, [layers], wav.requires_grad)
+        x = G.WavCl8Fn.apply(wav, adt)
+        fmap = []
+        for m, sp, _ in layers:
             x = G.conv(x, _w(m, W), m.bias, sp, cdt, wkey=G.weight_key(m))
             fmap.append(x)
-        m = self.conv_post
-        y = G.conv(x, _w(m, W), m.bias, G.ConvSpec(K=3, pad=1, co_pad=4), cdt, wkey=G.weight_key(m))
-        score = y[..., 0].contiguous()
-        fmap.append(score)
+        score = x[..., 0].contiguous()
+        fmap[-1] = score
         return score, fmap
 
 
@@ -194,10 +231,20 @@ class MultiScaleDiscriminator(_DiscBase):
         self.discriminators = nn.ModuleList(
             [DiscriminatorS(use_spectral_norm=True), DiscriminatorS(), DiscriminatorS()])
 
+    def prepare(self, wav, dgrad_first=None):
+        """``_prepare`` over the three scales' convs for a (B, T) wav batch -> W."""
+        B, T = wav.shape
+        layers = []
+        for i, d in enumerate(self.discriminators):
+            if i:
+                T = T // 2 + 1  # AvgPool1d(4, 2, padding 2)
+            layers.append(d._layers(B, T))
+        return _prepare(self, layers, wav.requires_grad if dgrad_first is None else dgrad_first)
+
     def forward(self, y, y_hat):
         B = y.shape[0]
         x = torch.cat([y, y_hat], 0)
-        W = _batched_weights(self)
+        W = self.prepare(x)
         rs, gs, frs, fgs = [], [], [], []
         for i, d in enumerate(self.discriminators):
             if i != 0:

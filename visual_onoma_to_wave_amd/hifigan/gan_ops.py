@@ -125,25 +125,41 @@ def _slot_fn(wkey, tag):
     return get
 
 
+# Version of a spectral-normed conv's weight, which moves with each training-mode power iteration:
+# never equal to a cached one, so every use re-packs -- into the module's persistent slots (the
+# grouped layouts' diagonal blocks only), not a dense buffer per call.
+VOLATILE = object()
+
+
 def weight_key(m):
     """Cache key of a conv module's effective weight: the module and its parameters' version
-    counters (bumped by every optimizer step / load_state_dict).  None (no caching) for
-    spectral-normed convs, whose weight moves with each training-mode power iteration."""
+    counters (bumped by every optimizer step / load_state_dict); ``(m, VOLATILE)`` (re-packed on
+    every use) for spectral-normed convs."""
     if hasattr(m, "weight_g"):
         return (m, m.weight_v._version, m.weight_g._version)
     if hasattr(m, "weight_orig"):
-        return None
+        return (m, VOLATILE)
     return (m, m.weight._version)
 
 
+def volatile(wkey):
+    return wkey is None or wkey[1] is VOLATILE
+
+
+# pack_builds: packs built on first use at a new parameter version (tests: zero after prepack)
+STATS = {"pack_builds": 0}
+
+
 def _cached(wkey, tag, build):
-    if wkey is None:
+    if volatile(wkey):
         return build()
     per = (_CAPTURE_PACKS if torch.cuda.is_current_stream_capturing() else _PACKS).setdefault(wkey[0], {})
     hit = per.get(tag)
     if hit is not None and hit[0] == wkey[1:]:
         return hit[1]
     val = build()
+    if isinstance(tag, tuple):
+        STATS["pack_builds"] += 1
     per[tag] = (wkey[1:], val)
     return val
 
@@ -271,7 +287,7 @@ class ConvFn(torch.autograd.Function):
         elif need_x and spec.transposed is not None:
             s, p = spec.transposed
             # ConvTranspose1d(Ci -> Co, k, s, p) adjoint = Conv1d(Co -> Ci, W as (Ci, Co, k), stride s, pad p)
-            wc = ops.pack_conv_weight(w, cdt)
+            wc = _cached(ctx.wkey, (spec, cdt, "dgrad_convt"), lambda: ops.pack_conv_weight(w, cdt))
             ga = ops.conv1d(gz.to(cdt), wc, None, Co=w.shape[0], K=spec.K, pad=p, stride=s, T_out=x.shape[1],
                             out_dtype=x.dtype, compute_dtype=cdt)
             need_x = False
@@ -349,12 +365,103 @@ def _conv_joined(x, w, b, spec, cdt, wkey):
     return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
 
 
+def _joined(shape, spec, has_res=False):
+    """Whether ``conv`` runs an input of this (N, T, C) shape as one joined sequence."""
+    return (FLAT_T > 0 and not has_res and spec.groups == 1 and spec.dil == 1 and spec.transposed is None
+            and len(shape) == 3 and shape[0] >= 8 and out_len(spec, shape[1]) <= FLAT_T)
+
+
 def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None):
     """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged."""
-    if (FLAT_T > 0 and res1 is None and res2 is None and spec.groups == 1 and spec.dil == 1
-            and spec.transposed is None and x.dim() == 3 and x.shape[0] >= 8 and out_len(spec, x.shape[1]) <= FLAT_T):
+    if _joined(x.shape, spec, res1 is not None or res2 is not None):
         return _conv_joined(x, w, b, spec, cdt, wkey)
     return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey)
+
+
+def conv_spec(shape, spec, has_res=False):
+    """The spec ``conv`` hands to ConvFn for an input of this shape (joined sequences run unpadded)."""
+    return replace(spec, pad=0) if _joined(shape, spec, has_res) else spec
+
+
+# ----------------------------------------------------------------------------- batched packing
+# After every optimizer step each conv's packed weights (forward, and the input-gradient layouts
+# its backward uses) are stale: ~270 pack launches of 4-27 us per C5 step when each conv packs on
+# first use.  ``prepack`` writes all of a model's packs in one vo_pack_batch launch right after its
+# batched weight normalisation and records them under the same cache tags and persistent slots
+# that _conv_fwd / ConvFn.backward / _dgrad look up, so those find them (a conv whose tag the plan
+# missed still packs itself: the plan changes speed, never results).
+
+def _pack_plan(w_shape, spec, cdt, ci_out, dgrad):
+    """[(tag, dst shape, vo_pack_batch job fields)] of the packs one conv's forward (and with
+    ``dgrad``, its backward's input gradient) looks up -- the tags and layouts of _conv_fwd /
+    ConvFn.backward / _dgrad.  ``spec`` as ConvFn sees it (``conv_spec``), ci_out = its input's
+    channel count."""
+    G, CT = ops.PJ_GATHER, ops.PJ_CONVT
+
+    def job(mode, swap, T, rows, width, dst_rows, ld, rpg, cpg, cig, K, tap0, tstep, src_rows):
+        return dict(mode=mode, swap=swap, T=T, rows=rows, width=width, dst_rows=dst_rows, ld=ld, rpg=rpg, cpg=cpg,
+                    cig=cig, K=K, tap0=tap0, tstep=tstep, src_rows=src_rows)
+    out = []
+    if spec.transposed is not None:
+        Ci, Co, K = w_shape  # ConvTranspose1d (Ci, Co, 2s)
+        s = spec.transposed[0]
+        out.append(((spec, cdt, "fwd"), (2, s * Co, Ci), job(CT, 0, 2, s * Co, Ci, s * Co, Ci, s * Co, 0, Co, K, s, 0, Ci)))
+        if dgrad:  # the adjoint conv's weight: w read as a (Ci, Co, K) Conv1d weight
+            out.append(((spec, cdt, "dgrad_convt"), (K, Ci, Co), job(G, 0, K, Ci, Co, Ci, Co, Ci, 0, Co, K, 0, 1, Ci)))
+        return out
+    Co, cig, K = w_shape
+    g = spec.groups
+    Ci, cog = cig * g, Co // g
+    if spec.plain():
+        out.append(((spec, cdt, "fwd"), (K, Co, Ci), job(G, 0, K, Co, Ci, Co, Ci, Co, 0, Ci, K, 0, 1, Co)))
+        if dgrad:
+            out.append(((spec, cdt, "dgrad_plain"), (K, Ci, Co), job(G, 1, K, Ci, Co, Ci, Co, Ci, 0, Ci, K, K - 1, -1, Co)))
+        return out
+    co_rows = spec.co_pad if spec.co_pad is not None and spec.co_pad > Co else Co
+    ld = Ci if spec.ci_pad is None else spec.ci_pad
+    out.append(((spec, cdt, "fwd"), (K, co_rows, ld), job(G, 0, K, Co, cig, co_rows, ld, cog, cig, cig, K, 0, 1, Co)))
+    if dgrad and spec.dil == 1 and not (ci_out > Ci and g != 1):
+        S, co_in = spec.stride, -(-Co // 8) * 8
+        for r in range(S):
+            k_r = (r + spec.pad) % S
+            J = len(range(k_r, K, S))
+            if J == 0:
+                continue
+            out.append(((spec, cdt, "dgrad", r, ci_out, co_in), (J, ci_out, co_in),
+                        job(G, 1, J, Ci, cog, ci_out, co_in, cig, cog, cig, K, k_r + S * (J - 1), -S, Co)))
+    return out
+
+
+PREPACK = os.environ.get("VO_PREPACK", "1") != "0"  # 0: every conv packs on first use (A/B)
+
+
+def prepack(entries, cdt):
+    """entries: [(wkey, w, spec, input shape (N, T, C), dgrad[, has residual inputs])] -- ``spec`` /
+    shape as passed to ``conv`` -> every pack those convs will look up that is not cached at these
+    parameter versions, in one vo_pack_batch launch (entries with a volatile key pack on use)."""
+    if not PREPACK:
+        return 0
+    store = _CAPTURE_PACKS if torch.cuda.is_current_stream_capturing() else _PACKS
+    jobs, done = [], []
+    for wkey, w, spec, shape, dgrad, *res in entries:
+        if volatile(wkey):
+            continue
+        per = store.setdefault(wkey[0], {})
+        src = None
+        for tag, dshape, f in _pack_plan(tuple(w.shape), conv_spec(shape, spec, bool(res and res[0])), cdt, shape[-1],
+                                         dgrad):
+            hit = per.get(tag)
+            if hit is not None and hit[0] == wkey[1:]:
+                continue
+            if src is None:
+                src = w.detach().float().contiguous()
+            dst = _slot_fn(wkey, tag)(dshape, cdt, w.device)
+            jobs.append((src, dst, f))
+            done.append((per, tag, wkey[1:], dst))
+    ops.pack_batch(jobs, cdt)
+    for per, tag, ver, dst in done:
+        per[tag] = (ver, dst)
+    return len(jobs)
 
 
 class WeightNormFn(torch.autograd.Function):

@@ -251,38 +251,58 @@ class Generator(HipModule):
         dt = self.compute_dtype
         adt = torch.float32 if dt == torch.float32 else torch.bfloat16
 
-        # every weight-normed conv's w = g v / ||v|| in one batched launch (and one in the backward)
+        # every weight-normed conv's w = g v / ||v|| in one batched launch (and one in the backward),
+        # then every packed weight the convs below look up in one more (gan_ops.prepack)
         W = G.weight_norm_all(list(self.modules()))
 
         def wgt(m):
             return W[m] if m in W else m.weight
+        plan = self._train_plan(mel_cl.shape[0], mel_cl.shape[1])
+        G.prepack([(G.weight_key(m), wgt(m), sp, shape, m is not self.conv_pre, res) for m, sp, shape, res in plan], dt)
+        spec = {m: sp for m, sp, _, _ in plan}
 
-        x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, G.ConvSpec(K=7, pad=3), dt,
+        x = G.conv(mel_cl.to(adt).contiguous(), wgt(self.conv_pre), self.conv_pre.bias, spec[self.conv_pre], dt,
                    wkey=G.weight_key(self.conv_pre))
-        for i, (u, k) in enumerate(zip(self.h.upsample_rates, self.h.upsample_kernel_sizes)):
+        for i in range(self.num_upsamples):
             m = self.ups[i]
-            x = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=k, pad=(k - u) // 2, pre_slope=LRELU_SLOPE,
-                                                     transposed=(u, (k - u) // 2)), dt, wkey=G.weight_key(m))
+            x = G.conv(x, wgt(m), m.bias, spec[m], dt, wkey=G.weight_key(m))
             xs = None
             for j in range(self.num_kernels):
                 rb = self.resblocks[i * self.num_kernels + j]
-                kk = rb.kernel_size
                 cur = x
-                for n, (d, c1, c2) in enumerate(zip(rb.dilation, rb.convs1, rb.convs2)):
-                    t = G.conv(cur, wgt(c1), c1.bias, G.ConvSpec(K=kk, pad=get_padding(kk, d), dil=d,
-                                                                 pre_slope=LRELU_SLOPE, post="lrelu",
-                                                                 post_slope=LRELU_SLOPE), dt,
-                               wkey=G.weight_key(c1))
+                for n, (c1, c2) in enumerate(zip(rb.convs1, rb.convs2)):
+                    t = G.conv(cur, wgt(c1), c1.bias, spec[c1], dt, wkey=G.weight_key(c1))
                     last = n == len(rb.dilation) - 1
-                    sp = G.ConvSpec(K=kk, pad=get_padding(kk, 1), out_scale=1.0 / self.num_kernels if last else 1.0)
-                    cur = G.conv(t, wgt(c2), c2.bias, sp, dt, res1=cur, res2=xs if last else None,
+                    cur = G.conv(t, wgt(c2), c2.bias, spec[c2], dt, res1=cur, res2=xs if last else None,
                                  wkey=G.weight_key(c2))
                 xs = cur
             x = xs
         m = self.conv_post
-        y = G.conv(x, wgt(m), m.bias, G.ConvSpec(K=7, pad=3, pre_slope=0.01, post="tanh", co_pad=4), dt,
-                   wkey=G.weight_key(m))
+        y = G.conv(x, wgt(m), m.bias, spec[m], dt, wkey=G.weight_key(m))
         return y[..., 0].float()
+
+    def _train_plan(self, B, T):
+        """[(module, ConvSpec, input shape (N, T, C), has residual inputs)] of ``train_forward``'s
+        convs for a (B, T, 80) mel batch, in launch order."""
+        from . import gan_ops as G
+        plan = [(self.conv_pre, G.ConvSpec(K=7, pad=3), (B, T, self.conv_pre.in_channels), False)]
+        C = self.conv_pre.out_channels
+        for i, (u, k) in enumerate(zip(self.h.upsample_rates, self.h.upsample_kernel_sizes)):
+            m = self.ups[i]
+            sp = G.ConvSpec(K=k, pad=(k - u) // 2, pre_slope=LRELU_SLOPE, transposed=(u, (k - u) // 2))
+            plan.append((m, sp, (B, T, C), False))
+            T, C = G.out_len(sp, T), m.out_channels
+            for j in range(self.num_kernels):
+                rb = self.resblocks[i * self.num_kernels + j]
+                kk = rb.kernel_size
+                for n, (d, c1, c2) in enumerate(zip(rb.dilation, rb.convs1, rb.convs2)):
+                    plan.append((c1, G.ConvSpec(K=kk, pad=get_padding(kk, d), dil=d, pre_slope=LRELU_SLOPE,
+                                                post="lrelu", post_slope=LRELU_SLOPE), (B, T, C), False))
+                    last = n == len(rb.dilation) - 1
+                    plan.append((c2, G.ConvSpec(K=kk, pad=get_padding(kk, 1),
+                                                out_scale=1.0 / self.num_kernels if last else 1.0), (B, T, C), True))
+        plan.append((self.conv_post, G.ConvSpec(K=7, pad=3, pre_slope=0.01, post="tanh", co_pad=4), (B, T, C), False))
+        return plan
 
     def forward(self, x):
         """x (B, 80, T) mel -> (B, 1, 256 * T) waveform (reference: models.py:149-165)."""

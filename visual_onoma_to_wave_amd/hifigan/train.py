@@ -31,12 +31,16 @@ def _single(disc, wav, grad):
     scores, fmaps = [], []
     ctx = torch.enable_grad() if grad else torch.no_grad()
     with ctx:
+        # frozen D: one weight-norm and one packing launch for the real and the generated pass
+        # together (both at these parameter versions; the generated pass's backward needs the
+        # input-gradient layouts of every conv)
+        W = disc.prepare(wav, dgrad_first=True)
         x = wav
         for i, d in enumerate(disc.discriminators):
             if isinstance(disc, MultiScaleDiscriminator) and i:
                 from . import gan_ops
                 x = gan_ops.AvgPoolFn.apply(x)
-            s, f = d(x)
+            s, f = d(x, W)
             scores.append(s)
             fmaps.append(f)
     return scores, fmaps

@@ -667,6 +667,33 @@ def pack_grouped_weight(w, dtype, groups=1, ci_pad=None, out=None):
     return out
 
 
+PJ_GATHER, PJ_CONVT = 0, 1
+_PJ_FIELDS = ("mode", "swap", "T", "rows", "width", "dst_rows", "ld", "rpg", "cpg", "cig", "K", "tap0", "tstep",
+              "src_rows")
+
+
+def pack_batch(jobs, dtype):
+    """Many weight packs in one launch (vo_pack_batch; layouts in include/vonoma.h): jobs is a list of
+    (src fp32 contiguous, dst contiguous tensor of ``dtype``, {field: int}).  Entries of dst a job
+    does not name are left as they are."""
+    if not jobs:
+        return
+    arr = (_lib.PackJob * len(jobs))()
+    for e, (src, dst, f) in zip(arr, jobs):
+        _contig(src, "src")
+        _contig(dst, "dst")
+        if src.dtype != torch.float32 or dst.dtype != dtype:
+            raise ValueError("pack_batch: src must be fp32 and dst the batch dtype")
+        rows_total = f["T"] * f["dst_rows"] * f["ld"]
+        if dst.numel() != rows_total:
+            raise ValueError(f"pack_batch: dst has {dst.numel()} elements, the job's layout {rows_total}")
+        e.src, e.dst = src.data_ptr(), dst.data_ptr()
+        for k in _PJ_FIELDS:
+            setattr(e, k, int(f[k]))
+    _lib.check(_lib.lib().vo_pack_batch(len(jobs), ctypes.cast(arr, ctypes.c_void_p), vo_dtype(dtype),
+                                        _stream(jobs[0][1])), "vo_pack_batch")
+
+
 def pack_dgrad_phase(w, groups, S, k_r, J, ci_out, co_in, dtype, out=None):
     """Stride phase k_r of a strided / grouped conv's input gradient: w (Co, Ci/groups, K) -> packed
     [J][ci_out][co_in] (taps k_r + S (J - 1 - t), channel roles swapped per group, zero padding).
