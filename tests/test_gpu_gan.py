@@ -297,6 +297,61 @@ def test_trainer_step_bf16():
     assert not torch.equal(before, g.conv_pre.weight_v.detach())
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,T,C,K,s,pad,Co", [(96, 51, 1024, 5, 1, 2, 1024), (40, 28, 512, 5, 3, 2, 1024),
+                                             (16, 17, 1024, 3, 1, 1, 1), (8, 10, 32, 5, 3, 2, 128),
+                                             (12, 64, 8, 7, 1, 3, 16)])
+def test_joined_conv_matches_per_sequence(N, T, C, K, s, pad, Co, dt):
+    """gan_ops.conv on many short sequences (laid end to end with their zero padding and run as one
+    -- vo_seq_remap join / split) == ConvFn per sequence: the output and the input, weight and bias
+    gradients (fp32 compute: 1e-5; bf16: 1e-2; the layouts themselves move bits exactly)."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    gen = torch.Generator().manual_seed(N * T + C + K)
+    x = torch.randn(N, T, C, generator=gen).cuda().to(dt)
+    w = (torch.randn(Co, C, K, generator=gen) / (C * K) ** 0.5).cuda()
+    b = (torch.randn(Co, generator=gen) * 0.1).cuda()
+    gy = None
+    spec = G.ConvSpec(K=K, pad=pad, stride=s, post="lrelu", post_slope=0.1, co_pad=4 if Co < 4 else None)
+    assert G._joined(x.shape, spec)
+    outs = []
+    for joined in (True, False):
+        xs, ws, bs = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+        y = G.conv(xs, ws, bs, spec, dt) if joined else G.ConvFn.apply(xs, ws, bs, None, None, spec, dt, None)
+        if gy is None:
+            gy = torch.randn(y.shape, generator=gen).cuda().to(y.dtype)
+        y.backward(gy)
+        outs.append([y.detach().float(), xs.grad.float(), ws.grad.float(), bs.grad.float()])
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    for name, a, r in zip(("y", "dx", "dw", "db"), *outs):
+        assert a.shape == r.shape, name
+        assert rel_l2(a.cpu(), r.cpu()) < tol, (name, rel_l2(a.cpu(), r.cpu()))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_seq_remap_exact(dt):
+    """vo_seq_remap (join, split and their adjoints) == index arithmetic in torch, bit for bit."""
+    from visual_onoma_to_wave_amd import ops
+    N, T, C, pad, S_in = 7, 13, 24 if dt == torch.float32 else 8, 3, 21
+    x = torch.randn(N * T, C).cuda().to(dt)
+    got = ops.seq_remap(x, N * S_in, S_in, T, pad, pad + T, -pad)
+    ref = torch.zeros(N, S_in, C, dtype=dt, device="cuda")
+    ref[:, pad:pad + T] = x.view(N, T, C)
+    assert torch.equal(got.view(N, S_in, C), ref)
+    back = ops.seq_remap(got, N * T, T, S_in, 0, T, pad)
+    assert torch.equal(back, x)
+    R = N * S_in - 4  # a joined conv's rows: the last sequence's tail slots missing
+    yj = torch.randn(R, C).cuda().to(dt)
+    split = ops.seq_remap(yj, N * 5, 5, S_in, 0, 5, 0)
+    ref = torch.nn.functional.pad(yj, (0, 0, 0, N * S_in - R)).view(N, S_in, C)[:, :5].reshape(N * 5, C)
+    assert torch.equal(split, ref)
+    adj = ops.seq_remap(split, R, S_in, 5, 0, 5, 0)
+    ref = torch.zeros(N, S_in, C, dtype=dt, device="cuda")
+    ref[:, :5] = split.view(N, 5, C)
+    assert torch.equal(adj, ref.view(-1, C)[:R])
+    with pytest.raises(RuntimeError):
+        ops.seq_remap(yj, N * 5, 5, S_in, 0, 5, R)  # reads past the source
+
+
 def _pack_cases():
     """(weight shape, ConvSpec as ConvFn sees it, input channels) of every conv the C5 step packs:
     the generator's (B = 16 x 32 frames: conv_pre runs joined), the MPD's and the MSD's (16 x 8192)."""

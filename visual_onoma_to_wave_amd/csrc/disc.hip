@@ -177,6 +177,26 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(PackBatchArgs a) {
   for (int t = 0; t < J.T; ++t) dst[plane * t] = from_f32<TD>(row[tb + ts * t]);
 }
 
+// Row remap between the joined and the per-sequence layouts of the short discriminator sequences
+// (hifigan/gan_ops._conv_joined): dst row r = (n, t) with n = r / Td, t = r mod Td receives src row
+// n Ss + t + shift when lo <= t < hi, zeros otherwise -- the join (sequences laid end to end with
+// their zero padding), the split (valid output slots back to (N, T_out)) and both adjoints, each one
+// streaming pass of 16-byte units (F.pad / slice / contiguous ran it as 4-5 fill and copy kernels).
+__global__ void __launch_bounds__(256) seq_remap_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        int64_t dst_rows, int uv, int Td, int64_t Ss, int lo, int hi,
+                                                        int shift) {
+  const int64_t n_units = dst_rows * uv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_units; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / uv;
+    const int c = (int)(i - r * uv);
+    const int64_t n = r / Td;
+    const int t = (int)(r - n * Td);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (t >= lo && t < hi) v = src[(n * Ss + t + shift) * uv + c];
+    dst[i] = v;
+  }
+}
+
 // wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
 // reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
 template <typename TD>
@@ -566,6 +586,27 @@ extern "C" int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* 
     }
   }
   return VO_OK;
+}
+
+extern "C" int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_t dst_rows, int row_bytes, int Td,
+                            int64_t Ss, int lo, int hi, int shift, void* stream) {
+  VO_CHECK_ARG(src && dst && src != dst, "seq_remap: null or aliased pointers");
+  VO_CHECK_ARG(row_bytes > 0 && row_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
+               "seq_remap: rows of %d bytes / pointers not 16-byte multiples", row_bytes);
+  VO_CHECK_ARG(dst_rows >= 0 && Td >= 1 && Ss >= 0 && 0 <= lo && lo <= hi && hi <= Td, "seq_remap: bad layout");
+  if (dst_rows == 0) return VO_OK;
+  if (lo < hi) {  // every row read lies in src
+    const int64_t n_last = (dst_rows - 1) / Td;
+    const int t_hi = (int)std::min<int64_t>(hi, n_last == 0 ? dst_rows : Td) - 1;
+    VO_CHECK_ARG(lo + shift >= 0 && n_last * Ss + t_hi + shift < src_rows,
+                 "seq_remap: reads outside the %lld source rows", (long long)src_rows);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int uv = row_bytes / 16;
+  hipLaunchKernelGGL(seq_remap_kernel, dim3(grid_for(dst_rows * uv)), dim3(256), 0, st, (const uint4*)src, (uint4*)dst,
+                     dst_rows, uv, Td, Ss, lo, hi, shift);
+  VO_RETURN_LAUNCH();
 }
 
 extern "C" int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream) {

@@ -354,15 +354,54 @@ class ConvFn(torch.autograd.Function):
 FLAT_T = int(os.environ.get("VO_FLAT_T", "64"))  # join sequences of up to this many output rows (0: off)
 
 
+class JoinSeqFn(torch.autograd.Function):
+    """(N, T, C) -> (1, N S_in, C): each sequence at offset ``pad`` of its S_in rows, zeros around it
+    (vo_seq_remap; the adjoint gathers the rows back)."""
+
+    @staticmethod
+    def forward(ctx, x, pad, S_in):
+        N, T, C = x.shape
+        ctx.dims = (N, T, pad, S_in)
+        return ops.seq_remap(x.contiguous(), N * S_in, S_in, T, pad, pad + T, -pad).view(1, N * S_in, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        N, T, pad, S_in = ctx.dims
+        C = g.shape[-1]
+        return ops.seq_remap(g.contiguous(), N * T, T, S_in, 0, T, pad).view(N, T, C), None, None
+
+
+class SplitSeqFn(torch.autograd.Function):
+    """(1, R, C) joined conv output -> (N, T_out, C): rows n S_out + t, t < T_out (the slots of
+    outputs that straddle two sequences are dropped; their gradient is zero)."""
+
+    @staticmethod
+    def forward(ctx, yj, N, S_out, T_out):
+        R, C = yj.shape[1], yj.shape[2]
+        ctx.dims = (R, S_out, T_out)
+        return ops.seq_remap(yj.contiguous(), N * T_out, T_out, S_out, 0, T_out, 0).view(N, T_out, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        R, S_out, T_out = ctx.dims
+        C = g.shape[-1]
+        return ops.seq_remap(g.contiguous(), R, S_out, T_out, 0, T_out, 0).view(1, R, C), None, None, None
+
+
 def _conv_joined(x, w, b, spec, cdt, wkey):
     N, T, C = x.shape
     st = spec.stride
     T_out = out_len(spec, T)
     S_out = -(-(T + 2 * spec.pad) // st)     # output slots per sequence
     S_in = st * S_out                         # input rows per sequence: its padding, then zeros
-    xj = F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
+    if (C * x.element_size()) % 16:
+        xj = F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
+    else:
+        xj = JoinSeqFn.apply(x, spec.pad, S_in)
     yj = ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey)  # slot u S_out + t <- rows u S_in + st t + k
-    return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
+    if (yj.shape[-1] * yj.element_size()) % 16:
+        return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
+    return SplitSeqFn.apply(yj, N, S_out, T_out)
 
 
 def _joined(shape, spec, has_res=False):

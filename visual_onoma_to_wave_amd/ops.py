@@ -694,6 +694,19 @@ def pack_batch(jobs, dtype):
                                         _stream(jobs[0][1])), "vo_pack_batch")
 
 
+def seq_remap(src, dst_rows, Td, Ss, lo, hi, shift):
+    """Rows of a channels-last tensor remapped (vo_seq_remap): returns (dst_rows, C) with row
+    r = (n, t) (n = r // Td, t = r % Td) = src row n Ss + t + shift for lo <= t < hi, else 0.
+    ``src``: contiguous, its last dim the row."""
+    _contig(src, "src")
+    C = src.shape[-1]
+    rows = src.numel() // C
+    dst = torch.empty((dst_rows, C), dtype=src.dtype, device=src.device)
+    _lib.check(_lib.lib().vo_seq_remap(_ptr(src), rows, _ptr(dst), dst_rows, C * src.element_size(), Td, Ss, lo, hi,
+                                       shift, _stream(src)), "vo_seq_remap")
+    return dst
+
+
 def pack_dgrad_phase(w, groups, S, k_r, J, ci_out, co_in, dtype, out=None):
     """Stride phase k_r of a strided / grouped conv's input gradient: w (Co, Ci/groups, K) -> packed
     [J][ci_out][co_in] (taps k_r + S (J - 1 - t), channel roles swapped per group, zero padding).
