@@ -338,7 +338,7 @@ typedef struct vo_pack_job {
   int mode, swap, T, rows, width, dst_rows, ld, rpg, cpg, cig, K, tap0, tstep, src_rows;
 } VoPackJob;
 int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* stream);
-/* Row remap of channels-last rows (row_bytes, a multiple of 16): dst row r (r < dst_rows; n = r / Td,
+/* Row remap of channels-last rows (row_bytes, a multiple of 4): dst row r (r < dst_rows; n = r / Td,
  * t = r mod Td) = src row n Ss + t + shift if lo <= t < hi, else zeros.  The joined-sequence layout of
  * the discriminators' short period columns (hifigan/gan_ops._conv_joined) and its adjoint. */
 int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_t dst_rows, int row_bytes, int Td,

@@ -182,16 +182,16 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(PackBatchArgs a) {
 // n Ss + t + shift when lo <= t < hi, zeros otherwise -- the join (sequences laid end to end with
 // their zero padding), the split (valid output slots back to (N, T_out)) and both adjoints, each one
 // streaming pass of 16-byte units (F.pad / slice / contiguous ran it as 4-5 fill and copy kernels).
-__global__ void __launch_bounds__(256) seq_remap_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                        int64_t dst_rows, int uv, int Td, int64_t Ss, int lo, int hi,
-                                                        int shift) {
+template <typename U>  // U: the copy unit (16, 8 or 4 bytes, the largest that divides a row)
+__global__ void __launch_bounds__(256) seq_remap_kernel(const U* __restrict__ src, U* __restrict__ dst, int64_t dst_rows,
+                                                        int uv, int Td, int64_t Ss, int lo, int hi, int shift) {
   const int64_t n_units = dst_rows * uv;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_units; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / uv;
     const int c = (int)(i - r * uv);
     const int64_t n = r / Td;
     const int t = (int)(r - n * Td);
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    U v = {};
     if (t >= lo && t < hi) v = src[(n * Ss + t + shift) * uv + c];
     dst[i] = v;
   }
@@ -591,9 +591,10 @@ extern "C" int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* 
 extern "C" int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_t dst_rows, int row_bytes, int Td,
                             int64_t Ss, int lo, int hi, int shift, void* stream) {
   VO_CHECK_ARG(src && dst && src != dst, "seq_remap: null or aliased pointers");
-  VO_CHECK_ARG(row_bytes > 0 && row_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
-               "seq_remap: rows of %d bytes / pointers not 16-byte multiples", row_bytes);
+  const int unit = row_bytes % 16 == 0 ? 16 : row_bytes % 8 == 0 ? 8 : 4;
+  VO_CHECK_ARG(row_bytes > 0 && row_bytes % 4 == 0 && (reinterpret_cast<uintptr_t>(src) % unit) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dst) % unit) == 0,
+               "seq_remap: rows of %d bytes / pointers not 4-byte multiples", row_bytes);
   VO_CHECK_ARG(dst_rows >= 0 && Td >= 1 && Ss >= 0 && 0 <= lo && lo <= hi && hi <= Td, "seq_remap: bad layout");
   if (dst_rows == 0) return VO_OK;
   if (lo < hi) {  // every row read lies in src
@@ -603,9 +604,17 @@ extern "C" int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_
                  "seq_remap: reads outside the %lld source rows", (long long)src_rows);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int uv = row_bytes / 16;
-  hipLaunchKernelGGL(seq_remap_kernel, dim3(grid_for(dst_rows * uv)), dim3(256), 0, st, (const uint4*)src, (uint4*)dst,
-                     dst_rows, uv, Td, Ss, lo, hi, shift);
+  const int uv = row_bytes / unit;
+  const dim3 g(grid_for(dst_rows * uv));
+  if (unit == 16)
+    hipLaunchKernelGGL(seq_remap_kernel<uint4>, g, dim3(256), 0, st, (const uint4*)src, (uint4*)dst, dst_rows, uv, Td,
+                       Ss, lo, hi, shift);
+  else if (unit == 8)
+    hipLaunchKernelGGL(seq_remap_kernel<uint2>, g, dim3(256), 0, st, (const uint2*)src, (uint2*)dst, dst_rows, uv, Td,
+                       Ss, lo, hi, shift);
+  else
+    hipLaunchKernelGGL(seq_remap_kernel<uint32_t>, g, dim3(256), 0, st, (const uint32_t*)src, (uint32_t*)dst,
+                       dst_rows, uv, Td, Ss, lo, hi, shift);
   VO_RETURN_LAUNCH();
 }
 

@@ -81,7 +81,7 @@ def _pack_grouped(w, dtype, groups, ci_pad, slot):
 def _bias(b, spec, n):
     b = b.detach().float()
     if b.numel() < n:
-        b = torch.cat([b, b.new_zeros(n - b.numel())])
+        b = F.pad(b, (0, n - b.numel()))
     return b.contiguous()
 
 
@@ -394,12 +394,12 @@ def _conv_joined(x, w, b, spec, cdt, wkey):
     T_out = out_len(spec, T)
     S_out = -(-(T + 2 * spec.pad) // st)     # output slots per sequence
     S_in = st * S_out                         # input rows per sequence: its padding, then zeros
-    if (C * x.element_size()) % 16:
+    if (C * x.element_size()) % 4:  # vo_seq_remap moves whole 4-byte words
         xj = F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
     else:
         xj = JoinSeqFn.apply(x, spec.pad, S_in)
     yj = ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey)  # slot u S_out + t <- rows u S_in + st t + k
-    if (yj.shape[-1] * yj.element_size()) % 16:
+    if (yj.shape[-1] * yj.element_size()) % 4:
         return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
     return SplitSeqFn.apply(yj, N, S_out, T_out)
 
