@@ -407,6 +407,10 @@ int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out,
  * (hifigan/models.py:96-103,155-163, SubLayers.py:85-93) in the training backward. */
 int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, int64_t rows,
                   int width, float slope, void* out, int ldo, void* stream);
+/* out = round(g * (ref > 0 ? 1 : slope)) + add (the masked gradient plus a residual branch's gradient
+ * in one pass; add has g's dtype; rows of 8-element vectors, 16-byte aligned). */
+int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, const void* add,
+                      int lda, int64_t rows, int width, float slope, void* out, int ldo, void* stream);
 
 /* ------------------------------------------------------------------ training glue (round 2)
  * BatchNorm with batch statistics over channels-last x (M rows x C channels, VO_F32 / VO_BF16):

@@ -412,11 +412,13 @@ def test_pack_batch_matches_single_packs(dt):
             assert torch.equal(dst, ref(ws[wshape], spec, tag)), (wshape, spec, tag)
 
 
-def test_trainer_prepack_no_first_use_packs():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_trainer_prepack_no_first_use_packs(dt):
     """gan_ops.prepack: after the batched pre-pack no conv of a C5 step packs its own weights (every
     tag the plan writes is the one the conv looks up: generator, both discriminators, D step and
-    G step, the joined-sequence convs of B = 8), and the trained parameters equal the
-    pack-on-first-use path's bit for bit (bf16)."""
+    G step, the joined-sequence convs of B = 8); with it and the ResBlock residual-gradient links
+    (gan_ops.ResLink) the trained parameters and losses equal the pack-on-first-use, autograd-summed
+    path's bit for bit."""
     from visual_onoma_to_wave_amd import hifigan
     from visual_onoma_to_wave_amd.hifigan import gan_ops as G
     h = hifigan.AttrDict(hifigan_h())
@@ -425,11 +427,11 @@ def test_trainer_prepack_no_first_use_packs():
     finals, builds = [], []
     try:
         for pre in (True, False):
-            G.PREPACK = pre
+            G.PREPACK = G.RES_LINK = pre
             G.reset_pack_cache()
             torch.manual_seed(1234)
             g = _gen("cuda")
-            tr = hifigan.HifiGanTrainer(g, h).set_compute_dtype(torch.bfloat16)
+            tr = hifigan.HifiGanTrainer(g, h).set_compute_dtype(dt)
             tr.step(mel, y)
             n0 = G.STATS["pack_builds"]
             losses = tr.step(mel, y)
@@ -440,7 +442,7 @@ def test_trainer_prepack_no_first_use_packs():
                            torch.cat([p.detach().flatten().cpu() for p in tr.mpd.parameters()]),
                            torch.cat([p.detach().flatten().cpu() for p in tr.msd.parameters()])))
     finally:
-        G.PREPACK = True
+        G.PREPACK = G.RES_LINK = True
         G.reset_pack_cache()
     assert builds[0] == 0 and builds[1] > 200, builds
     (l1, g1, p1, s1), (l0, g0, p0, s0) = finals

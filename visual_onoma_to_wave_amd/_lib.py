@@ -144,6 +144,8 @@ _SIGNATURES = {
     "vo_pack_dgrad_phase": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_void_p, c_int, c_void_p]),
     "vo_pack_batch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
+    "vo_lrelu_mask_add": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
+                                  c_float, c_void_p, c_int, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_weight_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

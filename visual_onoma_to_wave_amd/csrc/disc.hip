@@ -390,14 +390,17 @@ __global__ void __launch_bounds__(256) gan_reduce_grad_v8_kernel(int kind, const
   }
 }
 
-template <typename TG, typename TR, bool FLAT>
+// ADD: out = round(masked) + add[r, c] (then rounded): a residual's gradient summed in the same
+// pass -- bit for bit the masked tensor followed by autograd's add of the two gradients
+template <typename TG, typename TR, bool FLAT, bool ADD = false>
 __global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict__ g, int ldg,
                                                             const TR* __restrict__ ref, int ldr, int64_t rows,
-                                                            int width, float slope, TG* __restrict__ out, int ldo) {
+                                                            int width, float slope, TG* __restrict__ out, int ldo,
+                                                            const TG* __restrict__ add = nullptr, int lda = 0) {
   const RowMap rm{width / 8};
   const int64_t nv = rows * rm.wv;
   for (int64_t v = blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256) {
-    int64_t og = v * 8, orf = v * 8, oo = v * 8;
+    int64_t og = v * 8, orf = v * 8, oo = v * 8, oa = v * 8;
     if constexpr (!FLAT) {
       int64_t r;
       int c;
@@ -405,12 +408,19 @@ __global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict
       og = r * ldg + c;
       orf = r * ldr + c;
       oo = r * ldo + c;
+      oa = r * lda + c;
     }
     float x[8], q[8];
     load8(g + og, x);
     load8(ref + orf, q);
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = q[e] > 0.f ? x[e] : x[e] * slope;
+    if constexpr (ADD) {
+      float a[8];
+      load8(add + oa, a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = to_f32(from_f32<TG>(x[e])) + a[e];
+    }
     store8(out + oo, x);
   }
 }
@@ -750,6 +760,31 @@ extern "C" int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* re
     return VO_ERR_INVALID;
   }
 #undef VO_LM
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
+                                 const void* add, int lda, int64_t rows, int width, float slope, void* out, int ldo,
+                                 void* stream) {
+  VO_CHECK_ARG(g && ref && add && out, "lrelu_mask_add: null pointer");
+  VO_CHECK_ARG(rows > 0 && width > 0 && ldg >= width && ldr >= width && ldo >= width && lda >= width,
+               "lrelu_mask_add: bad shape");
+  VO_CHECK_ARG(width % 8 == 0 && v8_ok(g, ldg) && v8_ok(ref, ldr) && v8_ok(out, ldo) && v8_ok(add, lda),
+               "lrelu_mask_add: rows must be 8-element vectors, 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int gv = grid_for(rows * (width / 8));
+#define VO_LMA(TG, TR)                                                                                          \
+  hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, false, true>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg, \
+                     (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo, (const TG*)add, lda)
+  if (g_dtype == VO_BF16 && ref_dtype == VO_BF16) VO_LMA(bf16_t, bf16_t);
+  else if (g_dtype == VO_F32 && ref_dtype == VO_F32) VO_LMA(float, float);
+  else if (g_dtype == VO_BF16 && ref_dtype == VO_F32) VO_LMA(bf16_t, float);
+  else if (g_dtype == VO_F32 && ref_dtype == VO_BF16) VO_LMA(float, bf16_t);
+  else {
+    vo_set_error("lrelu_mask_add: bad dtypes");
+    return VO_ERR_INVALID;
+  }
+#undef VO_LMA
   VO_RETURN_LAUNCH();
 }
 

@@ -238,15 +238,40 @@ def _ncw(t):
     return t.transpose(1, 2).float().contiguous()
 
 
+RES_LINK = os.environ.get("VO_RES_LINK", "1") != "0"  # 0: autograd sums the residual gradients (A/B)
+
+
+class ResLink:
+    """Hands a residual's gradient from the conv that adds it (``res1`` of the second conv of a
+    HiFi-GAN ResBlock pair) to the conv that read the same tensor as its input (the pair's first
+    conv), which adds it in its leaky-ReLU mask pass -- instead of autograd summing the two
+    gradients of that tensor with a separate add kernel.  Only for a tensor with exactly those
+    two uses."""
+
+    def __init__(self):
+        self.armed = False
+        self.g = None
+
+
 class ConvFn(torch.autograd.Function):
-    """y = (post(conv(pre(x), w) + b) + res1) * out_scale + res2, channels-last."""
+    """y = (post(conv(pre(x), w) + b) + res1) * out_scale + res2, channels-last.  ``link``:
+    (ResLink, "in" | "res"): this conv's input ("in") / res1 ("res") is the linked tensor."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None):
+    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None, link=None):
         if spec.post is not None and (res1 is not None or res2 is not None):
             raise ValueError("ConvFn: post-activation with residual inputs is not differentiable here")
         y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt, wkey)
         ctx.spec, ctx.cdt, ctx.wkey = spec, cdt, wkey
+        ctx.link = None
+        if link is not None:
+            lk, role = link
+            if role == "in":  # armed when this conv's backward will run and can take the residual
+                lk.armed = (x.requires_grad and spec.pre_slope is not None and spec.transposed is None
+                            and x.shape[-1] % 8 == 0 and res1 is None and res2 is None)
+                ctx.link = (lk, "in") if lk.armed else None
+            elif role == "res" and lk.armed and res1 is not None and res1.requires_grad:
+                ctx.link = (lk, "res")
         ctx.has = (res1 is not None, res2 is not None)
         ctx.save_for_backward(x, w, y if spec.post is not None else None)
         return y
@@ -259,6 +284,9 @@ class ConvFn(torch.autograd.Function):
         g_res2 = gy if ctx.has[1] and ctx.needs_input_grad[4] else None
         gz = gy * spec.out_scale if spec.out_scale != 1.0 else gy
         g_res1 = gz if ctx.has[0] and ctx.needs_input_grad[3] else None
+        lk, role = ctx.link if ctx.link is not None else (None, None)
+        if role == "res" and g_res1 is not None:  # the residual's gradient goes to the linked input conv
+            lk.g, g_res1 = g_res1, None
         if spec.post == "lrelu":
             gz = ops.lrelu_mask(gz, y, spec.post_slope)
         elif spec.post == "tanh":
@@ -333,7 +361,14 @@ class ConvFn(torch.autograd.Function):
             if need_b:
                 gb = gb2
         if ga is not None:
-            if spec.pre_slope is not None:
+            add = None
+            if role == "in" and lk.g is not None:  # this conv reads the linked tensor: its residual gradient joins here
+                add, lk.g = lk.g, None
+            if add is not None and add.dtype == ga.dtype and ga.shape == add.shape:
+                ga = ops.lrelu_mask(ga, xin, spec.pre_slope, out=ga if ga.is_contiguous() else None, add=add)
+            elif add is not None:
+                raise RuntimeError("ConvFn: linked residual gradient does not match the input gradient")
+            elif spec.pre_slope is not None:
                 ga = ops.lrelu_mask(ga, xin, spec.pre_slope, out=ga if ga.is_contiguous() else None)
             if ga.shape[-1] != x.shape[-1]:
                 ga = F.pad(ga, (0, x.shape[-1] - ga.shape[-1]))
@@ -342,7 +377,7 @@ class ConvFn(torch.autograd.Function):
             gw = None
         if not ctx.needs_input_grad[2]:
             gb = None
-        return gx, gw, gb, g_res1, g_res2, None, None, None
+        return gx, gw, gb, g_res1, g_res2, None, None, None, None
 
 
 # Many short sequences (the MPD's period columns: 96-352 sequences of 10-51 rows at C5): the conv
@@ -410,11 +445,14 @@ def _joined(shape, spec, has_res=False):
             and len(shape) == 3 and shape[0] >= 8 and out_len(spec, shape[1]) <= FLAT_T)
 
 
-def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None):
-    """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged."""
+def conv(x, w, b, spec, cdt, res1=None, res2=None, wkey=None, link=None):
+    """``wkey`` (``weight_key(module)``): reuse the packed weights while the parameters are unchanged.
+    ``link``: (ResLink, role) -- see ResLink."""
     if _joined(x.shape, spec, res1 is not None or res2 is not None):
+        if link is not None:
+            raise ValueError("conv: a linked conv cannot run joined")
         return _conv_joined(x, w, b, spec, cdt, wkey)
-    return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey)
+    return ConvFn.apply(x, w, b, res1, res2, spec, cdt, wkey, link)
 
 
 def conv_spec(shape, spec, has_res=False):

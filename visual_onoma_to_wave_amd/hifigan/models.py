@@ -271,10 +271,14 @@ class Generator(HipModule):
                 rb = self.resblocks[i * self.num_kernels + j]
                 cur = x
                 for n, (c1, c2) in enumerate(zip(rb.convs1, rb.convs2)):
-                    t = G.conv(cur, wgt(c1), c1.bias, spec[c1], dt, wkey=G.weight_key(c1))
+                    # after the first pair, cur has exactly two uses (c1's input, c2's residual):
+                    # their gradients meet in c1's leaky-ReLU mask pass (gan_ops.ResLink)
+                    lk = G.ResLink() if n > 0 and G.RES_LINK else None
+                    t = G.conv(cur, wgt(c1), c1.bias, spec[c1], dt, wkey=G.weight_key(c1),
+                               link=(lk, "in") if lk else None)
                     last = n == len(rb.dilation) - 1
                     cur = G.conv(t, wgt(c2), c2.bias, spec[c2], dt, res1=cur, res2=xs if last else None,
-                                 wkey=G.weight_key(c2))
+                                 wkey=G.weight_key(c2), link=(lk, "res") if lk else None)
                 xs = cur
             x = xs
         m = self.conv_post

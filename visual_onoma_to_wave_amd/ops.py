@@ -987,11 +987,22 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     return (w, db) if with_bias else w
 
 
-def lrelu_mask(g, ref, slope, out=None):
+def lrelu_mask(g, ref, slope, out=None, add=None):
     """g * (ref > 0 ? 1 : slope) (leaky-ReLU / ReLU backward); g, ref (..., C) with row-contiguous
-    last dims (ref may be a channel slice of a wider tensor).  out=g computes in place."""
+    last dims (ref may be a channel slice of a wider tensor).  out=g computes in place.  ``add``
+    (g's shape and dtype): that rounded result plus ``add`` in the same pass (vo_lrelu_mask_add)."""
     if g.shape != ref.shape:
         raise ValueError("lrelu_mask: g and ref shapes differ")
+    if add is not None:
+        if add.shape != g.shape or add.dtype != g.dtype:
+            raise ValueError("lrelu_mask: add must match g")
+        C = g.shape[-1]
+        g, ref, add = g.contiguous(), ref.contiguous(), add.contiguous()
+        out = torch.empty_like(g) if out is None else _contig(out, "out")
+        _lib.check(_lib.lib().vo_lrelu_mask_add(_ptr(g), C, vo_dtype(g), _ptr(ref), C, vo_dtype(ref), _ptr(add), C,
+                                                g.numel() // C, C, float(slope), _ptr(out), C, _stream(g)),
+                   "vo_lrelu_mask_add")
+        return out
     C = g.shape[-1]
 
     def row_strided(t):  # (..., C) rows at a common stride (a channel slice of a wider tensor is fine)
