@@ -258,33 +258,24 @@ class MultiScaleDiscriminator(_DiscBase):
 
 
 def feature_loss(fmap_r, fmap_g):
-    loss = 0
-    for dr, dg in zip(fmap_r, fmap_g):
-        for rl, gl in zip(dr, dg):
-            loss = loss + G.l1_mean(gl, rl)
-    return loss * 2
+    """2 * sum over discriminators and layers of mean|f_r - f_g| (f_r held constant): one
+    ``gan_loss_terms`` vector for every layer."""
+    items = [(gl, rl, ops.GAN_L1, 2.0 / gl.numel()) for dr, dg in zip(fmap_r, fmap_g) for rl, gl in zip(dr, dg)]
+    return G.gan_loss_terms(items).sum()
 
 
 def discriminator_loss(disc_real_outputs, disc_generated_outputs):
-    loss = 0
-    r_losses, g_losses = [], []
-    for dr, dg in zip(disc_real_outputs, disc_generated_outputs):
-        r_loss = G.one_minus_sq_mean(dr)
-        g_loss = G.sq_mean(dg)
-        loss = loss + (r_loss + g_loss)
-        r_losses.append(r_loss)
-        g_losses.append(g_loss)
-    return loss, r_losses, g_losses
+    """(sum of mean((1 - D(y))^2) + mean(D(G(x))^2), [real terms], [generated terms])."""
+    n = len(disc_real_outputs)
+    t = G.gan_loss_terms([(dr, None, ops.GAN_ONE_MINUS_SQ, 1.0 / dr.numel()) for dr in disc_real_outputs]
+                         + [(dg, None, ops.GAN_SQ, 1.0 / dg.numel()) for dg in disc_generated_outputs])
+    return t.sum(), list(t[:n].unbind()), list(t[n:].unbind())
 
 
 def generator_loss(disc_outputs):
-    loss = 0
-    gen_losses = []
-    for dg in disc_outputs:
-        l_ = G.one_minus_sq_mean(dg)
-        gen_losses.append(l_)
-        loss = loss + l_
-    return loss, gen_losses
+    """(sum of mean((1 - D(G(x)))^2), [terms])."""
+    t = G.gan_loss_terms([(dg, None, ops.GAN_ONE_MINUS_SQ, 1.0 / dg.numel()) for dg in disc_outputs])
+    return t.sum(), list(t.unbind())
 
 
 class MelLoss(nn.Module):

@@ -635,6 +635,50 @@ class GanLossFn(torch.autograd.Function):
         return ga, None, None, None
 
 
+class GanLossTermsFn(torch.autograd.Function):
+    """Many GAN / feature-matching terms scale_i * reduce_i(a_i, b_i) as one (n,) vector: the
+    reductions accumulate into one zeroed vector and are scaled by one multiply (the per-term path
+    was a zero fill, the reduction, a scalar multiply and an add per term -- 54 feature-matching
+    terms per G step), and the backward runs one gradient launch per term off one scaled vector."""
+
+    @staticmethod
+    def forward(ctx, kinds, sv, *ab):
+        n = len(kinds)
+        a, b = ab[:n], ab[n:]
+        out = torch.zeros(n, dtype=torch.float32, device=a[0].device)
+        for i in range(n):
+            ops.gan_reduce(kinds[i], a[i], b[i], out=out[i])
+        ctx.kinds = kinds
+        ctx.save_for_backward(sv, *a, *b)
+        return out * sv
+
+    @staticmethod
+    def backward(ctx, g):
+        sv, *ab = ctx.saved_tensors
+        n = len(ctx.kinds)
+        gs = g.float() * sv
+        gas = [ops.gan_reduce_grad(ctx.kinds[i], ab[i], ab[n + i], gs[i]) if ctx.needs_input_grad[2 + i] else None
+               for i in range(n)]
+        return (None, None, *gas, *([None] * n))
+
+
+_SCALES = {}  # (scales, device) -> fp32 vector (made outside graph capture, reused inside)
+
+
+def gan_loss_terms(items):
+    """items: [(a, b or None, kind, scale)] -> (n,) fp32 tensor of scale * reduce(a, b) (b held
+    constant), differentiable in each a."""
+    dev = items[0][0].device
+    key = (tuple(float(it[3]) for it in items), dev)
+    sv = _SCALES.get(key)
+    if sv is None:
+        if torch.cuda.is_current_stream_capturing():  # no host -> device copy inside a capture
+            return torch.stack([GanLossFn.apply(a, None if b is None else b.detach(), k, sc) for a, b, k, sc in items])
+        sv = _SCALES[key] = torch.tensor(key[0], dtype=torch.float32, device=dev)
+    return GanLossTermsFn.apply(tuple(it[2] for it in items), sv, *[it[0] for it in items],
+                                *[None if it[1] is None else it[1].detach() for it in items])
+
+
 def l1_mean(a, b):
     return GanLossFn.apply(a, b.detach(), ops.GAN_L1, 1.0 / a.numel())
 
