@@ -362,6 +362,18 @@ int vo_weight_norm(int n, const void* const* v, const void* const* g, void* cons
                    const int* len, void* stream);
 int vo_weight_norm_bwd(int n, const void* const* v, const void* const* g, const void* const* dw, void* const* dv,
                        void* const* dg, const int* rows, const int* len, void* stream);
+/* Spectral normalisation (torch.nn.utils.spectral_norm: dim 0, one power iteration per training
+ * forward; the HiFi-GAN V1 MSD's first scale in C5) for n layers per call.  Layer: W = weight_orig
+ * (rows x L fp32), buffers u (rows) / v (L) updated in place when power != 0 (v = normalize(W^T u),
+ * u = normalize(W v), normalize(x) = x / max(|x|, eps)), copies of the u / v used written to
+ * u_out / v_out, sigma = u . W v, w = W / sigma; vraw (L) and s (rows) are scratch.  Replaces the
+ * per-layer PyTorch hook (two gemv, norms, clamps, divides, clones and a dot per layer). */
+typedef struct vo_sn_layer {
+  const float* W;
+  float *u, *v, *u_out, *v_out, *vraw, *s, *sigma, *w;
+  int rows, L;
+} VoSnLayer;
+int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float eps, void* stream);
 int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
                   int dtype, float* out, float* workspace, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,

@@ -353,6 +353,38 @@ def test_seq_remap_exact(dt):
         ops.seq_remap(yj, N * 5, 5, S_in, 0, 5, R)  # reads past the source
 
 
+@pytest.mark.parametrize("training", [True, False])
+def test_spectral_norm_vs_torch_hook(training):
+    """gan_ops.spectral_norm_all (vo_spectral_norm, every layer of the spectral-normed MSD scale in
+    one call) against torch.nn.utils.spectral_norm's own hook on a copy of the same modules: the
+    weights, the updated u / v buffers (two passes: the power iteration carries over), and the
+    weight_orig gradients of a random linear loss (fp32: 1e-5 / 1e-5 / 1e-4)."""
+    import copy
+    from torch.nn.utils.spectral_norm import SpectralNorm
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import DiscriminatorS
+    torch.manual_seed(3)
+    d = DiscriminatorS(use_spectral_norm=True).cuda().train(training)
+    ref = copy.deepcopy(d)
+    mods, rmods = list(d.convs) + [d.conv_post], list(ref.convs) + [ref.conv_post]
+    for it in range(2):
+        W = G.spectral_norm_all(mods)
+        rw = []
+        for m in rmods:
+            hook = next(h for h in m._forward_pre_hooks.values() if isinstance(h, SpectralNorm))
+            hook(m, None)
+            rw.append(m.weight)
+        gens = [torch.randn(w.shape, generator=torch.Generator().manual_seed(10 * it + i)).cuda()
+                for i, w in enumerate(rw)]
+        ours = torch.autograd.grad(sum((W[m] * g).sum() for m, g in zip(mods, gens)), [m.weight_orig for m in mods])
+        theirs = torch.autograd.grad(sum((w * g).sum() for w, g in zip(rw, gens)), [m.weight_orig for m in rmods])
+        for m, rm, w, go, gt in zip(mods, rmods, rw, ours, theirs):
+            assert rel_l2(W[m].detach().cpu(), w.detach().cpu()) < 1e-5
+            assert rel_l2(m.weight_u.cpu(), rm.weight_u.cpu()) < 1e-5
+            assert rel_l2(m.weight_v.cpu(), rm.weight_v.cpu()) < 1e-5
+            assert rel_l2(go.cpu(), gt.cpu()) < 1e-4, rel_l2(go.cpu(), gt.cpu())
+
+
 def _pack_cases():
     """(weight shape, ConvSpec as ConvFn sees it, input channels) of every conv the C5 step packs:
     the generator's (B = 16 x 32 frames: conv_pre runs joined), the MPD's and the MSD's (16 x 8192)."""

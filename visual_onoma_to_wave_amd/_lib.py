@@ -52,6 +52,12 @@ class PackJob(ctypes.Structure):
                              "tstep", "src_rows")]
 
 
+class SnLayer(ctypes.Structure):
+    """VoSnLayer (include/vonoma.h, vo_spectral_norm)."""
+    _fields_ = [(f, c_void_p) for f in ("W", "u", "v", "u_out", "v_out", "vraw", "s", "sigma", "w")] + [
+        ("rows", c_int), ("L", c_int)]
+
+
 class HeadDesc(ctypes.Structure):
     _fields_ = [
         ("kind", c_int),
@@ -146,6 +152,7 @@ _SIGNATURES = {
     "vo_pack_batch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "vo_lrelu_mask_add": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
                                   c_float, c_void_p, c_int, c_void_p]),
+    "vo_spectral_norm": (c_int, [c_int, c_void_p, c_int, c_float, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_weight_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

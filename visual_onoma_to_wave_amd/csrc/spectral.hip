@@ -1,0 +1,187 @@
+// Spectral normalisation w = W / sigma(W) with one power iteration per training forward
+// (torch.nn.utils.spectral_norm, dim 0, n_power_iterations 1, eps 1e-12 -- the first scale of the
+// HiFi-GAN V1 MSD, config C5) for MANY layers per launch.  PyTorch's hook ran ~13 kernels per layer
+// and forward (two rocBLAS gemv, norms, clamps, divides, clones, a dot): 8 layers x 3 discriminator
+// passes per C5 step.  Here five launches cover every layer of a pass:
+//   1. vraw = W^T u           one thread per column, 4 waves over interleaved rows, LDS sum in order
+//   2. s = W vraw / max(|vraw|, eps)   one wave per row (|vraw| summed in a fixed order per block)
+//   3. per layer: u = s / max(|s|, eps), sigma = u . s, v = vraw / max(|vraw|, eps)  (buffers + copies)
+//   4. w = W / sigma
+// (eval mode, no power iteration: vraw = v, the norm taken as 1, u kept: sigma = u . W v).
+// Fixed summation orders: deterministic.  Layer tables ride in the kernel arguments.
+
+#include <algorithm>
+
+#include "vo_common.h"
+
+namespace vo {
+
+constexpr int SN_MAX = 16;
+
+struct SnLayer {
+  const float* W;  // (rows, L) = weight_orig flattened
+  float* u;        // (rows) buffer, updated in place (power iteration)
+  float* v;        // (L) buffer, updated in place
+  float* u_out;    // copies of the u / v sigma was computed with (saved for the backward)
+  float* v_out;
+  float* vraw;     // (L) scratch
+  float* s;        // (rows) scratch
+  float* sigma;    // (1)
+  float* w;        // (rows, L) output
+  int rows, L;
+};
+struct SnArgs {
+  SnLayer l[SN_MAX];
+  int blk0[SN_MAX + 1];  // first workgroup of each layer in the launch
+  int n;
+  int power;
+  float eps;
+};
+
+__device__ __forceinline__ int sn_layer(const SnArgs& a, int b) {
+  int li = 0;
+  while (li + 1 < a.n && a.blk0[li + 1] <= b) ++li;
+  return li;
+}
+
+// 1. vraw[c] = sum_r W[r][c] u[r]: 64 columns per workgroup, wave w sums rows w, w + 4, ...
+__global__ void __launch_bounds__(256) sn_wtu_kernel(SnArgs a) {
+  __shared__ float part[4][64];
+  const int li = sn_layer(a, blockIdx.x);
+  const SnLayer L = a.l[li];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = (blockIdx.x - a.blk0[li]) * 64 + lane;
+  float acc = 0.f;
+  if (c < L.L)
+    for (int r = wv; r < L.rows; r += 4) acc += L.W[(int64_t)r * L.L + c] * L.u[r];
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && c < L.L) L.vraw[c] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+__device__ __forceinline__ float sn_block_sumsq(const float* x, int n, float* red) {
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) ss += x[i] * x[i];
+  ss = wave_sum(ss);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// 2. s[r] = (W[r] . vraw) / nv, one wave per row, 4 rows per workgroup
+__global__ void __launch_bounds__(256) sn_wv_kernel(SnArgs a) {
+  __shared__ float red[4];
+  const int li = sn_layer(a, blockIdx.x);
+  const SnLayer L = a.l[li];
+  const float* vr = a.power ? L.vraw : L.v;
+  const float nv = a.power ? fmaxf(sqrtf(sn_block_sumsq(vr, L.L, red)), a.eps) : 1.f;
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x - a.blk0[li]) * 4 + (threadIdx.x >> 6);
+  if (r >= L.rows) return;
+  const float* row = L.W + (int64_t)r * L.L;
+  float acc = 0.f;
+  for (int c = lane; c < L.L; c += 64) acc += row[c] * vr[c];
+  acc = wave_sum(acc);
+  if (lane == 0) L.s[r] = acc / nv;
+}
+
+// 3. one workgroup per layer: u, sigma, v
+__global__ void __launch_bounds__(256) sn_finish_kernel(SnArgs a) {
+  __shared__ float red[4];
+  const SnLayer L = a.l[blockIdx.x];
+  float dot;
+  if (a.power) {
+    const float nu = fmaxf(sqrtf(sn_block_sumsq(L.s, L.rows, red)), a.eps);
+    const float nv = fmaxf(sqrtf(sn_block_sumsq(L.vraw, L.L, red)), a.eps);
+    float d = 0.f;
+    for (int i = threadIdx.x; i < L.rows; i += 256) {
+      const float u = L.s[i] / nu;
+      L.u[i] = u;
+      L.u_out[i] = u;
+      d += u * L.s[i];
+    }
+    for (int i = threadIdx.x; i < L.L; i += 256) {
+      const float v = L.vraw[i] / nv;
+      L.v[i] = v;
+      L.v_out[i] = v;
+    }
+    d = wave_sum(d);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+    __syncthreads();
+    dot = ((red[0] + red[1]) + red[2]) + red[3];
+  } else {
+    float d = 0.f;
+    for (int i = threadIdx.x; i < L.rows; i += 256) {
+      d += L.u[i] * L.s[i];
+      L.u_out[i] = L.u[i];
+    }
+    for (int i = threadIdx.x; i < L.L; i += 256) L.v_out[i] = L.v[i];
+    d = wave_sum(d);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+    __syncthreads();
+    dot = ((red[0] + red[1]) + red[2]) + red[3];
+  }
+  if (threadIdx.x == 0) L.sigma[0] = dot;
+}
+
+// 4. w = W / sigma
+__global__ void __launch_bounds__(256) sn_scale_kernel(SnArgs a) {
+  const int li = sn_layer(a, blockIdx.x);
+  const SnLayer L = a.l[li];
+  const float sg = L.sigma[0];
+  const int64_t n = (int64_t)L.rows * L.L;
+  const int64_t i0 = (int64_t)(blockIdx.x - a.blk0[li]) * 1024 + threadIdx.x;
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = i0 + k * 256;
+    if (i < n) L.w[i] = L.W[i] / sg;
+  }
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+extern "C" int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float eps, void* stream) {
+  VO_CHECK_ARG(n >= 0 && (n == 0 || layers), "spectral_norm: null table");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += SN_MAX) {
+    SnArgs a;
+    a.n = std::min(SN_MAX, n - i0);
+    a.power = power ? 1 : 0;
+    a.eps = eps;
+    for (int i = 0; i < a.n; ++i) {
+      const VoSnLayer& s = layers[i0 + i];
+      VO_CHECK_ARG(s.W && s.u && s.v && s.u_out && s.v_out && s.vraw && s.s && s.sigma && s.w,
+                   "spectral_norm: layer %d: null pointer", i0 + i);
+      VO_CHECK_ARG(s.rows > 0 && s.L > 0 && (int64_t)s.rows * s.L < (1LL << 31),
+                   "spectral_norm: layer %d: bad size", i0 + i);
+      a.l[i] = SnLayer{s.W, s.u, s.v, s.u_out, s.v_out, s.vraw, s.s, s.sigma, s.w, s.rows, s.L};
+    }
+    auto launch = [&](void (*k)(SnArgs), int (*blocks)(const SnLayer&)) -> int {
+      int total = 0;
+      for (int i = 0; i < a.n; ++i) {
+        a.blk0[i] = total;
+        total += blocks(a.l[i]);
+      }
+      a.blk0[a.n] = total;
+      hipLaunchKernelGGL(k, dim3((unsigned)total), dim3(256), 0, st, a);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        vo_set_error("spectral_norm: launch failed: %s", hipGetErrorString(e));
+        return (int)e;
+      }
+      return VO_OK;
+    };
+    int rc;
+    if (a.power && (rc = launch(sn_wtu_kernel, [](const SnLayer& l) { return (l.L + 63) / 64; })) != VO_OK) return rc;
+    if ((rc = launch(sn_wv_kernel, [](const SnLayer& l) { return (l.rows + 3) / 4; })) != VO_OK) return rc;
+    hipLaunchKernelGGL(sn_finish_kernel, dim3((unsigned)a.n), dim3(256), 0, st, a);
+    if ((rc = launch(sn_scale_kernel, [](const SnLayer& l) {
+           return (int)(((int64_t)l.rows * l.L + 1023) / 1024);
+         })) != VO_OK)
+      return rc;
+  }
+  return VO_OK;
+}

@@ -88,6 +88,8 @@ def _prepare(root, layers, dgrad_first):
         key = (root,) + tuple(v for m in mods for v in (m.weight_v._version, m.weight_g._version))
         W = G._cached(key, "W_frozen", lambda: dict(zip(mods, ops.weight_norm(
             [m.weight_v.detach() for m in mods], [m.weight_g.detach() for m in mods]))))
+    if G.BATCHED_SN:  # the spectral-normed convs: one power iteration per pass, as the hook would
+        W = {**W, **G.spectral_norm_all([m for m in root.modules() if hasattr(m, "weight_orig")])}
     cdt = root.compute_dtype
     G.prepack([(G.weight_key(m), _conv_w(m, W[m]), sp, shape, dgrad_first or i > 0)
                for d in layers for i, (m, sp, shape) in enumerate(d) if m in W], cdt)

@@ -563,8 +563,63 @@ class WeightNormFn(torch.autograd.Function):
         return (None, *dvs, *dgs)
 
 
-# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)
+class SpectralNormFn(torch.autograd.Function):
+    """w_k = W_k / sigma_k, sigma_k = u_k . W_k v_k (u, v after the power iteration, held constant:
+    torch.nn.utils.spectral_norm's autograd) for n layers in one vo_spectral_norm call.
+    apply(us, vs, power, eps, W_1..W_n) -> (w_1..w_n); the u / v buffers are updated in place."""
+
+    @staticmethod
+    def forward(ctx, us, vs, power, eps, *Ws):
+        ws, uo, vo, sig = ops.spectral_norm([W.detach() for W in Ws], us, vs, power, eps)
+        ctx.n = len(Ws)
+        ctx.save_for_backward(*Ws, *uo, *vo, *sig)
+        return tuple(ws)
+
+    @staticmethod
+    def backward(ctx, *gws):
+        n, sv = ctx.n, ctx.saved_tensors
+        out = []
+        for W, u, v, sg, g in zip(sv[:n], sv[n:2 * n], sv[2 * n:3 * n], sv[3 * n:], gws):
+            if g is None:
+                out.append(None)
+                continue
+            gm, Wm = g.reshape(W.shape[0], -1), W.reshape(W.shape[0], -1)
+            d = (gm * Wm).sum()  # dL/dsigma = -d / sigma^2; dsigma/dW = u v^T
+            out.append((gm / sg - (d / (sg * sg)) * torch.outer(u, v)).view_as(W))
+        return (None, None, None, None, *out)
+
+
+def spectral_norm_all(mods):
+    """{module: weight} of spectral-normed convs (``weight_orig`` / ``weight_u`` / ``weight_v``, torch's
+    hook: dim 0, one power iteration while the module trains), batched in one vo_spectral_norm call;
+    differentiable through SpectralNormFn while autograd records.  Modules whose hook differs
+    (other dim / iteration count) are left out (their hook runs per use)."""
+    from torch.nn.utils.spectral_norm import SpectralNorm
+    sel = []
+    for m in mods:
+        hook = next((h for h in m._forward_pre_hooks.values() if isinstance(h, SpectralNorm)), None)
+        if hook is not None and hook.name == "weight" and hook.dim == 0 and hook.n_power_iterations == 1:
+            sel.append((m, hook))
+    if not sel:
+        return {}
+    out = {}
+    for power in (True, False):
+        grp = [(m, h) for m, h in sel if bool(m.training) == power]
+        for eps in sorted({h.eps for _, h in grp}):
+            ms = [m for m, h in grp if h.eps == eps]
+            Ws = [m.weight_orig for m in ms]
+            us, vs = [m.weight_u for m in ms], [m.weight_v for m in ms]
+            if torch.is_grad_enabled() and any(W.requires_grad for W in Ws):
+                ws = SpectralNormFn.apply(us, vs, power, eps, *Ws)
+            else:
+                ws = ops.spectral_norm([W.detach() for W in Ws], us, vs, power, eps)[0]
+            out.update(zip(ms, ws))
+    return out
+
+
+# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)
 BATCHED_WN = os.environ.get("VO_BATCHED_WN", "1") != "0"
+BATCHED_SN = os.environ.get("VO_BATCHED_SN", "1") != "0"  # 0: torch's spectral-norm hook per conv (A/B)
 
 
 def weight_norm_all(mods):

@@ -796,6 +796,36 @@ def weight_norm(vs, gs):
     return ws
 
 
+def spectral_norm(Ws, us, vs, power, eps=1e-12):
+    """torch.nn.utils.spectral_norm's weight for many layers (vo_spectral_norm): Ws = weight_orig
+    (rows, ...) fp32, us / vs the u / v buffers (updated in place when ``power``) -> (w list, the u and
+    v copies sigma used, sigma list (1-element tensors))."""
+    n = len(Ws)
+    if n == 0:
+        return [], [], [], []
+    arr = (_lib.SnLayer * n)()
+    outs = []
+    for e, W, u, v in zip(arr, Ws, us, vs):
+        for t, name in ((W, "W"), (u, "u"), (v, "v")):
+            _contig(t, name)
+            if t.dtype != torch.float32:
+                raise ValueError(f"spectral_norm: {name} must be fp32")
+        rows, L = W.shape[0], W.numel() // W.shape[0]
+        if u.numel() != rows or v.numel() != L:
+            raise ValueError("spectral_norm: u / v do not match the weight")
+        o = dict(u_out=torch.empty_like(u), v_out=torch.empty_like(v), vraw=torch.empty_like(v),
+                 s=torch.empty_like(u), sigma=torch.empty(1, dtype=torch.float32, device=W.device),
+                 w=torch.empty_like(W))
+        outs.append(o)
+        e.W, e.u, e.v = W.data_ptr(), u.data_ptr(), v.data_ptr()
+        for k in ("u_out", "v_out", "vraw", "s", "sigma", "w"):
+            setattr(e, k, o[k].data_ptr())
+        e.rows, e.L = rows, L
+    _lib.check(_lib.lib().vo_spectral_norm(n, ctypes.cast(arr, ctypes.c_void_p), 1 if power else 0, float(eps),
+                                           _stream(Ws[0])), "vo_spectral_norm")
+    return [o["w"] for o in outs], [o["u_out"] for o in outs], [o["v_out"] for o in outs], [o["sigma"] for o in outs]
+
+
 def weight_norm_bwd(vs, gs, dws):
     """Backward of ``weight_norm``: lists of dL/dw -> (dL/dv list, dL/dg list)."""
     if not vs:
