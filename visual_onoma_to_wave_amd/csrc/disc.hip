@@ -114,8 +114,7 @@ template <typename TD>
 __global__ void __launch_bounds__(256) pack_batch_kernel(PackBatchArgs a) {
   extern __shared__ float lds[];  // 4 waves x (64 runs x a.kp floats), then 4 x 64 run offsets
   const int b = blockIdx.x;
-  int li = 0;
-  while (li + 1 < a.n && a.blk0[li + 1] <= b) ++li;  // uniform per workgroup
+  const int li = table_find(a.blk0, a.n, b);  // uniform per workgroup
   // the job by value: its fields are read from the kernel arguments once (through a reference
   // the compiler re-read them around every load: a scalar-memory round trip per element)
   const VoPackJob J = a.j[li];

@@ -39,9 +39,7 @@ struct SnArgs {
 };
 
 __device__ __forceinline__ int sn_layer(const SnArgs& a, int b) {
-  int li = 0;
-  while (li + 1 < a.n && a.blk0[li + 1] <= b) ++li;
-  return li;
+  return table_find(a.blk0, a.n, b);
 }
 
 // 1. vraw[c] = sum_r W[r][c] u[r]: 64 columns per workgroup, wave w sums rows w, w + 4, ...

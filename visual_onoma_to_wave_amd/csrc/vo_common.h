@@ -37,11 +37,18 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 // are identical (a NaN input gives a NaN either way).
 __device__ __forceinline__ float lrelu_max(float v, float s) { return __builtin_elementwise_maximum(v, v * s); }
 
-// Workgroup barrier for LDS hand-offs: this wave's LDS operations drained, then s_barrier.
-// __syncthreads() adds a workgroup-scope release fence, and on gfx950 that fence waits vmcnt(0):
-// every outstanding global load or store of the wave (an epilogue's y stores, a prefetch meant to
-// stay in flight across the barrier) is drained at each barrier.  LDS-DMA destinations still
-// need their own vmcnt wait before this barrier; no global memory is handed between waves.
+// Index of the table entry owning item x: the last i < n with start[i] <= x (start ascending,
+// start[0] = 0) -- a binary search over a table in the kernel arguments, so a workgroup near the
+// end of a 32-entry table pays 5 dependent scalar loads instead of 32.
+__device__ __forceinline__ int table_find(const int* start, int n, int x) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (start[mid] <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs by linear id (w -> XCD w % 8), and each
 // XCD has its own L2.  xcd_grouped_id(w, n) maps linear id w of an n-workgroup grid to a logical id
 // in [0, n) such that consecutive logical ids run on one XCD: workgroups that read the same bytes
@@ -52,6 +59,11 @@ __device__ __forceinline__ int xcd_grouped_id(int w, int n) {
   return x * q + (x < r ? x : r) + k;
 }
 
+// Workgroup barrier for LDS hand-offs: this wave's LDS operations drained, then s_barrier.
+// __syncthreads() adds a workgroup-scope release fence, and on gfx950 that fence waits vmcnt(0):
+// every outstanding global load or store of the wave (an epilogue's y stores, a prefetch meant to
+// stay in flight across the barrier) is drained at each barrier.  LDS-DMA destinations still
+// need their own vmcnt wait before this barrier; no global memory is handed between waves.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------- 8-element vectors

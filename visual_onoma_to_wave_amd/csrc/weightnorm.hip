@@ -36,8 +36,7 @@ __global__ void __launch_bounds__(256) weight_norm_kernel(WnArgs a) {
   // this wave's global row (wave-uniform: the layer lookup below stays scalar)
   const int gr = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (gr >= a.row0[a.n]) return;                       // uniform per wave
-  int li = 0;
-  while (li + 1 < a.n && a.row0[li + 1] <= gr) ++li;
+  const int li = table_find(a.row0, a.n, gr);
   const WnLayer& L = a.l[li];
   const int r = gr - a.row0[li], len = L.len;
   const int64_t base = (int64_t)r * len;
