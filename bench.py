@@ -5,9 +5,10 @@ Headline (``--mode infer``, the default): one step = one batch of B synthetic re
 strips (B x 1 x 24 x 102*T_src, T_src=12) through the acoustic model (teacher-forced durations
 summing to T_mel=512 frames, predicted energy) and the HiFi-GAN V1
 generator on its postnet mel (config C3 shape per utterance) -> B x 131,072 samples.  The same
-run also measures BASELINE.json's per-config lines C2 (acoustic only, B=32, mel-frames/s) and
-C3 (generator only, B=64 x 80 x 512, samples/s), each with its own roofline, under
-``configs`` of the one JSON line.  Inputs are resident in HBM before every timed region.
+run also measures BASELINE.json's per-config lines C2 (acoustic only, B=32, mel-frames/s),
+C3 (generator only, B=64 x 80 x 512, samples/s) and -- on one GPU -- C4 (the acoustic training
+step, B=32 x 512 frames) and C5 (the HiFi-GAN V1 training step, B=16 x 8192 samples) as graphed
+single-GPU steps, each with its own roofline, under ``configs`` of the one JSON line.  Inputs are resident in HBM before every timed region.
 Multi-GPU: one process per GPU (torchrun), every rank synthesises its own batch (utterances
 are independent: replicas, no data-path collective), only the timing uses a
 barrier and a MAX all-reduce.
@@ -57,7 +58,8 @@ def parse():
     ap.add_argument("--precision", default="mixed", choices=["mixed", "bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-kernel-timer", action="store_true")
-    ap.add_argument("--no-configs", action="store_true", help="infer: skip the C2 / C3 sub-measurements")
+    ap.add_argument("--no-configs", action="store_true", help="infer: skip the C2 / C3 / C4 / C5 sub-measurements")
+    ap.add_argument("--no-train-configs", action="store_true", help="infer: skip the C4 / C5 sub-measurements")
     ap.add_argument("--no-graph", action="store_true", help="train / gan modes: eager steps instead of one HIP graph")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="infer: run acoustic model and vocoder back to back instead of overlapping the acoustic "
@@ -298,7 +300,68 @@ def measure_c3(a, dev, dist, gen=None):
 
 # ----------------------------------------------------------------------------------- training configs
 
-def bench_train(a, dev, rank, world, dist):
+C4_FWD_FLOPS_B32 = 771.4e9    # vTTS forward at B = 32, T_src = 12, T_mel = 512
+GEN_FLOPS_PER_SAMPLE = 2398848.0  # HiFi-GAN V1 generator FLOPs per output sample
+MSD_CFG = [(1, 128, 15, 1, 1, 7), (128, 128, 41, 2, 4, 20), (128, 256, 41, 2, 16, 20), (256, 512, 41, 4, 16, 20),
+           (512, 1024, 41, 4, 16, 20), (1024, 1024, 41, 1, 16, 20), (1024, 1024, 5, 1, 1, 2)]
+# dominant kernel and kernel families (time, FLOPs, fraction of peak) of the training steps in the
+# committed serialized kernel traces (tools/train_prof.sh -> tools/train_dominant.py)
+TRAIN_DOMINANT = os.path.join("profiles", "r04", "train_dominant.json")
+
+
+def disc_forward_flops(T, B):
+    """Algorithmic FLOPs of one MPD + MSD forward (HiFi-GAN V1) on B waveforms of T samples."""
+    tot = 0
+    ch = [1, 32, 128, 512, 1024, 1024]
+    for p in (2, 3, 5, 7, 11):
+        H = -(-T // p)
+        for i in range(5):
+            Ho = (H + 4 - 5) // (3 if i < 4 else 1) + 1
+            tot += 2 * ch[i] * ch[i + 1] * 5 * Ho * p * B
+            H = Ho
+        tot += 2 * 1024 * 3 * H * p * B
+    L0 = T
+    for sc in range(3):
+        if sc:
+            L0 = (L0 + 4 - 4) // 2 + 1  # AvgPool1d(4, 2, padding=2)
+        L = L0
+        for ci, co, k, s_, g, p in MSD_CFG:
+            L = (L + 2 * p - k) // s_ + 1
+            tot += 2 * (ci // g) * co * k * L * B
+        tot += 2 * 1024 * 3 * L * B
+    return float(tot)
+
+
+def train_step_flops(mode, B, seg=8192):
+    """Algorithmic FLOPs of one training step (forward counts x the backward's 2 passes):
+    C4: 3 x the vTTS forward; C5: the generator 3 x (forward, input and weight gradients), the
+    D step 3 x D(real + fake), the G step D(fake) + D(real features) + D's input gradient."""
+    if mode == "train":
+        return 3 * C4_FWD_FLOPS_B32 * B / 32
+    return 3 * GEN_FLOPS_PER_SAMPLE * B * seg + 9 * disc_forward_flops(seg, B)
+
+
+def _dominant(mode):
+    try:
+        with open(os.path.join(REPO, TRAIN_DOMINANT)) as f:
+            return json.load(f).get(mode)
+    except OSError:
+        return None
+
+
+def train_roofline(mode, B, ms, peak):
+    fl = train_step_flops(mode, B)
+    r = {"bound": "mfma", "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "peak": peak, "unit": "TFLOP/s",
+         "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4), "traffic": None,
+         "flops_per_step": fl, "flops_source": "bench.train_step_flops (DESIGN.md section 7)",
+         "measured_in": "whole graphed step (HIP-graph replays, wall clock over the timed steps)"}
+    dom = _dominant(mode)
+    if dom:  # from the committed serialized kernel trace of this step (not measured in this run)
+        r["dominant_kernel"] = dom
+    return r
+
+
+def run_train(a, dev, rank, world, dist, B=None):
     """C4: scripts/04_train.py step (teacher-forced forward, FastSpeech2Loss, backward with the
     bucketed RCCL all-reduce, clip 1.0, Adam + schedule) on B utterances per GPU, replayed as
     one HIP graph (the all-reduces captured on the side-stream branch) unless --no-graph."""
@@ -307,6 +370,7 @@ def bench_train(a, dev, rank, world, dist):
     from visual_onoma_to_wave_amd import synth
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
     from visual_onoma_to_wave_amd.train import GradBucketer, GraphedTrainStep, train_step, unused_on_path
+    B = B or a.batch
     pc, mc, tc = configs()
     m = vTTS(pc, mc, tc)
     load_into(m, vtts_arrays())
@@ -319,7 +383,7 @@ def bench_train(a, dev, rank, world, dist):
         skip = unused_on_path(m)
         bk = GradBucketer([p for p in m.parameters() if id(p) not in skip], comm_dtype=comm)
         bk.broadcast_parameters(m)
-    b = synth.acoustic_batch(1234 + rank, a.batch, a.src_len, a.mel_len)
+    b = synth.acoustic_batch(1234 + rank, B, a.src_len, a.mel_len)
     t = {k: (torch.from_numpy(v).to(dev) if isinstance(v, np.ndarray) else v) for k, v in b.items()}
     batch = (None, t["audiotypes"], t["texts"], t["src_lens"], t["max_src_len"], t["mels"], t["mel_lens"],
              t["max_mel_len"], t["e_targets"], None, t["d_targets"], t["images"], None)
@@ -332,23 +396,25 @@ def bench_train(a, dev, rank, world, dist):
     for _ in range(a.warmup):
         run(batch)
     elapsed, losses = timed(lambda: run(batch), a.steps, dist)
-    frames = a.batch * a.mel_len * a.steps * world
+    frames = B * a.mel_len * a.steps * world
     n_grad = sum(p.numel() for p in (bk.params if bk else []))
-    if rank == 0:
-        print(json.dumps({
-            "metric": "C4 training mel-frames/sec (FastSpeech2 + variance loss, DDP)", "value": round(frames / elapsed, 1),
-            "unit": "mel-frames/s", "n_gpus": world, "ranks_seen": a.ranks_seen, "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
-            "final_loss": round(float(losses[0].detach()) if torch.is_tensor(losses[0]) else float(losses[0]), 5), "hip_graph": graphed,
-            "allreduce_bytes_per_step": n_grad * (2 if comm is not None else 4) if dist else 0,
-            "config": {"workload": "C4 train step", "per_gpu_batch": a.batch, "global_batch": a.batch * world,
-                       "seq_len": a.mel_len, "src_len": a.src_len,
-                       "parallelism": f"dp{world} (RCCL bucketed all-reduce, {a.comm_dtype})"}}))
+    ms = elapsed / a.steps * 1e3
+    peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
+    return {
+        "metric": "C4 training mel-frames/sec (FastSpeech2 + variance loss, DDP)", "value": round(frames / elapsed, 1),
+        "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
+        "final_loss": round(float(losses[0].detach()) if torch.is_tensor(losses[0]) else float(losses[0]), 5),
+        "hip_graph": graphed,
+        "allreduce_bytes_per_step": n_grad * (2 if comm is not None else 4) if dist else 0,
+        "roofline": train_roofline("train", B, ms, peak),
+        "config": {"workload": "C4 train step", "per_gpu_batch": B, "global_batch": B * world,
+                   "seq_len": a.mel_len, "src_len": a.src_len,
+                   "parallelism": f"dp{world} (RCCL bucketed all-reduce, {a.comm_dtype})"}}
 
 
-def bench_gan(a, dev, rank, world, dist):
+def run_gan(a, dev, rank, world, dist, B=None):
     """C5: HiFi-GAN V1 training step (generator + MPD + MSD, D step then G step with adversarial,
     feature-matching and 45 x mel-L1 losses, AdamW) on B segments of 8192 samples per GPU
     (scripts/hifigan/config.json: batch 16, segment 8192)."""
@@ -356,6 +422,7 @@ def bench_gan(a, dev, rank, world, dist):
     from weights import load_into
     from visual_onoma_to_wave_amd import hifigan
     from visual_onoma_to_wave_amd.hifigan.discriminators import MelLoss
+    B = B or a.batch
     h = hifigan.AttrDict(hifigan_h())
     g = hifigan.Generator(h)
     load_into(g, hifigan_arrays())
@@ -367,7 +434,7 @@ def bench_gan(a, dev, rank, world, dist):
                                 stft_loss_weight=a.stft_loss)
     run = tr.step_graphed if graphed else tr.step
     tr.set_compute_dtype(torch.float32 if a.precision == "fp32" else torch.bfloat16)
-    B, seg = a.batch, h.segment_size
+    seg = h.segment_size
     gen = torch.Generator().manual_seed(99 + rank)
     t = torch.arange(seg, dtype=torch.float32) / h.sampling_rate
     f0 = 110.0 + 330.0 * torch.rand(B, 1, generator=gen)
@@ -379,20 +446,35 @@ def bench_gan(a, dev, rank, world, dist):
         run(x, y)
     elapsed, losses = timed(lambda: run(x, y), a.steps, dist)
     samples = B * seg * a.steps * world
+    ms = elapsed / a.steps * 1e3
+    peak = F32_PEAK_TFLOPS if a.precision == "fp32" else BF16_PEAK_TFLOPS
+    return {
+        "metric": "C5 HiFi-GAN training audio samples/sec (G + MPD + MSD, DDP)", "value": round(samples / elapsed, 1),
+        "unit": "audio samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16" if a.precision != "fp32" else "f32",
+        "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
+        "losses": {k: round(float(v), 4) for k, v in losses.items()},
+        "hip_graph": graphed,
+        "roofline": train_roofline("gan", B, ms, peak) if not a.stft_loss else None,
+        "config": {"workload": "C5 HiFi-GAN V1 train step" + (
+                       f" + {a.stft_loss} x multi-resolution STFT loss" if a.stft_loss else ""),
+                   "per_gpu_batch": B, "global_batch": B * world,
+                   "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D, {a.comm_dtype})"}}
+
+
+def bench_train(a, dev, rank, world, dist):
+    res = run_train(a, dev, rank, world, dist)
     if rank == 0:
-        print(json.dumps({
-            "metric": "C5 HiFi-GAN training audio samples/sec (G + MPD + MSD, DDP)", "value": round(samples / elapsed, 1),
-            "unit": "audio samples/s", "n_gpus": world, "ranks_seen": a.ranks_seen, "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16" if a.precision != "fp32" else "f32",
-            "data": "synthetic (sinusoid + noise segments, their mel as generator input)",
-            "losses": {k: round(float(v), 4) for k, v in losses.items()},
-            "hip_graph": graphed,
-            "config": {"workload": "C5 HiFi-GAN V1 train step" + (
-                           f" + {a.stft_loss} x multi-resolution STFT loss" if a.stft_loss else ""),
-                       "per_gpu_batch": B, "global_batch": B * world,
-                       "segment": seg, "parallelism": f"dp{world} (RCCL bucketed all-reduce, G and D, {a.comm_dtype})"}}))
+        res["ranks_seen"] = a.ranks_seen
+        print(json.dumps(res))
+
+
+def bench_gan(a, dev, rank, world, dist):
+    res = run_gan(a, dev, rank, world, dist)
+    if rank == 0:
+        res["ranks_seen"] = a.ranks_seen
+        print(json.dumps(res))
 
 
 # ----------------------------------------------------------------------------------- launch
@@ -568,6 +650,12 @@ def infer(a, dev, rank, world, dist):
     configs = None
     if not a.no_configs:  # BASELINE.json's per-config lines, same run, same models
         configs = {"C2": measure_c2(a, dev, dist, model), "C3": measure_c3(a, dev, dist, gen)}
+        if world == 1 and not a.no_train_configs:
+            # C4 / C5 as single-GPU graphed steps (BASELINE.json configs 4 and 5 at their per-GPU
+            # batches; the DDP form is --mode train / gan under torchrun)
+            configs["C4"] = run_train(a, dev, rank, world, dist, B=32)
+            torch.cuda.empty_cache()
+            configs["C5"] = run_gan(a, dev, rank, world, dist, B=16)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:

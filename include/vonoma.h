@@ -207,12 +207,13 @@ typedef struct vo_head_desc {
 int vo_variance_head(const vo_head_desc* d, void* stream);
 
 /* Training-side energy embedding (config C4, teacher-forced): idx = bucketize(target, bins)
- * (right=False), out = x + table[idx] (out of place), rows = B*T, table (n_bins + 1, D) fp32;
+ * (right=False; a NaN target -> n_bins, as torch.bucketize), out = x + table[idx] (out of place),
+ * rows = B*T, table (n_table >= n_bins + 1, D) fp32 (VO_ERR_INVALID otherwise);
  * vo_embed_bwd: dtable[e] = sum of dy rows with idx == e, added in row order (deterministic).
  * Replaces: energy_embedding(torch.bucketize(e_target, energy_bins)) and its autograd
  * (scripts/model/modules.py:53-64,101-104). */
 int vo_bucket_embed(const void* x, int x_dtype, const float* target, const float* bins, int n_bins,
-                    const float* table, int64_t rows, int D, void* out, int32_t* idx_out, void* stream);
+                    const float* table, int n_table, int64_t rows, int D, void* out, int32_t* idx_out, void* stream);
 int vo_embed_bwd(const void* dy, int dy_dtype, const int32_t* idx, int64_t rows, int D, int n_table, float* dtable,
                  void* stream);
 

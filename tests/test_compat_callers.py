@@ -90,6 +90,7 @@ def caller_tree(tmp_path, monkeypatch):
         yield tmp_path
     finally:
         compat._caller_mods.clear()
+        compat._caller_errors.clear()
         for k in list(sys.modules):
             if k.split(".")[0] in _ROOTS:
                 del sys.modules[k]
@@ -140,6 +141,7 @@ def test_missing_name_without_caller_tree(tmp_path, monkeypatch):
                    if callable(f))
     finally:
         compat._caller_mods.clear()
+        compat._caller_errors.clear()
         for k in list(sys.modules):
             if k.split(".")[0] in _ROOTS:
                 del sys.modules[k]
@@ -163,6 +165,43 @@ def test_caller_root_argument(tmp_path, monkeypatch):
     finally:
         compat._caller_root = None
         compat._caller_mods.clear()
+        compat._caller_errors.clear()
+        for k in list(sys.modules):
+            if k.split(".")[0] in _ROOTS:
+                del sys.modules[k]
+        sys.modules.update({k: v for k, v in saved.items() if v is not None})
+
+
+def test_failing_caller_tree_probes_stay_probes(tmp_path, monkeypatch):
+    """A caller tools.py whose own imports fail (matplotlib / tensorboard absent) makes ``hasattr`` /
+    ``getattr(..., default)`` return False / the default -- AttributeError chained from the real
+    error -- and is executed once, not on every probe; a name that is not one of the reference's
+    off-path helpers never executes the caller's file."""
+    (tmp_path / "scripts" / "utils").mkdir(parents=True)
+    counter = tmp_path / "count.txt"
+    (tmp_path / "scripts" / "utils" / "tools.py").write_text(textwrap.dedent(f"""
+        open({str(counter)!r}, "a").write("x")
+        import a_module_that_is_not_installed  # noqa
+        def plot_mel(data, stats, titles):
+            return "ok"
+    """))
+    monkeypatch.chdir(tmp_path)
+    saved = {k: sys.modules.get(k) for k in list(sys.modules) if k.split(".")[0] in _ROOTS}
+    from visual_onoma_to_wave_amd import compat
+    compat.install()
+    try:
+        tools = sys.modules["utils.tools"]
+        assert not hasattr(tools, "plot_mel")
+        assert getattr(tools, "synth_one_sample", "default") == "default"
+        with pytest.raises(AttributeError) as ei:
+            tools.plot_mel
+        assert isinstance(ei.value.__cause__, ImportError)
+        assert counter.read_text() == "x"  # executed once
+        assert not hasattr(tools, "no_such_helper")
+        assert counter.read_text() == "x"
+    finally:
+        compat._caller_mods.clear()
+        compat._caller_errors.clear()
         for k in list(sys.modules):
             if k.split(".")[0] in _ROOTS:
                 del sys.modules[k]

@@ -107,12 +107,15 @@ def test_bucketed_ddp_vtts_grads_match_shard_mean(device):
         assert not bad, bad[:8]
 
 
-def _rccl_graph_worker(rank, world, port, out):
+def _rccl_graph_worker(rank, world, port, out, bound=True):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if bound:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:  # default group not bound to a device: the graph group must still connect eagerly
+        dist.init_process_group("nccl", rank=rank, world_size=world)
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim
     from visual_onoma_to_wave_amd.train import GradBucketer, GraphedTrainStep, train_step, unused_on_path
     res = []
@@ -137,12 +140,16 @@ def _rccl_graph_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_graphed_ddp_step_rccl_matches_eager(device):
+@pytest.mark.parametrize("bound", [True, False])
+def test_graphed_ddp_step_rccl_matches_eager(device, bound):
     """The bucketed RCCL all-reduce captured inside the HIP graph of the whole step (one rank:
-    the collective is a real RCCL launch on the side-stream branch of the graph)."""
+    the collective is a real RCCL launch on the side-stream branch of the graph), with the default
+    process group bound to the device (init_process_group(device_id=...)) and without (the graph
+    group's communicator is then connected eagerly by new_group(device_id=...), not inside the
+    capture)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_rccl_graph_worker, args=(1, _free_port(), out), nprocs=1, join=True)
+    mp.spawn(_rccl_graph_worker, args=(1, _free_port(), out, bound), nprocs=1, join=True)
     (le, pe), (lg, pg) = out[0]
     assert np.isfinite(lg).all()
     p_err = float((pg - pe).norm() / pe.norm())

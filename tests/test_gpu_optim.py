@@ -163,3 +163,77 @@ def test_gan_trainer_fused_adamw_matches_torch_adamw(monkeypatch):
     assert rel_l2(gf, gt) < 1e-4
     for k in lt:
         assert abs(lf[k] - lt[k]) <= 1e-3 * abs(lt[k]) + 1e-5, (k, lf[k], lt[k])
+
+
+def test_capturable_lr_survives_load_state_dict():
+    """A capturable FusedAdam (device-tensor lr, the graphed C4 / C5 steps) keeps its lr tensor through
+    load_state_dict (the loaded value is copied into it), so a step captured after a resume still
+    follows the schedule: replays at lr = 0 leave the parameters unchanged, replays at a new lr move
+    them exactly as eager steps at that lr do.  A float-lr group refuses to be captured."""
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    init = _params(5, 4)
+    grads = [g.cuda() for g in _grads(6, init, 1)[0]]
+    src = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    ref_opt = torch.optim.Adam(src, lr=3e-3)
+    for p, g in zip(src, grads):
+        p.grad = g.clone()
+    ref_opt.step()
+    sd = ref_opt.state_dict()
+
+    ps = [torch.nn.Parameter(p.detach().clone()) for p in src]
+    lr_t = torch.tensor(1e-3, device="cuda")
+    opt = FusedAdam(ps, lr=lr_t, capturable=True)
+    opt.load_state_dict(sd)
+    assert opt.param_groups[0]["lr"] is lr_t and float(lr_t) == pytest.approx(3e-3)
+    for p, g in zip(ps, grads):
+        p.grad = g.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        opt.step()  # warm-up (allocates nothing new; state exists)
+    torch.cuda.current_stream().wait_stream(s)
+    eager = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ref2 = FusedAdam(eager, lr=torch.tensor(0.0, device="cuda"), capturable=True)
+    ref2.load_state_dict(opt.state_dict())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        opt.step()
+    lr_t.fill_(0.0)
+    before = [p.detach().clone() for p in ps]
+    graph.replay()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b.detach()) for a, b in zip(before, ps))  # lr 0: no movement
+    lr_t.fill_(5e-3)
+    graph.replay()
+    ref2.param_groups[0]["lr"].fill_(0.0)
+    for p, g in zip(eager, grads):
+        p.grad = g.clone()
+    ref2.step()  # the lr-0 step (advances the step count as the replay did)
+    ref2.param_groups[0]["lr"].fill_(5e-3)
+    ref2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ps, eager):
+        assert rel_l2(a.detach().cpu(), b.detach().cpu()) < 1e-6
+    moved = max(float((a.detach() - b).abs().max()) for a, b in zip(ps, before))
+    assert moved > 1e-4  # the new lr took effect
+
+    # a float learning rate cannot be captured (it would be frozen into the graph)
+    fl = FusedAdam([torch.nn.Parameter(init[0].clone().cuda())], lr=1e-3, capturable=True)
+    fl.param_groups[0]["params"][0].grad = torch.ones_like(fl.param_groups[0]["params"][0])
+    g2 = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="device-tensor learning rates"):
+        with torch.cuda.graph(g2):
+            fl.step()
+
+
+def test_load_state_dict_refuses_unequal_steps():
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    ps = [torch.nn.Parameter(torch.randn(4, device="cuda")) for _ in range(2)]
+    ref = torch.optim.Adam(ps, lr=1e-3)
+    ps[0].grad = torch.ones_like(ps[0])
+    ref.step()
+    ps[1].grad = torch.ones_like(ps[1])
+    ref.step()  # ps[0] at step 2, ps[1] at step 1
+    opt = FusedAdam([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=1e-3)
+    with pytest.raises(ValueError, match="unequal per-parameter steps"):
+        opt.load_state_dict(ref.state_dict())

@@ -233,7 +233,7 @@ def test_bucket_embed_vs_torch(dt):
     bins = torch.linspace(-1.06798, 5.10888, 255)
     tgt = torch.randn(B, T, generator=g) * 2 + 1
     tgt[0, :6] = bins[torch.tensor([0, 1, 100, 200, 253, 254])]          # exactly on edges (right=False)
-    tgt[1, :4] = torch.tensor([-5.0, 9.0, float(bins[7]) - 1e-6, float(bins[7]) + 1e-6])
+    tgt[1, :5] = torch.tensor([-5.0, 9.0, float(bins[7]) - 1e-6, float(bins[7]) + 1e-6, float("nan")])
     emb = torch.nn.Embedding(256, D)
     x = torch.randn(B, T, D, generator=g)
     xg = x.to(dt).cuda().requires_grad_(True)
@@ -253,3 +253,8 @@ def test_bucket_embed_vs_torch(dt):
     assert torch.equal(xg.grad.cpu(), dy.to(dt))
     err = float((e_h.weight.grad.cpu() - emb.weight.grad).norm() / emb.weight.grad.norm())
     assert err < 1e-6, err
+    assert int(idx_ref[1, 4]) == 255  # NaN -> len(bins), as torch.bucketize
+    # a table with fewer than len(bins) + 1 rows is refused before any launch
+    from visual_onoma_to_wave_amd import ops
+    with pytest.raises(Exception, match="table has 200 rows"):
+        ops.bucket_embed(x.cuda().contiguous(), tgt.cuda(), bins.cuda(), torch.zeros(200, D, device="cuda"))

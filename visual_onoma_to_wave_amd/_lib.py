@@ -106,8 +106,8 @@ _SIGNATURES = {
                                        c_void_p]),
     "vo_lr_lengths": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_variance_head": (c_int, [ctypes.POINTER(HeadDesc), c_void_p]),
-    "vo_bucket_embed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, ctypes.c_int64, c_int,
-                                c_void_p, c_void_p, c_void_p]),
+    "vo_bucket_embed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, ctypes.c_int64,
+                                c_int, c_void_p, c_void_p, c_void_p]),
     "vo_adam_multi": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                               c_float, c_float, c_float, c_int, c_void_p]),
     "vo_opt_step_increment": (c_int, [c_void_p, c_void_p]),

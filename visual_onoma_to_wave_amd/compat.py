@@ -55,6 +55,7 @@ _MAP = {
 
 _caller_root = None          # set by install(caller_root=...)
 _caller_mods = {}            # "utils.tools" -> the caller's module (executed once)
+_caller_errors = {}          # "utils.tools" -> the exception its execution raised (not retried)
 
 
 def install(prefixes=("", "scripts."), caller_root=None):
@@ -66,6 +67,7 @@ def install(prefixes=("", "scripts."), caller_root=None):
     if caller_root is not None:
         _caller_root = os.fspath(caller_root)
     _caller_mods.clear()
+    _caller_errors.clear()
     if "scripts." in prefixes and "scripts" not in sys.modules:
         import types
         pkg = types.ModuleType("scripts")
@@ -106,6 +108,8 @@ def _load_caller(modname):
     rel = modname.replace(".", os.sep) + ".py"
     path = next((os.path.join(d, rel) for d in _scripts_dirs()
                  if os.path.isfile(os.path.join(d, rel))), None)
+    if modname in _caller_errors:  # a failed execution is not retried on every attribute probe
+        raise _caller_errors[modname]
     mod = None
     if path is not None:
         pkg, _, leaf = modname.rpartition(".")
@@ -119,19 +123,39 @@ def _load_caller(modname):
         sys.modules[name] = mod
         try:
             spec.loader.exec_module(mod)
-        except BaseException:
+        except Exception as e:
             del sys.modules[name]
+            _caller_errors[modname] = e
             raise
     _caller_mods[modname] = mod
     return mod
 
 
+# names off the synthesis path that the caller's own utils files provide (reference
+# scripts/utils/tools.py, scripts/utils/model.py); any other missing name is an AttributeError
+# without executing the caller's file
+CALLER_NAMES = {
+    "utils.tools": {"to_device_synth", "log", "synth_one_sample", "plot_mel_withinput", "synth_samples",
+                    "synth_for_eval", "synth_for_eval_strech", "synth_for_eval_continue", "plot_mel",
+                    "pad_2D_image", "save_figure_to_numpy", "plot_alignment_to_numpy"},
+    "utils.model": set(),
+}
+
+
 def caller_attr(modname, name):
     """``name`` from the caller's own ``scripts/<modname>.py`` (module ``__getattr__`` hook of
-    ``utils.tools`` / ``utils.model``); AttributeError when the caller's tree lacks it."""
-    if name.startswith("__"):
-        raise AttributeError(name)
-    mod = _load_caller(modname)
+    ``utils.tools`` / ``utils.model``) for the names in ``CALLER_NAMES``.  Always AttributeError
+    otherwise -- also when executing the caller's file failed (an optional import it needs is
+    missing), so ``hasattr`` / ``getattr(..., default)`` probes stay probes; the failure is
+    remembered and chained, not re-executed."""
+    allowed = CALLER_NAMES.get(modname)
+    if name.startswith("__") or (allowed is not None and name not in allowed):
+        raise AttributeError(f"module '{modname}' has no attribute '{name}'")
+    try:
+        mod = _load_caller(modname)
+    except Exception as e:
+        raise AttributeError(f"module '{modname}' has no attribute '{name}': executing the caller's "
+                             f"scripts/{modname.replace('.', '/')}.py failed ({type(e).__name__}: {e})") from e
     if mod is None or not hasattr(mod, name):
         raise AttributeError(
             f"module '{modname}' has no attribute '{name}': it is not on the synthesis path "

@@ -956,10 +956,12 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
         // Round 2: weights by LDS-DMA (GL): 0.084 / 0.134 / 0.171 -> 0.083 / 0.126 / 0.163 ms for
         // k = 3 / 7 / 11 alone (tools/ab_conv_cfg.py, bit-identical), within noise in the bench step;
         // conv_cfg 3 = register-staged weights, 4 = GL with 3-tap steps (spills)
+#ifdef VO_ABLATIONS  // measured-and-dropped tiles (A/B builds only: make abl)
         if (vo_tune_get("conv_cfg") == 1) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 4, 2, 2, 2, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 2) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 3) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 4) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 3, 1, 1, 0, true>(d, st);
+#endif
         // Round 2: role-split staging (RS: half the waves issue the weight DMA, half copy the window by
         // LDS-DMA two chunks ahead; bare step barriers): k = 7 / 11 0.137 / 0.175 -> 0.130 / 0.168 ms,
         // k = 3 0.084 -> 0.096 (two-step chunks: the weight waves' 8 DMA pieces per step, not the

@@ -24,6 +24,7 @@ __global__ void __launch_bounds__(256) bucket_embed_kernel(const TX* __restrict_
     const int mid = (lo + hi) >> 1;
     if (bins[mid] < v) lo = mid + 1; else hi = mid;
   }
+  if (v != v) lo = n_bins;   // NaN -> n_bins, as torch.bucketize
   if (lane == 0 && idx_out) idx_out[row] = lo;
   const float* e = table + (int64_t)lo * D;
   const TX* xr = x + row * D;
@@ -55,9 +56,12 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const TG* __restrict__ d
 using namespace vo;
 
 extern "C" int vo_bucket_embed(const void* x, int x_dtype, const float* target, const float* bins, int n_bins,
-                               const float* table, int64_t rows, int D, void* out, int32_t* idx_out, void* stream) {
+                               const float* table, int n_table, int64_t rows, int D, void* out, int32_t* idx_out,
+                               void* stream) {
   VO_CHECK_ARG(x && target && bins && table && out, "bucket_embed: null pointer");
   VO_CHECK_ARG(rows >= 0 && D > 0 && D % 4 == 0 && n_bins > 0, "bucket_embed: bad sizes");
+  VO_CHECK_ARG(n_table >= n_bins + 1, "bucket_embed: table has %d rows, bucketize over %d bins needs %d", n_table,
+               n_bins, n_bins + 1);
   VO_CHECK_ARG(x_dtype == VO_F32 || x_dtype == VO_BF16, "bucket_embed: x must be fp32 or bf16");
   if (rows == 0) return VO_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

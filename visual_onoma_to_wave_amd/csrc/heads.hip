@@ -49,12 +49,14 @@ __global__ void __launch_bounds__(256) head_kernel(vo_head_desc d) {
     v = __fdiv_rn(__fsub_rn(v, d.e_mean), d.e_std);
     pred = v;
   }
-  // bucketize(right=False): number of bins strictly below v
+  // bucketize(right=False): number of bins strictly below v; a NaN goes to bucket n_bins, as in
+  // torch.bucketize (every comparison with NaN is false there)
   int lo = 0, hi = d.n_bins;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (d.bins[mid] < v) lo = mid + 1; else hi = mid;
   }
+  if (v != v) lo = d.n_bins;
   const int idx = lo;
   if (lane == 0) {
     d.pred[row] = pred;

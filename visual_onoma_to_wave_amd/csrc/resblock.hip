@@ -611,6 +611,9 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
 int vo_pair3_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                  const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                  hipStream_t st, int* handled);  // resblock4.hip
+int vo_pair_pc_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                   const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale,
+                   hipStream_t st, int* handled);  // resblock_pc.hip
 int vo_pair_wave_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                      const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                      hipStream_t st, int* handled);  // resblock5.hip
@@ -636,6 +639,14 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
+  // round 4: C = 128, k = 7 / 11 -> the producer-role kernel (resblock_pc.hip); pair_cfg 70 keeps the
+  // round-3 kernel below (the A/B reference, and the path of every other C = 128 shape)
+  if (C == 128 && cfg == 0) {
+    int handled = 0;
+    const int rc = vo_pair_pc_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, st, &handled);
+    if (handled) return rc;
+  }
+#ifdef VO_ABLATIONS  // measured-and-dropped variants (A/B builds only: make abl)
   if (cfg == 50) {  // round 3: C = 32 with wave-private frames (resblock5.hip)
     int handled = 0;
     const int rc = vo_pair_wave_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
@@ -646,10 +657,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     const int rc = vo_pair3_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;
   }
-  // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
-  // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
-  // At C = 128 it measured -1 % (k = 7) / +5 % (k = 11): there only pair_cfg 30 selects it.
-  if ((C == 64 && cfg != 9 && (cfg < 20 || (cfg >= 32 && cfg <= 35))) || cfg == 30 || cfg == 31) {
+  if (cfg == 30 || cfg == 31) {  // the version-2 kernel at C = 128 (resblock2.hip): -1 % at k = 7, +5 % at k = 11
     int handled = 0;
     const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;
@@ -670,22 +678,15 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
       const bool small = cfg == 9 ? K <= 7 : cfg == 1;
       return small ? pair_launch<32, 1, 8, 2, true, 1>(a, B, st) : pair_launch<32, 1, 8, 4, true, 1>(a, B, st);
     }
-    // 512-row in-place tiles, window / residual fetched after P2: k = 11 -13 %, k = 7 -3 %
-    // (k = 3 is HBM-bound at ~5 TB/s either way; tools/ab_sb.py pair32 9 5)
-    return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true, false>(a, B, st);
   }
   if (C == 128) {
-    // 2 x 4 waves of 64 channels (2 waves/SIMD), weights by LDS-DMA.  k = 3: 128-row tiles;
-    // k >= 7: 192-row tiles with T1 over the window (IP), 8 % faster at k = 11 (tools/ab_sb.py).
-    // pair_cfg 1 = the register-staged 128-row kernel, 13 = its no-global-load timing ablation.
-    // In the bench step: s1 0.62 -> 0.545 ms per launch (tools/bench_ab.sh).
+    // 2 x 4 waves of 64 channels (2 waves/SIMD), weights by LDS-DMA.  pair_cfg 1 = the register-staged
+    // 128-row kernel, 13 = its no-global-load timing ablation.
     if (cfg == 1) return pair_launch<128, 2, 4, 2, false, 1>(a, B, st);
-#ifdef VO_ABLATIONS  // timing ablations (garbage results): never in the shipped dispatch
     if (cfg == 13) return pair_launch<128, 2, 4, 2, false, 1, 3>(a, B, st);
     if (cfg == 16) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, true>(a, B, st);
     if (cfg == 17) return pair_launch<128, 2, 4, 4, false, 1, 2, 0, false, true, true, false, true>(a, B, st);
     if (cfg == 25) return pair_launch<128, 2, 4, 4, false, 1, 1, 0, false, true, true, false, true>(a, B, st);
-#endif
     if (cfg == 2) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
     if (cfg == 3) return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
     // two 4-wave workgroups per CU (79 KB LDS each: 128-row in-place tiles, half-tap weight
@@ -695,54 +696,52 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
     // weight stream per MFMA of the 192-row kernel (384 rows spill)
     if (cfg == 6) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
     if (cfg == 7) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
-    // measured on the round-2 epilogue (tools/bench_ab.sh, two rounds each): the default k >= 7
-    // kernel with the pinned fragment pipeline (SB) +1.5 % (one spilled VGPR), with setprio
-    // around its MFMA clusters (PRIO 1) within noise -- neither kept.
-    // measured and dropped (tools/ab_sb.py): one wave per SIMD with 128 x 64-row wave tiles
-    // (0.375 LDS reads per MFMA) 30-45 % slower -- latency no longer hidden; three waves per
-    // SIMD (12 waves, 2 x 6) 15 % slower  Round 3, remeasured with the pinned fragment pipeline
-    // (SB) and 512 registers per wave (launch bounds 1 workgroup / CU): 20-27 % slower at k = 7 / 11
-    // (tools/mrf_bench.py, profiles/r03/s1_one_wave_per_simd_ab.txt), 2 % faster at k = 3.
-    // timing ablations (VO_ABLATIONS builds only): no window / residual loads 0.70 -> 0.58 ms at
-    // k = 11, 0.52 -> 0.41 at k = 7 (cfg 17); no weight DMA 0.70 -> 0.63 (cfg 25).  Measured and
-    // dropped in round 2 (tools/ab_pair2.py): the next window staged through registers during P2
-    // with T1 beside the window (192-row tiles: +20 %), the next group's DMA pieces spread between
-    // the tap steps (+2 %), 320 / 384-row tiles (spill), the version-2 kernel (pair_cfg 30: +5 % at
-    // k = 11 -- its in-P2 window loads wait behind the in-order vmcnt of the weight DMA), and an
-    // L2 / MALL prefetch of the epilogue's bytes (next window, residual, accumulator) by LDS-DMA
-    // pieces into a trash row during P2: +8 % with 1 KiB pieces (1-4 per wave per group: +8..18 %),
-    // +7 % with 8 KiB one-dword-per-line pieces (26 per tile) -- the piece issue costs more than
-    // the exposed loads it shortens; and a kernel with the weights out of LDS altogether (each
-    // wave's A fragments loaded from global one tap ahead into a register ring, no per-tap barrier,
-    // the freed LDS double-buffering the window, filled between taps): bit-identical but +20 %
-    // (k = 11: 0.69 -> 0.83 ms; MFMA busy 46.5 -> 38.6 %, waits on the fragment loads 56 % of wave
-    // cycles -- one tap of prefetch does not cover the L1 / L2 latency of 64 KiB of fragment loads
-    // per tap per CU, and a deeper ring does not fit the registers)
     if (cfg == 60) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, true, true, true, false, true>(a, B, st);
-    if (cfg == 9) {  // the previous defaults
+    if (cfg == 9) {  // the round-2 defaults
       if (K <= 3) return pair_launch<128, 2, 4, 2, false, 1, 0, 0, false, true>(a, B, st);
       return pair_launch<128, 2, 4, 3, false, 1, 0, 0, false, true, true>(a, B, st);
     }
-    // 256-row in-place tiles, window / residual fetched after P2 (no window registers live in
-    // the MFMA loop): k = 3 with half-tap buffers (-10 %), k >= 7 with whole taps (-4..6 %)
-    // against the 128 / 192-row kernels (tools/ab_sb.py pair 9 6 7)
+    if (cfg == 61 && K > 3) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
+  }
+  if (C == 64) {
+    // pair_cfg 3 / 4 / 5: 512-row IP + LDS-DMA / 384-row IP + LDS-DMA / 512-row IP
+    // pair_cfg 1 = LDS-DMA weights + pinned fragment pipeline: 7 % faster alone (tools/ab_sb.py)
+    // but 15 % slower inside the bench step with the MRF accumulator (tools/bench_ab.sh)
+    if (cfg == 3) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
+    if (cfg == 4) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
+    if (cfg == 5) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
+    if (cfg == 1) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, true, true>(a, B, st);
+    if (cfg == 9) return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);  // the round-2 default
+    if (cfg == 2 && K <= 3) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
+  }
+#endif
+  // C = 64, k >= 7: the version-2 kernel (resblock2.hip: compile-time K, next window fetched during
+  // P2): 0.453 -> 0.408 ms at k = 11, 0.359 -> 0.326 at k = 7, bit-identical (tools/ab_pair2.py).
+  if (C == 64) {
+    int handled = 0;
+    const int rc = vo_pair2_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
+  if (C == 32) {
+    // 512-row in-place tiles, window / residual fetched after P2: k = 11 -13 %, k = 7 -3 %
+    // (k = 3 is HBM-bound at ~5 TB/s either way; tools/ab_sb.py pair32 9 5); without the VALU diet
+    return pair_launch<32, 1, 8, 4, true, 1, 0, 0, false, false, true, false, true, false>(a, B, st);
+  }
+  if (C == 128) {
+    // 256-row in-place tiles, window / residual fetched after P2 (no window registers live in the
+    // MFMA loop): k = 3 with half-tap buffers (-10 %), k >= 7 with whole taps and the software-
+    // pipelined steps (SB: the next (tap, plane) step's fragments read right after the current step's
+    // first MFMA, -1..2 %).  Measured and dropped (tools/ab_sb.py, tools/mrf_bench.py, DESIGN.md
+    // section 3): one wave per SIMD with 128 x 64-row wave tiles (20-45 % slower), three waves per SIMD
+    // (15 % slower), the next window staged through registers during P2 (+20 %), 320 / 384-row tiles
+    // (spill), an L2 / MALL prefetch of the epilogue's bytes by LDS-DMA pieces (+7..18 %), the weights
+    // out of LDS (A fragments from global one tap ahead: +20 %).  Timing ablations (VO_ABLATIONS
+    // builds): no window / residual loads 0.70 -> 0.58 ms at k = 11; no weight DMA 0.70 -> 0.63.
     if (K <= 3) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, true>(a, B, st);
-    // round 3: the software-pipelined steps (SB: the next (tap, plane) step's fragments read right
-    // after the current step's first MFMA) -1..2 % at k = 7 / 11, bit-identical (pair_cfg 61 = without)
-    if (cfg == 61) return pair_launch<128, 2, 4, 4, false, 1, 0, 0, false, true, true, false, true>(a, B, st);
     return pair_launch<128, 2, 4, 4, false, 1, 0, 0, true, true, true, false, true>(a, B, st);
   }
-  // C = 64: k = 3 -> both convs resident in LDS; k >= 7 -> 2-tap groups, register staged.
-  // pair_cfg 3 / 4 / 5: 512-row IP + LDS-DMA / 384-row IP + LDS-DMA / 512-row IP (the default)
-  // pair_cfg 1 = LDS-DMA weights + pinned fragment pipeline: 7 % faster alone (tools/ab_sb.py)
-  // but 15 % slower inside the bench step with the MRF accumulator (tools/bench_ab.sh)
-  if (cfg == 3) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
-  if (cfg == 4) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, false, true, true, false, true>(a, B, st);
-  if (cfg == 5) return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
-  if (K <= 3 && cfg != 2) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
-  if (cfg == 1) return pair_launch<64, 1, 8, 3, false, 2, 0, 0, true, true>(a, B, st);
-  if (cfg == 9) return pair_launch<64, 1, 8, 3, false, 2>(a, B, st);  // the previous default
-  // k >= 7: 512-row in-place tiles, window / residual fetched after P2: -5 % against the
-  // 384-row kernel with T1 beside the window (tools/ab_sb.py pair64 9 5)
+  // C = 64: k = 3 -> both convs resident in LDS; other k (the version-2 kernel covers 7 / 11) ->
+  // 512-row in-place tiles, window / residual fetched after P2 (-5 % against the 384-row kernel)
+  if (K <= 3) return pair_launch<64, 1, 8, 2, true, 1>(a, B, st);
   return pair_launch<64, 1, 8, 4, false, 2, 0, 0, false, false, true, false, true>(a, B, st);
 }

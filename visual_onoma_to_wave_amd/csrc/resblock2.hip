@@ -504,13 +504,19 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
                  const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                  hipStream_t st, int* handled) {
   *handled = 0;
-  if (!((C == 64 || C == 128) && (K == 7 || K == 11) && dil >= 1 && dil <= PAIR2_DMAX)) return VO_OK;
+#ifdef VO_ABLATIONS
+  const bool c128 = C == 128;  // the C = 128 form is an A/B variant (pair_cfg 30 / 31)
+#else
+  const bool c128 = false;
+#endif
+  if (!((C == 64 || c128) && (K == 7 || K == 11) && dil >= 1 && dil <= PAIR2_DMAX)) return VO_OK;
   Pair2Args a;
   a.x = (const bf16_t*)x; a.w1 = (const bf16_t*)w1; a.b1 = b1; a.w2 = (const bf16_t*)w2; a.b2 = b2;
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
   a.T = T; a.dil = dil; a.slope = slope; a.out_scale = out_scale;
   a.tiles_per_b = a.ntiles = 0;
   *handled = 1;
+#ifdef VO_ABLATIONS
   if (C == 128) {  // 2 x 4 waves of 64 channels, 256-row tiles, whole taps by LDS-DMA
     if (K == 7) return pair2_launch<128, 2, 4, 4, 7, true, 1>(a, B, st);
     return pair2_launch<128, 2, 4, 4, 11, true, 1>(a, B, st);
@@ -520,7 +526,7 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
   // faster alone (tools/ab_pair2.py), but s2 -3.6 % / s3 +4 % and the same 13.75 ms in the bench step
   // VALU diet (VD) at C = 64: k = 11 0.408 -> 0.398 ms, k = 7 0.311 -> 0.318 (tools/mrf_bench.py
   // --tune pair_cfg=33,0, round 3): k = 11 ships with it, k = 7 without; cfg 33 swaps both, for A/B
-  if (cfg == 33) {
+  if (cfg == 33) {  // (A/B variants of the C = 64 kernel: VO_ABLATIONS builds only)
     if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, true>(a, B, st);
     return pair2_launch<64, 1, 8, 4, 11, false, 2, false>(a, B, st);
   }
@@ -541,6 +547,9 @@ int vo_pair2_try(const void* x, const void* w1, const float* b1, const void* w2,
     if (K == 7) return pair2_launch<64, 1, 4, 4, 7, false, 2>(a, B, st);
     return pair2_launch<64, 1, 4, 4, 11, false, 2>(a, B, st);
   }
+#else
+  (void)cfg;
+#endif
   if (K == 7) return pair2_launch<64, 1, 8, 4, 7, false, 2, false>(a, B, st);
   return pair2_launch<64, 1, 8, 4, 11, false, 2, true>(a, B, st);
 }

@@ -600,6 +600,7 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
+#ifdef VO_ABLATIONS  // measured-and-dropped variants (A/B builds only: make abl)
   if (C == 32 && (cfg == 30 || cfg == 31)) {  // round 3: wave-private frames (resblock5.hip)
     int handled = 0;
     const int rc = vo_rb3_wave_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, cfg, st, &handled);
@@ -610,10 +611,7 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
     if (C == 64) return rb3_launch<64, 1, 8, 4, false, 1, 2, false>(a, B, st);
     return rb3_launch<128, 2, 4, 4, false, 1, 2, false>(a, B, st);
   }
-  if (C == 32) {  // 256-row frames, all weights resident: 2 workgroups (4 waves / SIMD) per CU
-    if (cfg == 1) return rb3_launch<32, 1, 8, 4, true>(a, B, st);
-    return rb3_launch<32, 1, 8, 2, true>(a, B, st);
-  }
+  if (C == 32 && cfg == 1) return rb3_launch<32, 1, 8, 4, true>(a, B, st);
   if (C == 64) {
     if (cfg == 1) return rb3_launch<64, 1, 8, 2, false>(a, B, st);
     if (cfg == 4) return rb3_launch<64, 1, 8, 4, false, 1, 4>(a, B, st);
@@ -627,16 +625,23 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
     if (cfg == 41) return rb3_launch<64, 1, 8, 3, false, 1, 2, true, 3>(a, B, st);
     if (cfg == 43) return rb3_launch<64, 1, 8, 3, false, 1, 2, true, 3, true>(a, B, st);
     if (cfg == 44) return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 1, true>(a, B, st);
-    // a whole conv (3 taps, 24 KB) per streamed group: 6 barriers per tile instead of 24, 0.476 ->
-    // 0.448 ms (tools/mrf_bench.py --stages 2 --tune rb3_cfg=0,40, round 3, bit-identical); with the
-    // software-pipelined steps (PIPE) 0.443 -> 0.437 ms
     if (cfg == 45) return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3>(a, B, st);
-    return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3, true>(a, B, st);
   }
-  if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
-  if (cfg == 4) return rb3_launch<128, 2, 4, 4, false, 2, 4>(a, B, st);
-  // software-pipelined steps (PIPE: the next (tap, plane) step's fragments read during the current
-  // step's MFMAs): 0.720 -> 0.686 ms, bit-identical (tools/mrf_bench.py --tune rb3_cfg=0,42, round 3)
-  if (cfg == 42) return rb3_launch<128, 2, 4, 4, false>(a, B, st);
+  if (C == 128) {
+    if (cfg == 1) return rb3_launch<128, 2, 4, 2, false>(a, B, st);
+    if (cfg == 4) return rb3_launch<128, 2, 4, 4, false, 2, 4>(a, B, st);
+    if (cfg == 42) return rb3_launch<128, 2, 4, 4, false>(a, B, st);  // without the PIPE steps
+  }
+#else
+  (void)cfg;
+#endif
+  // C = 32: 256-row frames, all weights resident: 2 workgroups (4 waves / SIMD) per CU
+  if (C == 32) return rb3_launch<32, 1, 8, 2, true>(a, B, st);
+  // C = 64: a whole conv (3 taps, 24 KB) per streamed group: 6 barriers per tile instead of 24, 0.476
+  // -> 0.448 ms (tools/mrf_bench.py --stages 2 --tune rb3_cfg=0,40, round 3, bit-identical); with the
+  // software-pipelined steps (PIPE) 0.443 -> 0.437 ms
+  if (C == 64) return rb3_launch<64, 1, 8, 4, false, 1, 2, true, 3, true>(a, B, st);
+  // C = 128: software-pipelined steps (PIPE: the next (tap, plane) step's fragments read during the
+  // current step's MFMAs): 0.720 -> 0.686 ms, bit-identical (tools/mrf_bench.py --tune rb3_cfg=0,42)
   return rb3_launch<128, 2, 4, 4, false, 1, 2, true, 1, true>(a, B, st);
 }

@@ -20,6 +20,8 @@
 //  * the MRF accumulator rows are requested in the last c2 group and consumed by the epilogue.
 // Each wave owns all C output channels of 16 NJ consecutive rows (NI = C / 16 co tiles).
 
+// Measured-and-dropped (round 3): compiled only into the A/B library (make abl, -DVO_ABLATIONS).
+#ifdef VO_ABLATIONS
 #include <algorithm>
 #include <type_traits>
 
@@ -444,3 +446,4 @@ int vo_pair3_try(const void* x, const void* w1, const float* b1, const void* w2,
   if (K == 7) return pair3_launch<32, 8, 7, true, 1>(a, B, st);
   return pair3_launch<32, 7, 11, true, 1>(a, B, st);
 }
+#endif  // VO_ABLATIONS

@@ -20,6 +20,8 @@
 // tile's window DMA is issued before the last epilogue's stores.  Biases enter as the C operand of
 // each conv's first MFMA; leaky ReLU in packed fp32.  All weights stay resident in LDS.
 
+// Measured-and-dropped (round 3): compiled only into the A/B library (make abl, -DVO_ABLATIONS).
+#ifdef VO_ABLATIONS
 #include <algorithm>
 #include <type_traits>
 
@@ -331,3 +333,4 @@ int vo_pair_wave_try(const void* x, const void* w1, const float* b1, const void*
   if (dil == 3) return wave_launch<1, 11, 3, 10>(a, B, st);
   return wave_launch<1, 11, 5, 10>(a, B, st);
 }
+#endif  // VO_ABLATIONS

@@ -332,10 +332,14 @@ def bucket_embed(x, target, bins, table):
     tgt = _contig(target.float(), "target")
     if tgt.shape != (B, T):
         raise ValueError(f"bucket_embed: target {tuple(tgt.shape)} vs x {tuple(x.shape)}")
+    if table.dim() != 2 or table.shape[1] != D or table.dtype != torch.float32 or not table.is_contiguous():
+        raise ValueError(f"bucket_embed: table must be a contiguous fp32 (n, {D}) tensor, got "
+                         f"{tuple(table.shape)} {table.dtype}")
     out = torch.empty_like(x)
     idx = torch.empty((B, T), dtype=torch.int32, device=x.device)
     _lib.check(_lib.lib().vo_bucket_embed(_ptr(x), vo_dtype(x), _ptr(tgt), _ptr(bins), bins.numel(), _ptr(table),
-                                          B * T, D, _ptr(out), _ptr(idx), _stream(x)), "vo_bucket_embed")
+                                          table.shape[0], B * T, D, _ptr(out), _ptr(idx), _stream(x)),
+               "vo_bucket_embed")
     return out, idx
 
 

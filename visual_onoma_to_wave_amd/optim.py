@@ -10,10 +10,15 @@ memory (graph-capturable, no host synchronisation).  The state layout is torch's
 
 Semantics: torch's single-tensor Adam / AdamW (amsgrad and maximize off).  One step counter per
 param group (every ``state[p]["step"]`` is that group's tensor): parameters are updated together,
-as in the training steps here.  fp32 parameters, gradients and moments on the GPU.
+as in the training steps here -- ``load_state_dict`` refuses a group whose per-parameter steps
+differ, and ``step`` warns when a parameter first gets a gradient after the group's first step.
+A capturable group's device-tensor learning rate survives ``load_state_dict`` (the loaded value is
+copied into it), and capturing a step with a float learning rate raises.  fp32 parameters,
+gradients and moments on the GPU.
 """
 
 import ctypes
+import warnings
 
 import torch
 from torch.autograd.graph import increment_version
@@ -50,6 +55,11 @@ class FusedAdam(torch.optim.Optimizer):
         lr = group["lr"]
         if torch.is_tensor(lr):
             return lr if lr.dtype == torch.float32 else lr.float()
+        if torch.cuda.is_current_stream_capturing():
+            # a float lr would be baked into the graph as a constant: schedule changes between replays
+            # would be silently ignored
+            raise RuntimeError("FusedAdam: capturing a step needs device-tensor learning rates "
+                               "(construct with capturable=True and lr=torch.tensor(...))")
         t = group.get("_vo_lr")
         if t is None:
             t = group["_vo_lr"] = torch.empty((), dtype=torch.float32, device=group["params"][0].device)
@@ -57,7 +67,22 @@ class FusedAdam(torch.optim.Optimizer):
         return t
 
     def load_state_dict(self, state_dict):
+        # every per-parameter step of a group must agree: one step tensor per group drives the bias
+        # correction (a parameter loaded with a smaller step would get the wrong correction)
+        for i, g in enumerate(state_dict["param_groups"]):
+            steps = {float(state_dict["state"][k]["step"]) for k in g["params"]
+                     if k in state_dict["state"] and "step" in state_dict["state"][k]}
+            if len(steps) > 1:
+                raise ValueError(f"FusedAdam: param group {i} has unequal per-parameter steps {sorted(steps)[:4]}; "
+                                 "one step count per group is supported")
+        # a device-tensor learning rate (capturable groups) is the tensor a captured graph reads: keep
+        # that tensor and copy the loaded value into it (torch's update_group puts a Python float there)
+        lr_tensors = [g["lr"] if torch.is_tensor(g["lr"]) else None for g in self.param_groups]
         super().load_state_dict(state_dict)
+        for group, lt in zip(self.param_groups, lr_tensors):
+            if lt is not None:
+                lt.fill_(float(group["lr"]))
+                group["lr"] = lt
         for group in self.param_groups:
             group.pop("_vo_step", None)
             group.pop("_vo_lr", None)
@@ -72,8 +97,8 @@ class FusedAdam(torch.optim.Optimizer):
     def state_dict(self):
         sd = super().state_dict()
         for g in sd["param_groups"]:
-            g.pop("_vo_step", None)
-            g.pop("_vo_lr", None)
+            for k in ("_vo_step", "_vo_lr", "_vo_started", "_vo_warned"):
+                g.pop(k, None)
         return sd
 
     def _table(self, ps, gs, ms, vs):
@@ -111,6 +136,11 @@ class FusedAdam(torch.optim.Optimizer):
                     raise TypeError("FusedAdam: contiguous fp32 gradients only")
                 st = self.state[p]
                 if "exp_avg" not in st:
+                    if group.get("_vo_started") and not group.get("_vo_warned"):
+                        warnings.warn("FusedAdam: a parameter got its first gradient after the group's first step; "
+                                      "it shares the group's step count (torch's Adam would count its own steps "
+                                      "from 1), so its bias correction differs from torch's", RuntimeWarning)
+                        group["_vo_warned"] = True
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] = step_t
@@ -120,6 +150,7 @@ class FusedAdam(torch.optim.Optimizer):
                 vs.append(st["exp_avg_sq"])
             if not ps:
                 continue
+            group["_vo_started"] = True
             b1, b2 = group["betas"]
             lr_t = self._group_lr(group)
             tp, tg, tm, tv, tn = self._table(ps, gs, ms, vs)[1]

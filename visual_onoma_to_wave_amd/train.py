@@ -257,17 +257,24 @@ _GRAPH_GROUPS = {}
 
 def graph_group(group, device):
     """A process group over the same ranks as ``group`` reserved for collectives captured in HIP
-    graphs (created once per (group, device), on every rank at the same point: the first capture).
-    With the default group bound to a device (``init_process_group(..., device_id=dev)``) the new
-    RCCL communicator is split off eagerly, so no communicator is created inside a capture.
-    gloo groups are returned unchanged (gloo collectives cannot be captured)."""
+    graphs (created once per (group, device), on every rank at the same point: the first capture,
+    outside the capture itself).  The group is always created with ``device_id``: with the default
+    group bound to a device (``init_process_group(..., device_id=dev)``) its RCCL communicator is
+    split off eagerly, and without that binding torch connects the new communicator eagerly
+    (``eager_connect_single_device``) -- either way no communicator is created inside a capture,
+    and no eager collective ever runs on this group.  gloo groups are returned unchanged (gloo
+    collectives cannot be captured)."""
     if dist.get_backend(group) != "nccl":
         return group
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
     key = (id(group), str(device))
     if key not in _GRAPH_GROUPS:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("graph_group: create the graph collectives' group before the capture begins")
         ranks = None if group is None else dist.get_process_group_ranks(group)
-        dev = device if getattr(dist.distributed_c10d._get_default_group(), "bound_device_id", None) else None
-        _GRAPH_GROUPS[key] = dist.new_group(ranks=ranks, backend="nccl", device_id=dev,
+        _GRAPH_GROUPS[key] = dist.new_group(ranks=ranks, backend="nccl", device_id=device,
                                             group_desc="vo_graph_collectives")
     return _GRAPH_GROUPS[key]
 
