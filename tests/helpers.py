@@ -70,11 +70,11 @@ def t(x):
     return torch.from_numpy(np.array(x))
 
 
-def bf16_bar(ref_fp32, ref_bf16, floor=1e-2, slack=1.1):
+def bf16_bar(ref_fp32, ref_bf16, floor=1e-2, slack=1.0):
     """Tolerance of a bf16 HIP result: the survey's rel-L2 1e-2, or -- where the reference's own
     bf16 autocast on the same weights and input drifts further from its fp32 result (the
     deterministic test weights of weights.py drive the vocoder harder than 1e-2 allows any bf16
-    implementation) -- that drift times ``slack``: no worse than the reference run in bf16."""
+    implementation) -- that drift, no slack: no worse than the reference run in bf16."""
     return max(floor, slack * rel_l2(ref_bf16, ref_fp32))
 
 

@@ -4,7 +4,7 @@ by running the reference itself (tests/golden/make_goldens.py ``long_goldens``).
 
 Tolerances (relative L2): bf16 kernels <= 1e-2, except where the reference's own
 bf16 autocast on the same weights and input drifts further (the Generator on the deterministic
-test weights: 1.3e-2) -- there the bar is that drift x 1.1 (helpers.bf16_bar), computed in the
+test weights: 1.3e-2) -- there the bar is that drift, no slack (helpers.bf16_bar), computed in the
 test; fp32 mode <= 1e-4; integer results (mel_len, d_rounded, masks) bit-exact.
 """
 

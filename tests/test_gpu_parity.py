@@ -240,8 +240,8 @@ def test_upsamplers(gen, dt, tol):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_generator(gen, dt):
-    """fp32 <= 1e-4; bf16 held to helpers.bf16_bar: max(1e-2, 1.1 x the reference's own bf16
-    autocast drift on these weights, 1.3e-2)."""
+    """fp32 <= 1e-4; bf16 held to helpers.bf16_bar: max(1e-2, the reference's own bf16 autocast drift
+    on these weights, 1.31e-2)."""
     import numpy as _np
     from helpers import bf16_bar, oracle_generator_bf16
     from oracle import vocoder as V
@@ -257,17 +257,17 @@ def test_generator(gen, dt):
     assert rel_l2(wav.cpu(), g["wav"]) < tol
 
 
-@pytest.mark.parametrize("seed", [0, 1])
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
 def test_generator_bf16_reference_init(device, seed):
     """bf16 Generator on weights drawn the way the reference itself draws them: Generator(h) under
     weight_norm with PyTorch's default conv init (scripts/hifigan/models.py:10-13,58,94,146-147 --
     init_weights writes ``m.weight``, which the weight-norm hook recomputes from v and g at every
     forward, so v keeps the default init and g = ||v||), a C3-style mel clamp(N(-5, 2)) at
-    B = 2 x 96 frames, against the fp32 oracle on the CPU.  Bar: the survey's fixed rel-L2 1e-2
-    (seed 0 is the survey's measured case: the reference's own bf16 autocast drifts
-    3.4e-3, this path 2.4e-3).  Where the reference's own bf16 autocast already drifts past 1e-2 on
-    the same weights and mel (seed 1: 1.36e-2; this path 1.10e-2), this path must not drift further
-    than it -- no slack factor.  Per-stage local errors: tools/probes/gen_err_probe.py."""
+    B = 2 x 96 frames, against the fp32 oracle on the CPU.  Bar: no worse than the reference's own
+    bf16 arithmetic on the same weights and mel -- this path's rel-L2 <= the CPU bf16 autocast's
+    rel-L2 of the oracle Generator (the residual stream is bf16 in both: every stage input of the
+    autocast run comes out of a bf16 conv), no slack; on seed 0 (the survey's measured case) also the
+    survey's fixed 1e-2.  Per-stage local errors: tools/probes/gen_err_probe.py."""
     from visual_onoma_to_wave_amd import hifigan
     from helpers import oracle_generator_bf16
     from oracle import vocoder as V
@@ -287,9 +287,10 @@ def test_generator_bf16_reference_init(device, seed):
     assert wav.shape == ref.shape
     err = rel_l2(wav, ref)
     drift = rel_l2(oracle_generator_bf16(sd, mel, h), ref)
-    assert err < 1e-2 or err < drift, (err, drift)
+    print(f"seed {seed}: HIP bf16 rel-L2 {err:.3e}, reference bf16 autocast {drift:.3e}")
+    assert err <= drift, (err, drift)
     if seed == 0:
-        assert err < 5e-3, err
+        assert err < 1e-2, err
 
 
 # ------------------------------------------------------------------------------ kernels vs oracle
@@ -452,9 +453,9 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-# pair_cfg 0 = the shipped dispatch (C = 128, k = 7 / 11: the round-4 producer-role kernel,
-# resblock_pc.hip); 70 = the round-3 C = 128 kernel, kept as the A/B reference
-@pytest.mark.parametrize("cfg", [0, 70])
+# pair_cfg 0 = the shipped dispatch; 71 / 72 = the round-4 C = 128 candidates (producer roles,
+# resblock_pc.hip; register-streamed weights, resblock_rs.hip), other shapes fall back to the default
+@pytest.mark.parametrize("cfg", [0, 71, 72])
 @pytest.mark.parametrize("with_acc", [True, False])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
@@ -499,11 +500,12 @@ def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, with_acc, cfg):
     assert rel_l2(out.float().cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("cand", [71, 72])
 @pytest.mark.parametrize("T,k,d", [(32768, 11, 5), (32768, 7, 3), (777, 11, 1), (1, 7, 5)])
-def test_pair_c128_producer_roles_vs_round3(T, k, d):
-    """The round-4 C = 128 pair (producer roles, residual folded into the P2 accumulator init)
-    against the round-3 kernel on the same bf16 operands: the two differ only in fp32 summation
-    order before the one bf16 rounding of y."""
+def test_pair_c128_candidates_vs_shipped(T, k, d, cand):
+    """The round-4 C = 128 pair candidates (pair_cfg 71: producer roles; 72: register-streamed weights)
+    against the shipped kernel on the same bf16 operands: they differ only in fp32 summation order
+    before the one bf16 rounding of y."""
     from visual_onoma_to_wave_amd import _lib, ops
     C, B = 128, 4
     g = torch.Generator(device="cuda").manual_seed(T + 10 * k + d)
@@ -514,7 +516,7 @@ def test_pair_c128_producer_roles_vs_round3(T, k, d):
     b1 = torch.randn(C, device="cuda", generator=g) * 0.1
     b2 = torch.randn(C, device="cuda", generator=g) * 0.1
     outs = []
-    for cfg in (0, 70):
+    for cfg in (0, cand):
         o = acc.clone()
         _lib.lib().vo_tune(b"pair_cfg", cfg)
         try:

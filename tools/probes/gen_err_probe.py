@@ -2,7 +2,13 @@
 """Where the bf16 Generator's error comes from: the HIP path run stage by stage (conv_pre, each
 upsampler, each MRF, conv_post), each stage's LOCAL error = HIP stage on the HIP input against the
 fp32 oracle stage on that same input, beside the oracle's own CPU bf16-autocast local error, at the
-reference's default init (tests/test_gpu_parity.py::test_generator_bf16_reference_init_fixed_bar).
+reference's default init (tests/test_gpu_parity.py::test_generator_bf16_reference_init).
+
+Like with like (round 4): the autocast reference gets the stage input as a bf16 TENSOR (the HIP
+stage's input is bf16 in HBM).  Given an fp32 tensor, the autocast ResBlock's residual ``xt + x``
+promoted to fp32 and its residual stream stayed fp32 through the stage, while the HIP kernels (and
+the autocast reference inside a whole-Generator run, where every stage input comes out of a bf16
+conv) keep it in bf16.
 
     python tools/probes/gen_err_probe.py [seed]
 """
@@ -57,10 +63,10 @@ def main():
             x = ops.conv1d(x, wu, bu, Co=u * cout, K=2, pad=1, pre_act=ops.ACT_LRELU, pre_slope=LRELU_SLOPE,
                            transposed=dict(stride=u, pad=pad, cout=cout), out_dtype=dt, compute_dtype=dt)
             k = h["upsample_kernel_sizes"][i]
-            line(f"ups{i}", cl(x), V.upsample(sd, i, xin, k, u), auto(V.upsample, sd, i, xin, k, u))
+            line(f"ups{i}", cl(x), V.upsample(sd, i, xin, k, u), auto(V.upsample, sd, i, xin.to(dt), k, u))
             xin = cl(x)
             x = g.mrf(i, x)
-            line(f"mrf{i}", cl(x), V.mrf(sd, i, xin, h), auto(V.mrf, sd, i, xin, h))
+            line(f"mrf{i}", cl(x), V.mrf(sd, i, xin, h), auto(V.mrf, sd, i, xin.to(dt), h))
             # each ResBlock alone (local), through the same dispatch as the MRF
             nk = g.num_kernels
             for j in range(nk):
@@ -72,7 +78,7 @@ def main():
                 rk, rd = h["resblock_kernel_sizes"][j], h["resblock_dilation_sizes"][j]
                 xin16 = xin.to(dt).float()
                 line(f"  rb{j} k{rk}", cl(out), V.resblock(sd, key, xin16, rk, rd),
-                     auto(V.resblock, sd, key, xin16, rk, rd))
+                     auto(V.resblock, sd, key, xin16.to(dt), rk, rd))
         wk, bp = p["post"]
         xin = cl(x)
         wav = ops.conv_post(x, wk, bp, slope=0.01)
@@ -80,7 +86,7 @@ def main():
         def post(z):
             z = torch.nn.functional.leaky_relu(z)
             return torch.tanh(torch.nn.functional.conv1d(z, sd["conv_post.weight"], sd["conv_post.bias"], padding=3))
-        line("conv_post", wav.float().cpu().reshape(2, 1, -1), post(xin), auto(post, xin))
+        line("conv_post", wav.float().cpu().reshape(2, 1, -1), post(xin), auto(post, xin.to(dt)))
         ref = V.generator(sd, mel, h)
         print(f"end to end: HIP {rel_l2(wav.float().cpu().reshape(ref.shape), ref):.2e}   oracle bf16-autocast "
               f"{rel_l2(auto(V.generator, sd, mel, h), ref):.2e}")
