@@ -123,6 +123,10 @@ def roofline(ks, peak, label, batch=32):
                      "tflops": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12, 1),
                      "mfma_frac": round(v["flops_per_launch"] / (v["avg_ms"] * 1e-3) / 1e12 / peak, 3),
                      "hbm_gbs_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9, 1),
+                     # algorithmic bytes (read x + acc once, write y once, weights once) over the launch
+                     # time: the fraction of the HBM roofline the stage would reach at zero wasted traffic
+                     "hbm_frac_algorithmic": round(v["bytes_per_launch"] / (v["avg_ms"] * 1e-3) / 1e9
+                                                   / HBM_PEAK_GBS, 3),
                      # measured HBM bytes (committed PMC passes) over this run's launch time: the north
                      # star's "HBM roofline on the MRF" for the narrow stages
                      "hbm_frac_pmc": (round(pmc[k] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)

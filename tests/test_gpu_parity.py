@@ -453,9 +453,7 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-# pair_cfg 0 = the shipped dispatch; 71 / 72 = the round-4 C = 128 candidates (producer roles,
-# resblock_pc.hip; register-streamed weights, resblock_rs.hip), other shapes fall back to the default
-@pytest.mark.parametrize("cfg", [0, 71, 72])
+@pytest.mark.parametrize("cfg", [0])  # the shipped dispatch (A/B candidates: test_pair_c128_candidates_vs_shipped)
 @pytest.mark.parametrize("with_acc", [True, False])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),
@@ -500,13 +498,18 @@ def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, with_acc, cfg):
     assert rel_l2(out.float().cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("cand", [71, 72])
+@pytest.mark.parametrize("cand,rs", [(71, 0), (72, 0), (72, 2)])
 @pytest.mark.parametrize("T,k,d", [(32768, 11, 5), (32768, 7, 3), (777, 11, 1), (1, 7, 5)])
-def test_pair_c128_candidates_vs_shipped(T, k, d, cand):
-    """The round-4 C = 128 pair candidates (pair_cfg 71: producer roles; 72: register-streamed weights)
-    against the shipped kernel on the same bf16 operands: they differ only in fp32 summation order
-    before the one bf16 rounding of y."""
+def test_pair_c128_candidates_vs_shipped(T, k, d, cand, rs):
+    """The round-4 C = 128 pair candidates (pair_cfg 71: producer roles; 72: register-streamed weights,
+    rs_cfg 2: its two-waves-per-SIMD variant).  Measured slower and built only into the A/B library
+    (``make abl``; run with VO_LIB_PATH=visual_onoma_to_wave_amd/lib/libvonoma_abl.so).  Against the
+    shipped kernel on the same bf16 operands: they differ only in fp32 summation order before the one
+    bf16 rounding of y."""
     from visual_onoma_to_wave_amd import _lib, ops
+    if _lib.lib().vo_tune(b"pc_cfg", 8) != 0:
+        pytest.skip("A/B candidates: ablation build only (make abl)")
+    _lib.lib().vo_tune(b"pc_cfg", 0)
     C, B = 128, 4
     g = torch.Generator(device="cuda").manual_seed(T + 10 * k + d)
     x = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
@@ -519,10 +522,12 @@ def test_pair_c128_candidates_vs_shipped(T, k, d, cand):
     for cfg in (0, cand):
         o = acc.clone()
         _lib.lib().vo_tune(b"pair_cfg", cfg)
+        _lib.lib().vo_tune(b"rs_cfg", rs if cfg else 0)
         try:
             ops.resblock_pair(x, p1, b1, p2, b2, k, d, 0.1, out=o, out_scale=1.0 / 3, acc=o)
             torch.cuda.synchronize()
         finally:
             _lib.lib().vo_tune(b"pair_cfg", 0)
+            _lib.lib().vo_tune(b"rs_cfg", 0)
         outs.append(o.float())
     assert rel_l2(outs[0].cpu(), outs[1].cpu()) < 2e-3

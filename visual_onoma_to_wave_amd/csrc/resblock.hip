@@ -642,8 +642,9 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
+#ifdef VO_ABLATIONS  // measured-and-dropped variants (A/B builds only: make abl)
   // round-4 C = 128 candidates (k = 7 / 11): pair_cfg 71 = producer roles (resblock_pc.hip),
-  // 72 = register-streamed weights, one wave per SIMD (resblock_rs.hip)
+  // 72 = register-streamed weights, one wave per SIMD (resblock_rs.hip; rs_cfg 2: two per SIMD)
   if (C == 128 && cfg == 71) {
     int handled = 0;
     const int rc = vo_pair_pc_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, st, &handled);
@@ -655,7 +656,6 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
                                   vo_tune_get("rs_cfg"), st, &handled);
     if (handled) return rc;
   }
-#ifdef VO_ABLATIONS  // measured-and-dropped variants (A/B builds only: make abl)
   if (cfg == 50) {  // round 3: C = 32 with wave-private frames (resblock5.hip)
     int handled = 0;
     const int rc = vo_pair_wave_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);

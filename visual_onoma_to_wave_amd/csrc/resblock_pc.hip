@@ -25,6 +25,7 @@
 //    residual registers live through P2.
 // The fold rounds differently from (c2 + b2 + x) * s + acc_in in the last fp32 bits only.
 
+#ifdef VO_ABLATIONS  // round-4 C = 128 candidate (producer roles): measured slower, A/B builds only
 #include <type_traits>
 
 #include "mrf_common.h"
@@ -535,3 +536,5 @@ extern "C" int vo_pc_stamps(unsigned long long* host, int n) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pc_stamp), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
+
+#endif  // VO_ABLATIONS

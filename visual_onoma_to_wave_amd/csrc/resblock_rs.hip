@@ -23,6 +23,7 @@
 //    (acc = b2 + x), the MRF accumulator rows two slices before P2 ends and added in the y
 //    epilogue: y = acc * out_scale + acc_in.
 
+#ifdef VO_ABLATIONS  // round-4 C = 128 candidate (register-streamed weights): measured slower, A/B builds only
 #include <type_traits>
 
 #include "mrf_common.h"
@@ -410,3 +411,5 @@ int vo_pair_rs_try(const void* x, const void* w1, const float* b1, const void* w
   if (K == 7) return acc ? rs_launch<7, true, 12, 1, 5>(a, B, st) : rs_launch<7, false, 12, 1, 5>(a, B, st);
   return acc ? rs_launch<11, true, 12, 1, 5>(a, B, st) : rs_launch<11, false, 12, 1, 5>(a, B, st);
 }
+
+#endif  // VO_ABLATIONS
