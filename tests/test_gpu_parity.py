@@ -406,9 +406,11 @@ def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
 
 
 @pytest.mark.parametrize("C,T", [(32, 1000), (64, 777), (128, 300), (32, 5), (64, 1), (128, 13), (128, 232),
-                                 (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768)])
+                                 (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768),
+                                 # register-resident frames: 104 (C = 32) / 72 (C = 64) output rows per tile
+                                 (32, 104), (32, 105), (32, 24), (64, 72), (64, 73), (64, 16), (64, 72 * 5 - 1)])
 @pytest.mark.parametrize("with_acc", [True, False])
-@pytest.mark.parametrize("cfg", [0])  # the shipped kernels (the A/B variants live in the VO_ABLATIONS build)
+@pytest.mark.parametrize("cfg", [0, 80, 81, 82, 83])  # shipped kernels; 80-83 = register-resident frames (C = 32 / 64)
 def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     """vo_resblock3 (a whole k = 3 ResBlock, dilations 1/3/5, in one launch) against the torch fp32
     ResBlock at tile edges (frame 232 / 488 valid rows), T = 1, and multi-tile persistent runs;

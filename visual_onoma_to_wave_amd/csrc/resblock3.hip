@@ -570,6 +570,9 @@ using namespace vo;
 int vo_rb3_wave_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
                     const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
                     float out_scale, int cfg, hipStream_t st, int* handled);  // resblock5.hip
+int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                  const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
+                  float out_scale, int cfg, hipStream_t st, int* handled);  // resblock_rr.hip
 
 extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
                             const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C,
@@ -600,6 +603,11 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
+  if (cfg >= 80 && cfg <= 83) {  // round 4: register-resident frames (resblock_rr.hip), C = 32 / 64, dilations (1, 3, 5)
+    int handled = 0;
+    const int rc = vo_rb3_rr_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, cfg, st, &handled);
+    if (handled) return rc;
+  }
 #ifdef VO_ABLATIONS  // measured-and-dropped variants (A/B builds only: make abl)
   if (C == 32 && (cfg == 30 || cfg == 31)) {  // round 3: wave-private frames (resblock5.hip)
     int handled = 0;
