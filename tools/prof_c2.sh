@@ -12,5 +12,28 @@ tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print("total ms", tot / 1e6)
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
     print(f'{float(r["TotalDurationNs"])/1e6:8.2f} ms {int(r["Calls"]):6d} calls {float(r["AverageNs"])/1e3:8.1f} us  {r["Name"][:150]}')
+
+
+def cls(n):  # kernel class of the C2 breakdown
+    if "layernorm" in n or "ln_" in n:
+        return "LayerNorm (+ residual, pad-row zeroing)"
+    if "attn" in n or "attention" in n:
+        return "attention"
+    if "conv_splitk_reduce" in n or "conv1d_kernel<float" in n:
+        return "fp32 short-sequence convs (encoder / predictors, T_src = 12; split reduction)"
+    if "conv1d_kernel<unsigned short" in n:
+        return "bf16 convs over T_mel (decoder FFN / qkv / fc, PostNet, mel_linear)"
+    return "glue (embeddings, VFE, length regulator, heads, masks, casts)"
+
+
+agg = {}
+for r in rows:
+    c = cls(r["Name"])
+    a = agg.setdefault(c, [0.0, 0])
+    a[0] += float(r["TotalDurationNs"])
+    a[1] += int(r["Calls"])
+print("\nper kernel class (trace totals over all bench launches; share of kernel time):")
+for c, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+    print(f"{t / tot * 100:6.1f} %  {t / 1e6:8.2f} ms  {n:6d} launches  {c}")
 PY
 rm -f $OUT/run_kernel_trace.csv

@@ -333,16 +333,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <int O, int NB, int NK, int n>
 __device__ __forceinline__ u32x4 shifted_w(const u32x4 (&in)[NB][NK], int s) {
   constexpr int m = n + O;
-  constexpr int q = m >= NB ? 1 : (m < 0 ? -1 : 0);
+  constexpr int q = m >= 0 ? m / NB : -((-m + NB - 1) / NB);  // floor(m / NB): lanes to move
   constexpr int r = m - q * NB;
-  static_assert(r >= 0 && r < NB, "|shift| <= NB");
+  static_assert(q >= -2 && q <= 2, "|shift| <= 2 NB");
   if constexpr (q == 0) {
     return in[r][s];
   } else {
     constexpr int ctrl = q > 0 ? 0x130 : 0x138;  // wave_shl:1 (lane i reads i + 1) / wave_shr:1
     u32x4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (unsigned)__builtin_amdgcn_mov_dpp((int)in[r][s][i], ctrl, 0xf, 0xf, true);
+    for (int i = 0; i < 4; ++i) {
+      int t = __builtin_amdgcn_mov_dpp((int)in[r][s][i], ctrl, 0xf, 0xf, true);
+      if constexpr (q == 2 || q == -2) t = __builtin_amdgcn_mov_dpp(t, ctrl, 0xf, 0xf, true);
+      v[i] = (unsigned)t;
+    }
     return v;
   }
 }
@@ -351,7 +355,7 @@ __device__ __forceinline__ int rrw_perm(int cb, int m) {  // D row m of co-block
   return 32 * cb + 16 * (m >> 4) + 8 * ((m >> 2) & 1) + (m & 3) + 4 * ((m >> 3) & 1);
 }
 
-template <int C, int NB, int NWV, bool PF>
+template <int C, int NB, int NWV, bool PF, bool RM>
 __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
   constexpr int NK = C / 16;   // 16-channel K-steps
   constexpr int NCB = C / 32;  // 32-channel output blocks
@@ -361,7 +365,7 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
   constexpr int NFR = 6 * 3 * NK * NCB;  // weight fragments; then 6 * NCB bias fragments
   constexpr int NST = 3 * NK;
   static_assert(C == 32 || C == 64, "narrow stages");
-  static_assert(NB >= 5, "dilation 5 shifts by at most one lane");
+  static_assert(2 * NB >= 5, "dilation 5 shifts by at most two lanes");
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   u32x4* wfr = reinterpret_cast<u32x4*>(smem_raw);  // [NFR + 6 NCB][64 lanes]
@@ -413,6 +417,18 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
   };
   const u32x4 ones = u32x4{lh == 0 ? 0x3f803f80u : 0u, 0u, 0u, 0u};  // B: 1.0 in K rows 0 and 1
   const bf16x8 onesv = __builtin_bit_cast(bf16x8, ones);
+  // RM: the residual x_s enters a c2 conv's accumulator through two more MFMAs per (block, co-block)
+  // with permuted-identity A fragments (K-step 2 cb + v, v = 0 / 1; the same for every cb): exact
+  // (x * 1.0 summed in fp32), and the epilogue needs no bf16 unpack and add (2 VALU per value)
+  bf16x8 idf[2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int m = lane & 31;
+    const int um = m >> 4, hm = (m >> 2) & 1, jm = (m & 3) + 4 * ((m >> 3) & 1);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (um == v && lh == hm) w[jm >> 1] = (jm & 1) ? 0x3f800000u : 0x00003f80u;
+    idf[v] = __builtin_bit_cast(bf16x8, u32x4{w[0], w[1], w[2], w[3]});
+  }
 
   u32x4 xn[PF ? NB : 1][NK];
   if constexpr (PF) load_rows(a.x, tile, xn);
@@ -458,6 +474,16 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
           acc[n][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, abias[cb]), onesv, zero, 0, 0, 0);
+      if constexpr (RM && (cv & 1)) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+              acc[n][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(idf[v], __builtin_bit_cast(bf16x8, xb[n][2 * cb + v]),
+                                                                  acc[n][cb], 0, 0, 0);
+      }
       auto tap = [&](auto kc, auto jc) {
         constexpr int k = decltype(kc)::value;
         constexpr int j0 = decltype(jc)::value;
@@ -516,11 +542,17 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
                 in[n][s] = u32x4{w[0], w[1], w[2], w[3]};
               } else {
                 float xf[8];
-                unpack8(opaque(xb[n][s]), xf);
+                if constexpr (RM) {
+#pragma unroll
+                  for (int e = 0; e < 8; ++e) xf[e] = 0.f;
+                } else {
+                  unpack8(opaque(xb[n][s]), xf);
+                }
                 uint32_t w[4], l[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                  const float z0 = av[8 * u + 2 * e] + xf[2 * e], z1 = av[8 * u + 2 * e + 1] + xf[2 * e + 1];
+                  const float z0 = RM ? av[8 * u + 2 * e] : av[8 * u + 2 * e] + xf[2 * e];
+                  const float z1 = RM ? av[8 * u + 2 * e + 1] : av[8 * u + 2 * e + 1] + xf[2 * e + 1];
                   w[e] = pk_bf16(z0, z1);
                   l[e] = pk_bf16(lrelu_max(z0, slope), lrelu_max(z1, slope));
                   if constexpr (EDGE) l[e] &= km;
@@ -563,13 +595,18 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
             const int s = 2 * cb + u;
             const f32x16 av = acc[n][cb];
             float xf[8], af8[8];
-            unpack8(opaque(xb[n][s]), xf);
+            if constexpr (RM) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) xf[e] = 0.f;
+            } else {
+              unpack8(opaque(xb[n][s]), xf);
+            }
             if constexpr (ACC) unpack8(ain[n][s], af8);
             uint32_t w[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float z0 = (av[8 * u + 2 * e] + xf[2 * e]) * a.out_scale;
-              float z1 = (av[8 * u + 2 * e + 1] + xf[2 * e + 1]) * a.out_scale;
+              float z0 = (RM ? av[8 * u + 2 * e] : av[8 * u + 2 * e] + xf[2 * e]) * a.out_scale;
+              float z1 = (RM ? av[8 * u + 2 * e + 1] : av[8 * u + 2 * e + 1] + xf[2 * e + 1]) * a.out_scale;
               if constexpr (ACC) {
                 z0 += af8[2 * e];
                 z1 += af8[2 * e + 1];
@@ -587,14 +624,14 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3w_kernel(RrArgs a) {
   }
 }
 
-template <int C, int NB, int NWV, bool PF>
+template <int C, int NB, int NWV, bool PF, bool RM = true>
 static int rr3w_launch(RrArgs a, int B, hipStream_t st) {
   constexpr int OR = 32 * NB - 2 * RR_HALO;
   constexpr size_t lds = (size_t)(6 * 3 * (C / 16) * (C / 32) + 6 * (C / 32)) * 1024;
   static_assert(lds <= 160 * 1024, "LDS");
   a.tiles_per_b = (a.T + OR - 1) / OR;
   a.ntiles = a.tiles_per_b * B;
-  auto kern = mrf_rr3w_kernel<C, NB, NWV, PF>;
+  auto kern = mrf_rr3w_kernel<C, NB, NWV, PF, RM>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -647,13 +684,13 @@ int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, 
   a.T = T; a.slope = slope; a.out_scale = out_scale;
   *handled = 1;
   if (C == 32) {
-    if (cfg == 82) return rr3w_launch<32, 5, 8, false>(a, B, st);
-    if (cfg == 83) return rr3w_launch<32, 10, 4, false>(a, B, st);
+    if (cfg == 82) return rr3w_launch<32, 4, 8, false>(a, B, st);
+    if (cfg == 83) return rr3w_launch<32, 8, 4, true>(a, B, st);
     if (cfg == 81) return rr3_launch<32, 8, 8, false>(a, B, st);
     return rr3_launch<32, 12, 4, true>(a, B, st);
   }
-  if (cfg == 82) return rr3w_launch<64, 5, 4, false>(a, B, st);
-  if (cfg == 83) return rr3w_launch<64, 5, 4, true>(a, B, st);
+  if (cfg == 82) return rr3w_launch<64, 4, 4, false>(a, B, st);
+  if (cfg == 83) return rr3w_launch<64, 4, 4, true>(a, B, st);
   if (cfg == 81) return rr3_launch<64, 6, 4, true>(a, B, st);
   return rr3_launch<64, 6, 4, false>(a, B, st);
 }
