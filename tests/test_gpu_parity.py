@@ -410,7 +410,9 @@ def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
                                  # register-resident frames: 104 (C = 32) / 72 (C = 64) output rows per tile
                                  (32, 104), (32, 105), (32, 24), (64, 72), (64, 73), (64, 16), (64, 72 * 5 - 1)])
 @pytest.mark.parametrize("with_acc", [True, False])
-@pytest.mark.parametrize("cfg", [0, 80, 81, 82, 83])  # shipped kernels; 80-83 = register-resident frames (C = 32 / 64)
+# cfg 0: the shipped dispatch (C = 32: register-resident frames); 80: any rb3_cfg != 0 keeps the LDS-frame
+# kernel (the A/B variants 80-87 of resblock_rr.hip are in the VO_ABLATIONS library)
+@pytest.mark.parametrize("cfg", [0, 80])
 def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     """vo_resblock3 (a whole k = 3 ResBlock, dilations 1/3/5, in one launch) against the torch fp32
     ResBlock at tile edges (frame 232 / 488 valid rows), T = 1, and multi-tile persistent runs;
@@ -455,7 +457,8 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-@pytest.mark.parametrize("cfg", [0])  # the shipped dispatch (A/B candidates: test_pair_c128_candidates_vs_shipped)
+# cfg 0: the shipped dispatch (C = 32 at dilation 1: register-resident frames); 93: the LDS-tile kernels
+@pytest.mark.parametrize("cfg", [0, 93])
 @pytest.mark.parametrize("with_acc", [True, False])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),

@@ -662,6 +662,232 @@ static int rr3_launch(RrArgs a, int B, hipStream_t st) {
   VO_RETURN_LAUNCH();
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same formulation for a k = 7 / 11 ResBlock iteration (vo_resblock_pair):
+//   y = (x + c2(lrelu(c1_D(lrelu x)))) * out_scale (+ acc)
+// c1 (dilation D) and c2 (dilation 1) run over the whole 16 NB-row frame; the valid rows shrink by
+// the halo (K - 1) / 2 * (D + 1) per side.  Tap shifts of up to 15 lanes are one DPP row_shl /
+// row_shr per dword (lane-major frames).  Both convs' weights live in LDS (C = 32: 2 K KiB).  x is
+// read twice: the frame at the start (its leaky ReLU is the c1 input) and the output rows again for
+// the residual at the end (L2 / MALL hits: the frame was fetched one tile earlier).
+struct RrpArgs {
+  const bf16_t* x;
+  const bf16_t* w[2];
+  const float* bias[2];
+  bf16_t* y;
+  const bf16_t* acc;
+  int T, tiles_per_b, ntiles;
+  float slope, out_scale;
+};
+
+template <int C, int K, int D, int NB, int NWV>
+__global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
+  constexpr int NS = C / 32, NCB = C / 16, NT = NWV * 64, F = 16 * NB;
+  constexpr int HK = (K - 1) / 2;
+  constexpr int HALO = HK * (D + 1);
+  constexpr int OR = F - 2 * HALO;
+  constexpr int NFR = 2 * K * NS * NCB;
+  constexpr int NST = K * NS;  // steps per conv
+  static_assert(OR > 0 && HK * D < 16 * NB, "frame too small for the halo");
+  static_assert((2 * NST) % 2 == 0, "fragment parity repeats per tile");
+
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  u32x4* wfr = reinterpret_cast<u32x4*>(smem_raw);
+  float* sb = reinterpret_cast<float*>(smem_raw + NFR * 1024);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lq = lane >> 4;
+  const int T = a.T;
+  const float slope = a.slope;
+
+  for (int i = tid; i < NFR * 64; i += NT) {
+    const int f = i >> 6, l = i & 63;
+    const int b = f % NCB, s = (f / NCB) % NS, k = (f / (NCB * NS)) % K, cv = f / (NCB * NS * K);
+    const int m = l & 15;
+    const int co = 32 * (b >> 1) + 8 * (m >> 2) + 4 * (b & 1) + (m & 3);
+    wfr[i] = *reinterpret_cast<const u32x4*>(a.w[cv] + k * C * C + co * C + 32 * s + 8 * (l >> 4));
+  }
+  for (int i = tid; i < 2 * C; i += NT) sb[i] = a.bias[i / C][i % C];
+  __syncthreads();
+
+  const int gw = blockIdx.x * NWV + wave, nw = gridDim.x * NWV;
+  int tile = (int)(((int64_t)gw * a.ntiles) / nw);
+  const int tile_end = (int)(((int64_t)(gw + 1) * a.ntiles) / nw);
+  if (tile >= tile_end) return;
+
+  const int lane_off = 2 * (lr * NB * C + 8 * lq);
+  auto utt_rsrc = [&](const bf16_t* base, int b) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)b * T * C), (short)0, T * C * 2, 0x00020000);
+  };
+  auto load_rows = [&](const bf16_t* base, int tl, u32x4 (&fr)[NB][NS]) {
+    const int b = tl / a.tiles_per_b;
+    const int w0 = (tl - b * a.tiles_per_b) * OR - HALO;
+    const __amdgpu_buffer_rsrc_t rs = utt_rsrc(base, b);
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        fr[n][s] = __builtin_amdgcn_raw_buffer_load_b128(rs, (w0 + n) * C * 2 + lane_off, 64 * s, 0);
+  };
+  // tap of step j of a conv: the centre tap first (no shift), then 0 .. K - 1 without it
+  auto tap_of = [](int j) constexpr { return j == 0 ? (K - 1) / 2 : (j <= (K - 1) / 2 ? j - 1 : j); };
+
+  u32x4 af[2][NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) af[0][cb] = wfr[((HK * NS) * NCB + cb) * 64 + lane];  // (c1, centre, 0)
+
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / a.tiles_per_b;
+    const int t0 = (tile - b * a.tiles_per_b) * OR;
+    const int w0 = t0 - HALO;
+    const bool interior = w0 >= 0 && w0 + F <= T;
+    u32x4 in[NB][NS];
+    load_rows(a.x, tile, in);
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) in[n][s] = lrelu8_pk(in[n][s], slope);
+
+    int fl = lane;
+    asm volatile("" : "+v"(fl));
+    const u32x4* wl = wfr + fl;
+    f32x4 acc[NB][NCB];
+
+    auto conv = [&](auto cvc) {
+      constexpr int cv = decltype(cvc)::value;
+      constexpr int d = cv == 0 ? D : 1;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + cv * C + 32 * (cb >> 1) + 8 * lq + 4 * (cb & 1));
+#pragma unroll
+        for (int n = 0; n < NB; ++n) acc[n][cb] = bv;
+      }
+      auto step = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int k = tap_of(j);
+        constexpr int O = (k - HK) * d;
+        auto ks = [&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          constexpr int g = cv * NST + j * NS + s;
+          constexpr int fn = s + 1 < NS ? (((cv * K + k) * NS + s + 1) * NCB)
+                                        : (j + 1 < K ? (((cv * K + tap_of(j + 1)) * NS) * NCB)
+                                                     : ((((cv + 1) % 2 * K + HK) * NS) * NCB));
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) af[(g + 1) & 1][cb] = wl[(fn + cb) * 64];
+          __builtin_amdgcn_sched_barrier(0);
+          auto blk = [&](auto nc) {
+            constexpr int n = decltype(nc)::value;
+            const bf16x8 bv = __builtin_bit_cast(bf16x8, shifted<O, NB, NS, n>(in, s));
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+              acc[n][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[g & 1][cb]), bv,
+                                                                  acc[n][cb], 0, 0, 0);
+          };
+          static_for<NB>(blk);
+        };
+        static_for<NS>(ks);
+      };
+      static_for<K>(step);
+    };
+    conv(std::integral_constant<int, 0>{});
+    // T1 = lrelu(c1 + b1), zero outside [0, T) (c2's padding), over the c1 input
+    auto epi1 = [&](auto edge) {
+      constexpr bool EDGE = decltype(edge)::value;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        uint32_t km = 0xffffffffu;
+        if constexpr (EDGE) {
+          const int pos = w0 + lr * NB + n;
+          km = (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const f32x4 lo = acc[n][2 * s], hi = acc[n][2 * s + 1];
+          const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          uint32_t w[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w[e] = pk_bf16(lrelu_max(v[2 * e], slope), lrelu_max(v[2 * e + 1], slope));
+            if constexpr (EDGE) w[e] &= km;
+          }
+          in[n][s] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    };
+    if (interior)
+      epi1(std::false_type{});
+    else
+      epi1(std::true_type{});
+    // the residual rows and the MRF accumulator rows, in flight during c2
+    u32x4 xr[NB][NS], ain[NB][NS];
+    load_rows(a.x, tile, xr);
+    load_rows(a.acc ? a.acc : a.x, tile, ain);
+    conv(std::integral_constant<int, 1>{});
+
+    const int valid = min(OR, T - t0);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * 2, 0x00020000);
+    auto fin = [&](auto with_acc) {
+      constexpr bool ACC = decltype(with_acc)::value;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const int r = lr * NB + n - HALO;
+        const int off = r >= 0 ? r * C * 2 + 16 * lq : 0x40000000;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const f32x4 lo = acc[n][2 * s], hi = acc[n][2 * s + 1];
+          const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          float xf[8], af8[8];
+          unpack8(xr[n][s], xf);
+          if constexpr (ACC) unpack8(ain[n][s], af8);
+          uint32_t w[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float z0 = (v[2 * e] + xf[2 * e]) * a.out_scale, z1 = (v[2 * e + 1] + xf[2 * e + 1]) * a.out_scale;
+            if constexpr (ACC) {
+              z0 += af8[2 * e];
+              z1 += af8[2 * e + 1];
+            }
+            w[e] = pk_bf16(z0, z1);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[0], w[1], w[2], w[3]}, yrs, off, 64 * s, 0);
+        }
+      }
+    };
+    if (a.acc)
+      fin(std::true_type{});
+    else
+      fin(std::false_type{});
+  }
+}
+
+template <int C, int K, int D, int NB, int NWV>
+static int rrp_launch(RrpArgs a, int B, hipStream_t st) {
+  constexpr int OR = 16 * NB - 2 * ((K - 1) / 2) * (D + 1);
+  constexpr size_t lds = (size_t)2 * K * (C / 32) * (C / 16) * 1024 + 2 * C * sizeof(float);
+  static_assert(lds <= 160 * 1024, "LDS");
+  a.tiles_per_b = (a.T + OR - 1) / OR;
+  a.ntiles = a.tiles_per_b * B;
+  auto kern = mrf_rrp_kernel<C, K, D, NB, NWV>;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const int grid = (int)std::min<int64_t>(cus, (a.ntiles + NWV - 1) / NWV);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
+  VO_RETURN_LAUNCH();
+}
+
+template <int C, int K, int NB, int NWV>
+static int rrp_launch_d(RrpArgs a, int B, int dil, hipStream_t st) {
+  if (dil == 1) return rrp_launch<C, K, 1, NB, NWV>(a, B, st);
+  if (dil == 3) return rrp_launch<C, K, 3, NB, NWV>(a, B, st);
+  return rrp_launch<C, K, 5, NB, NWV>(a, B, st);
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -682,15 +908,55 @@ int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, 
   }
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
   a.T = T; a.slope = slope; a.out_scale = out_scale;
+#ifdef VO_ABLATIONS  // the other frame shapes / MFMA forms, measured
   *handled = 1;
   if (C == 32) {
+    if (cfg == 80) return rr3_launch<32, 12, 4, true>(a, B, st);
     if (cfg == 82) return rr3w_launch<32, 4, 8, false>(a, B, st);
     if (cfg == 83) return rr3w_launch<32, 8, 4, true>(a, B, st);
-    if (cfg == 81) return rr3_launch<32, 8, 8, false>(a, B, st);
-    return rr3_launch<32, 12, 4, true>(a, B, st);
+    if (cfg == 84) return rr3_launch<32, 8, 8, true>(a, B, st);
+    if (cfg == 85) return rr3_launch<32, 7, 8, true>(a, B, st);
+    if (cfg == 86) return rr3_launch<32, 6, 12, false>(a, B, st);
+    if (cfg == 87) return rr3_launch<32, 10, 8, false>(a, B, st);
+  } else {
+    if (cfg == 80) return rr3_launch<64, 6, 4, false>(a, B, st);
+    if (cfg == 81) return rr3_launch<64, 6, 4, true>(a, B, st);
+    if (cfg == 82) return rr3w_launch<64, 4, 4, false>(a, B, st);
+    if (cfg == 83) return rr3w_launch<64, 4, 4, true>(a, B, st);
   }
-  if (cfg == 82) return rr3w_launch<64, 4, 4, false>(a, B, st);
-  if (cfg == 83) return rr3w_launch<64, 4, 4, true>(a, B, st);
-  if (cfg == 81) return rr3_launch<64, 6, 4, true>(a, B, st);
-  return rr3_launch<64, 6, 4, false>(a, B, st);
+  *handled = 0;
+#endif
+  // shipped: C = 32, 16x16x32, 128-row frames (8 blocks), two waves per SIMD: 0.300 -> 0.254 ms
+  // (tools/mrf_bench.py --stages 3 --tune rb3_cfg=0,81 before the switch); C = 64 keeps the LDS-frame
+  // kernel (no register-resident variant beat it)
+  if (C != 32 || cfg != 0) return VO_OK;
+  *handled = 1;
+  return rr3_launch<32, 8, 8, false>(a, B, st);
+}
+
+// vo_resblock_pair's register-resident path (C = 32, K = 7 / 11, dilations 1 / 3 / 5)
+int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                   const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
+                   hipStream_t st, int* handled) {
+  *handled = 0;
+  if (C != 32 || !(K == 7 || K == 11) || !(dil == 1 || dil == 3 || dil == 5)) return VO_OK;
+  if ((int64_t)T * C * 2 >= (int64_t)1 << 31) return VO_OK;
+  RrpArgs a;
+  a.x = (const bf16_t*)x;
+  a.w[0] = (const bf16_t*)w1; a.bias[0] = b1; a.w[1] = (const bf16_t*)w2; a.bias[1] = b2;
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
+  a.T = T; a.slope = slope; a.out_scale = out_scale;
+#ifdef VO_ABLATIONS  // other frame shapes
+  *handled = 1;
+  if (cfg == 90) return K == 7 ? rrp_launch_d<32, 7, 12, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 12, 8>(a, B, dil, st);
+  if (cfg == 91) return K == 7 ? rrp_launch_d<32, 7, 16, 4>(a, B, dil, st) : rrp_launch_d<32, 11, 16, 4>(a, B, dil, st);
+  if (cfg == 92) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 10, 8>(a, B, dil, st);
+  if (cfg == 93) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 8, 8>(a, B, dil, st);
+  *handled = 0;
+#endif
+  // shipped for dilation 1 only (the halo, (K - 1) / 2 * (d + 1) rows per side, costs more than the
+  // frames save at d = 3 / 5): k = 7 0.197 -> 0.187 ms, k = 11 0.238 -> 0.217 (pair_cfg 93, round 4)
+  if (dil != 1 || cfg != 0) return VO_OK;
+  *handled = 1;
+  return K == 7 ? rrp_launch<32, 7, 1, 8, 8>(a, B, st) : rrp_launch<32, 11, 1, 8, 8>(a, B, st);
 }
