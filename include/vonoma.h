@@ -126,6 +126,14 @@ int vo_layernorm(const void* x, int x_dtype, const void* res, int res_dtype, con
                  const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
                  int y_dtype, void* stream);
 
+/* vo_layernorm with an fp32 y and, in the same pass, its bf16 copy y16 (round to nearest even;
+ * pad rows 0 in both).  The mixed-precision decoder keeps its residual stream (y) in fp32, as the
+ * reference's bf16 autocast does, while the next conv reads y16 -- the same bits that conv's own
+ * fp32 -> bf16 staging would make, at half the bytes.  x / res: both fp32 or both bf16. */
+int vo_layernorm_dual(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
+                      const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
+                      void* y16, void* stream);
+
 /* Backward of vo_layernorm (training, config C4): gh = dL/d(x + res) (the gradient of both x
  * and res; 0 on pad rows), dgamma / dbeta (fp32, D) summed over the unmasked rows.  x / res /
  * gh share x_dtype.  workspace: vo_layernorm_bwd_workspace_size(B, T, D) bytes (per-workgroup

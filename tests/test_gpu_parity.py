@@ -536,3 +536,43 @@ def test_pair_c128_candidates_vs_shipped(T, k, d, cand, rs):
             _lib.lib().vo_tune(b"rs_cfg", 0)
         outs.append(o.float())
     assert rel_l2(outs[0].cpu(), outs[1].cpu()) < 2e-3
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("D", [256, 512])
+def test_layernorm_dual_bf16_copy(D, dt):
+    """vo_layernorm_dual: y bit-identical to vo_layernorm's fp32 y, y16 exactly y rounded to bf16
+    (nearest even) -- what a bf16 conv's staging makes of y -- pad rows 0 in both."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(D)
+    xdt = torch.float32 if dt == "f32" else torch.bfloat16
+    B, T = 3, 77
+    x = torch.randn(B, T, D, device="cuda", generator=g).to(xdt)
+    res = torch.randn(B, T, D, device="cuda", generator=g).to(xdt)
+    gam = torch.randn(D, device="cuda", generator=g)
+    bet = torch.randn(D, device="cuda", generator=g)
+    lens = torch.tensor([77, 40, 1], dtype=torch.int32, device="cuda")
+    y1 = ops.layernorm(x, gam, bet, res=res, lens=lens, out_dtype=torch.float32)
+    y, y16 = ops.layernorm(x, gam, bet, res=res, lens=lens, out_dtype=torch.float32, with_bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y1)
+    assert torch.equal(y16, y.to(torch.bfloat16))
+    assert not y16[1, 40:].any() and not y16[2, 1:].any()
+
+
+def test_decoder_ln_bf16_copy_bit_identical(vtts):
+    """The mixed decoder with the LayerNorms' bf16 copies feeding the q/k/v and FFN w_1 convs
+    (vo_layernorm_dual) gives bit-for-bit the outputs of converting the fp32 stream in the convs."""
+    from visual_onoma_to_wave_amd.transformer.Models import Decoder
+    _prec(vtts, "mixed")
+    g = golden("vtts_tf")
+    outs = []
+    for flag in (False, True):
+        Decoder.ln_bf16_copy = flag
+        try:
+            outs.append(_run_vtts(vtts, g, True))
+        finally:
+            Decoder.ln_bf16_copy = True
+    for a, b in zip(outs[0], outs[1]):
+        if torch.is_tensor(a):
+            assert torch.equal(a, b)

@@ -92,6 +92,8 @@ _SIGNATURES = {
                                c_void_p, c_int, c_void_p]),
     "vo_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                              c_int, c_int, c_float, c_void_p, c_int, c_void_p]),
+    "vo_layernorm_dual": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                  c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "vo_layernorm_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),
     "vo_layernorm_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                  c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

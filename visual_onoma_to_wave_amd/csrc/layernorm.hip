@@ -8,12 +8,15 @@
 
 namespace vo {
 
-template <typename TX, typename TR, typename TY, int NPL>
+// DUAL (round 4): a bf16 copy of y beside it (y16) -- the next conv of the "mixed" decoder, whose
+// residual stream is fp32, reads the copy: half the bytes per re-read of its input tiles, and the same
+// bits as the conv's own fp32 -> bf16 staging (round to nearest even)
+template <typename TX, typename TR, typename TY, int NPL, bool DUAL = false>
 __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x, const TR* __restrict__ res,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         const int32_t* __restrict__ lens, int B, int T,
-                                                        float eps, TY* __restrict__ y) {
+                                                        float eps, TY* __restrict__ y, bf16_t* __restrict__ y16) {
   constexpr int D = NPL * 64;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -24,7 +27,10 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x
   if (lens && t >= lens[b]) {
     float z[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < NPL; i += 4) store4(yr + i, z);
+    for (int i = 0; i < NPL; i += 4) {
+      store4(yr + i, z);
+      if constexpr (DUAL) store4(y16 + row * D + c0 + i, z);
+    }
     return;
   }
   float v[NPL];
@@ -57,20 +63,21 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[i + e] - mean) * rstd * gamma[c0 + i + e] + beta[c0 + i + e];
     store4(yr + i, o);
+    if constexpr (DUAL) store4(y16 + row * D + c0 + i, o);
   }
 }
 
-template <typename TX, typename TR, typename TY>
+template <typename TX, typename TR, typename TY, bool DUAL = false>
 static int ln_launch(const void* x, const void* res, const float* g, const float* bt, const int32_t* lens,
-                     int B, int T, int D, float eps, void* y, hipStream_t st) {
+                     int B, int T, int D, float eps, void* y, hipStream_t st, void* y16 = nullptr) {
   const int64_t rows = (int64_t)B * T;
   dim3 grid((unsigned)((rows + 3) / 4));
   if (D == 256)
-    hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 4>), grid, dim3(256), 0, st, (const TX*)x, (const TR*)res,
-                       g, bt, lens, B, T, eps, (TY*)y);
+    hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 4, DUAL>), grid, dim3(256), 0, st, (const TX*)x,
+                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16);
   else
-    hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 8>), grid, dim3(256), 0, st, (const TX*)x, (const TR*)res,
-                       g, bt, lens, B, T, eps, (TY*)y);
+    hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 8, DUAL>), grid, dim3(256), 0, st, (const TX*)x,
+                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16);
   VO_RETURN_LAUNCH();
 }
 
@@ -258,6 +265,23 @@ extern "C" int vo_layernorm(const void* x, int x_dtype, const void* res, int res
   if (x_dtype == VO_F32 && res_dtype == VO_F32 && y_dtype == VO_BF16) VO_LN(float, float, bf16_t);
 #undef VO_LN
   vo_set_error("layernorm: unsupported dtype combination");
+  return VO_ERR_INVALID;
+}
+
+extern "C" int vo_layernorm_dual(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
+                                 const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
+                                 void* y16, void* stream) {
+  VO_CHECK_ARG(x && gamma && beta && y && y16, "layernorm_dual: null pointer");
+  VO_CHECK_ARG(D == 256 || D == 512, "layernorm_dual: D=%d unsupported (256 or 512)", D);
+  VO_CHECK_ARG(B > 0 && T > 0, "layernorm_dual: empty");
+  VO_CHECK_ARG(y16 != y && y16 != x && y16 != res, "layernorm_dual: y16 must not alias x, res or y");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!res) res_dtype = x_dtype;
+  if (x_dtype == VO_F32 && res_dtype == VO_F32)
+    return ln_launch<float, float, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16);
+  if (x_dtype == VO_BF16 && res_dtype == VO_BF16)
+    return ln_launch<bf16_t, bf16_t, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16);
+  vo_set_error("layernorm_dual: unsupported dtype combination (fp32 y, fp32 or bf16 x / res)");
   return VO_ERR_INVALID;
 }
 

@@ -81,7 +81,7 @@ extern "C" int vo_tune_get(const char* key) {
 
 static const char* const kSymbols[] = {
     "vo_last_error",     "vo_version",       "vo_num_symbols", "vo_symbol_name",   "vo_conv1d",
-    "vo_pack_weight",    "vo_layernorm",     "vo_attention",   "vo_length_regulate", "vo_lr_lengths",
+    "vo_pack_weight",    "vo_layernorm",     "vo_layernorm_dual",     "vo_attention",   "vo_length_regulate", "vo_lr_lengths",
     "vo_variance_head",  "vo_vfe_stencil",   "vo_add_pos_class", "vo_conv_post",   "vo_transpose_bct",
     "vo_stft_mel",       "vo_mask_from_lengths", "vo_tune", "vo_resblock_pair", "vo_stft_mel_ex",
     "vo_pack_grouped",   "vo_pack_grouped_blocks", "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",

@@ -164,8 +164,10 @@ def pack_conv_weight(w, dtype, g=None, row_scale=None, transposed_stride=None):
 
 # ----------------------------------------------------------------------------- layer norm
 
-def layernorm(x, gamma, beta, res=None, lens=None, out=None, out_dtype=None, eps=1e-5):
-    """y = LN(x + res) * gamma + beta, rows t >= lens[b] zeroed.  x: (B, T, D)."""
+def layernorm(x, gamma, beta, res=None, lens=None, out=None, out_dtype=None, eps=1e-5, with_bf16=False):
+    """y = LN(x + res) * gamma + beta, rows t >= lens[b] zeroed.  x: (B, T, D).  ``with_bf16``
+    (fp32 y only): returns (y, y16), y16 the bf16 copy of y written in the same pass
+    (vo_layernorm_dual) for the next conv to read."""
     if x.dim() == 2:
         x = x.unsqueeze(0)
     B, T, D = x.shape
@@ -175,6 +177,15 @@ def layernorm(x, gamma, beta, res=None, lens=None, out=None, out_dtype=None, eps
         if res.shape != x.shape:
             raise ValueError("layernorm: res shape mismatch")
     out = out if out is not None else torch.empty(x.shape, dtype=out_dtype or x.dtype, device=x.device)
+    if with_bf16:
+        if out.dtype != torch.float32:
+            raise ValueError("layernorm: with_bf16 needs an fp32 output")
+        out16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        _lib.check(_lib.lib().vo_layernorm_dual(
+            _ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res) if res is not None else vo_dtype(x),
+            _ptr(gamma), _ptr(beta), _ptr(lens), B, T, D, eps, _ptr(out), _ptr(out16), _stream(x)),
+            "vo_layernorm_dual")
+        return out, out16
     _lib.check(_lib.lib().vo_layernorm(
         _ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res) if res is not None else vo_dtype(x),
         _ptr(gamma), _ptr(beta), _ptr(lens), B, T, D, eps, _ptr(out), vo_dtype(out), _stream(x)),

@@ -24,9 +24,15 @@ class FFTBlock(HipModule):
         self.slf_attn = MultiHeadAttention(n_head, d_model, d_k, d_v, dropout=dropout)
         self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
 
-    def run(self, x, lens):
-        y = self.slf_attn.run(x, lens, mask_rows=True)
-        return self.pos_ffn.run(y, lens)
+    def run(self, x, lens, x16=None, want16=False):
+        """x16 / want16: the bf16 copy of the fp32 residual stream handed between the LayerNorms and
+        the convs that read them (mixed precision; see MultiHeadAttention.run)."""
+        dual = x.dtype == torch.float32 and self.compute_dtype == torch.bfloat16
+        if dual:
+            y, y16 = self.slf_attn.run(x, lens, mask_rows=True, x16=x16, want16=True)
+        else:
+            y, y16 = self.slf_attn.run(x, lens, mask_rows=True), None
+        return self.pos_ffn.run(y, lens, x16=y16, want16=want16 and dual)
 
     def train_run(self, x, lens):
         """Training forward (autograd; dropout active), scripts/transformer/Layers.py:21-30."""

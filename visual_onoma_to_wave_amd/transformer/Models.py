@@ -116,6 +116,8 @@ class Decoder(HipModule):
         for layer in self.layer_stack:  # bench.py's C2 roofline: the decoder FFN's k = 9 conv
             layer.pos_ffn.timer_tag = "dec_ffn_w1"
 
+    ln_bf16_copy = True  # mixed precision: LayerNorms hand the next conv a bf16 copy (bit-identical; A/B)
+
     def run(self, x, mask, lens):
         """x (B, T, D) compute dtype (consumed in place for the PE add) -> (out, mask)."""
         B, T, D = x.shape
@@ -128,8 +130,16 @@ class Decoder(HipModule):
                 x = x[:, :T].contiguous()
             mask = mask[:, :T]  # lens past T mask nothing inside [0, T): no clamp needed
         ops.add_pos_class(x, pe=pe)
-        for layer in self.layer_stack:
-            x = layer.run(x, lens)
+        # mixed precision (fp32 residual stream, bf16 convs): each LayerNorm also writes the bf16
+        # copy the next conv reads (vo_layernorm_dual), the last one only the fp32 output
+        dual = self.ln_bf16_copy and x.dtype == torch.float32 and self.compute_dtype == torch.bfloat16
+        x16 = None
+        n = len(self.layer_stack)
+        for i, layer in enumerate(self.layer_stack):
+            if dual and i + 1 < n:
+                x, x16 = layer.run(x, lens, x16=x16, want16=True)
+            else:
+                x = layer.run(x, lens, x16=x16)
         return x, mask
 
     def train_run(self, x, mask, lens):

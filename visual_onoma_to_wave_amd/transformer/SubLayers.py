@@ -47,18 +47,21 @@ class MultiHeadAttention(HipModule):
             beta=self.layer_norm.bias.detach().float().to(device).contiguous(),
         )
 
-    def run(self, x, lens, mask_rows=False):
+    def run(self, x, lens, mask_rows=False, x16=None, want16=False):
         """x (B, L, D) residual stream (the compute dtype, or fp32 under bf16 compute: the
         decoder of the "mixed" precision keeps its residual stream and LayerNorm outputs in fp32,
         as bf16 autocast of the reference does); lens (B,) int32 -> LN(fc(attn) + x) (pad rows
-        zeroed when mask_rows, as FFTBlock.masked_fill does), in x's dtype."""
+        zeroed when mask_rows, as FFTBlock.masked_fill does), in x's dtype.  x16: x's bf16 copy
+        (the q/k/v projection reads it: the same bits as converting x on the fly, half the bytes);
+        want16 (fp32 x): returns (y, y16)."""
         p = self._packed(x.device, self._build)
         D = x.shape[-1]
         cd = self.compute_dtype
-        qkv = ops.conv1d(x, p["wqkv"], p["bqkv"], Co=3 * D, K=1, compute_dtype=cd, out_dtype=cd)
+        qkv = ops.conv1d(x16 if x16 is not None else x, p["wqkv"], p["bqkv"], Co=3 * D, K=1, compute_dtype=cd,
+                         out_dtype=cd)
         att, _ = self.attention(qkv, lens, self.n_head)
         y = ops.conv1d(att, p["wfc"], p["bfc"], Co=D, K=1, compute_dtype=cd, out_dtype=x.dtype)
-        return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens if mask_rows else None)
+        return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens if mask_rows else None, with_bf16=want16)
 
     def forward(self, q, k, v, mask=None):
         """Reference signature (self-attention only, as on the path): returns (out, None)."""
@@ -91,19 +94,20 @@ class PositionwiseFeedForward(HipModule):
             beta=self.layer_norm.bias.detach().float().to(device).contiguous(),
         )
 
-    def run(self, x, lens=None):
+    def run(self, x, lens=None, x16=None, want16=False):
         """LN(w_2(relu(w_1(x))) + x) in x's dtype (the residual stream, see
-        MultiHeadAttention.run), pad rows zeroed when lens is given."""
+        MultiHeadAttention.run), pad rows zeroed when lens is given.  x16 / want16: as
+        MultiHeadAttention.run (w_1 reads x16)."""
         p = self._packed(x.device, self._build)
         k1, k2 = self.kernel_size
         d_hid = self.w_1.out_channels
         cd = self.compute_dtype
-        h = ops.conv1d(x, p["w1"], p["b1"], Co=d_hid, K=k1, pad=(k1 - 1) // 2,
+        h = ops.conv1d(x16 if x16 is not None else x, p["w1"], p["b1"], Co=d_hid, K=k1, pad=(k1 - 1) // 2,
                        post_act=ops.ACT_RELU, compute_dtype=cd, out_dtype=cd,
                        tag=getattr(self, "timer_tag", None))
         y = ops.conv1d(h, p["w2"], p["b2"], Co=x.shape[-1], K=k2, pad=(k2 - 1) // 2,
                        compute_dtype=cd, out_dtype=x.dtype)
-        return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens)
+        return ops.layernorm(y, p["g"], p["beta"], res=x, lens=lens, with_bf16=want16)
 
     def forward(self, x):
         self._check_inference()
