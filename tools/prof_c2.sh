@@ -19,10 +19,10 @@ def cls(n):  # kernel class of the C2 breakdown
         return "LayerNorm (+ residual, pad-row zeroing)"
     if "attn" in n or "attention" in n:
         return "attention"
-    if "conv_splitk_reduce" in n or "conv1d_kernel<float" in n:
+    if "conv_splitk_reduce" in n or "conv1d_kernel<float, float, float" in n:
         return "fp32 short-sequence convs (encoder / predictors, T_src = 12; split reduction)"
-    if "conv1d_kernel<unsigned short" in n:
-        return "bf16 convs over T_mel (decoder FFN / qkv / fc, PostNet, mel_linear)"
+    if "conv1d_kernel<" in n:  # template <input, compute, output, ...>: bf16 compute
+        return "bf16-compute convs over T_mel (decoder FFN w_1 / w_2, q/k/v, fc; PostNet; mel_linear)"
     return "glue (embeddings, VFE, length regulator, heads, masks, casts)"
 
 

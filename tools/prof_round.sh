@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round profile set (round 3): a SERIALIZED rocprofv3 kernel trace of the bench step (no acoustic /
+# Round profile set (rounds 3-4): a SERIALIZED rocprofv3 kernel trace of the bench step (no acoustic /
 # vocoder pipeline, the C = 256 MRF chains one after another -- the configuration of bench.py's
 # roofline pass), its steady-state tail stats, and the HBM traffic per launch from separate
 # FETCH_SIZE / WRITE_SIZE --pmc passes over the same command (+ the C2 decoder FFN w_1 conv alone).
