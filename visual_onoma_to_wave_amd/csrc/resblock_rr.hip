@@ -939,7 +939,7 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
                    const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                    hipStream_t st, int* handled) {
   *handled = 0;
-  if (C != 32 || !(K == 7 || K == 11) || !(dil == 1 || dil == 3 || dil == 5)) return VO_OK;
+  if (!(C == 32 || (C == 64 && K == 7)) || !(K == 7 || K == 11) || !(dil == 1 || dil == 3 || dil == 5)) return VO_OK;
   if ((int64_t)T * C * 2 >= (int64_t)1 << 31) return VO_OK;
   RrpArgs a;
   a.x = (const bf16_t*)x;
@@ -947,16 +947,32 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
   a.T = T; a.slope = slope; a.out_scale = out_scale;
 #ifdef VO_ABLATIONS  // other frame shapes
-  *handled = 1;
-  if (cfg == 90) return K == 7 ? rrp_launch_d<32, 7, 12, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 12, 8>(a, B, dil, st);
-  if (cfg == 91) return K == 7 ? rrp_launch_d<32, 7, 16, 4>(a, B, dil, st) : rrp_launch_d<32, 11, 16, 4>(a, B, dil, st);
-  if (cfg == 92) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 10, 8>(a, B, dil, st);
-  if (cfg == 93) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 8, 8>(a, B, dil, st);
+  *handled = C == 32;
+  if (C == 32 && cfg == 90) return K == 7 ? rrp_launch_d<32, 7, 12, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 12, 8>(a, B, dil, st);
+  if (C == 32 && cfg == 91) return K == 7 ? rrp_launch_d<32, 7, 16, 4>(a, B, dil, st) : rrp_launch_d<32, 11, 16, 4>(a, B, dil, st);
+  if (C == 32 && cfg == 92) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 10, 8>(a, B, dil, st);
+  if (C == 32 && cfg == 93) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 8, 8>(a, B, dil, st);
   *handled = 0;
+  if (C == 64) {  // k = 7 (k = 11's two convs, 176 KiB, do not fit the LDS)
+    *handled = 1;
+    if (cfg == 94) return rrp_launch_d<64, 7, 10, 4>(a, B, dil, st);
+    if (cfg == 95) return rrp_launch_d<64, 7, 8, 4>(a, B, dil, st);
+    if (cfg == 96) return rrp_launch_d<64, 7, 12, 4>(a, B, dil, st);
+    *handled = 0;
+    return VO_OK;
+  }
 #endif
-  // shipped for dilation 1 only (the halo, (K - 1) / 2 * (d + 1) rows per side, costs more than the
+  if (cfg != 0) return VO_OK;
+  if (C == 64) {
+    // k = 7 at dilations 1 / 3, one wave per SIMD, 128-row frames: 0.312 -> 0.258 / 0.278 ms; at d = 5
+    // (18 halo rows per side) no faster (pair_cfg 95, round 4)
+    if (K != 7 || dil == 5) return VO_OK;
+    *handled = 1;
+    return dil == 1 ? rrp_launch<64, 7, 1, 8, 4>(a, B, st) : rrp_launch<64, 7, 3, 8, 4>(a, B, st);
+  }
+  // C = 32: dilation 1 only (the halo, (K - 1) / 2 * (d + 1) rows per side, costs more than the
   // frames save at d = 3 / 5): k = 7 0.197 -> 0.187 ms, k = 11 0.238 -> 0.217 (pair_cfg 93, round 4)
-  if (dil != 1 || cfg != 0) return VO_OK;
+  if (dil != 1) return VO_OK;
   *handled = 1;
   return K == 7 ? rrp_launch<32, 7, 1, 8, 8>(a, B, st) : rrp_launch<32, 11, 1, 8, 8>(a, B, st);
 }
