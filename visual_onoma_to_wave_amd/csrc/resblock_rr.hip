@@ -93,7 +93,7 @@ __device__ __forceinline__ u32x4 shifted(const u32x4 (&in)[NB][NS], int s) {
 
 // NWV waves per workgroup (NWV / 4 per SIMD); PF: the next frame requested at the start of a tile
 // (registers permitting; otherwise the partner wave covers the latency)
-template <int C, int NB, int NWV, bool PF>
+template <int C, int NB, int NWV, bool PF, bool PA = false, bool PL = false>
 __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3_kernel(RrArgs a) {
   constexpr int NS = C / 32;   // K-steps (32-channel planes)
   constexpr int NCB = C / 16;  // 16-channel output blocks
@@ -147,8 +147,10 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3_kernel(RrArgs a) {
         fr[n][s] = __builtin_amdgcn_raw_buffer_load_b128(rs, (w0 + n) * C * 2 + lane_off, 64 * s, 0);
   };
 
-  u32x4 xn[PF ? NB : 1][NS];
-  if constexpr (PF) load_rows(a.x, tile, xn);
+  // PF: the next frame requested at the start of a tile; PL: after the last conv's MFMAs, into the
+  // registers its input has just freed (in flight during the final epilogue and stores)
+  u32x4 xn[(PF || PL) ? NB : 1][NS];
+  if constexpr (PF || PL) load_rows(a.x, tile, xn);
   u32x4 af[2][NCB];  // A fragments: step g of a tile uses af[g & 1]
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) af[0][cb] = wfr[(NS * NCB + cb) * 64 + lane];  // (conv 0, tap 1, K-step 0)
@@ -159,12 +161,12 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3_kernel(RrArgs a) {
     const int w0 = t0 - RR_HALO;
     const bool interior = w0 >= 0 && w0 + F <= T;
     u32x4 xb[NB][NS], in[NB][NS];
-    if constexpr (PF) {
+    if constexpr (PF || PL) {
 #pragma unroll
       for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int s = 0; s < NS; ++s) xb[n][s] = xn[n][s];
-      load_rows(a.x, tile + 1 < tile_end ? tile + 1 : tile, xn);  // unconditional: no divergent wait
+      if constexpr (PF) load_rows(a.x, tile + 1 < tile_end ? tile + 1 : tile, xn);  // unconditional
     } else {
       load_rows(a.x, tile, xb);
     }
@@ -271,7 +273,11 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3_kernel(RrArgs a) {
     conv(std::integral_constant<int, 2>{});
     conv(std::integral_constant<int, 3>{});
     conv(std::integral_constant<int, 4>{});
+    // PA: the MRF accumulator rows requested before the last conv (in flight during its MFMAs)
+    u32x4 ainp[PA ? NB : 1][NS];
+    if constexpr (PA) load_rows(a.acc ? a.acc : a.x, tile, ainp);
     conv(std::integral_constant<int, 5>{});
+    if constexpr (PL) load_rows(a.x, tile + 1 < tile_end ? tile + 1 : tile, xn);
 
     // y = (x2 + c2 + b2) * out_scale (+ acc) on rows t0 .. t0 + valid - 1 = frame rows HALO ..: a
     // resource over exactly those rows drops the halo rows' stores (rows before it: an offset past
@@ -282,7 +288,16 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rr3_kernel(RrArgs a) {
     auto fin = [&](auto with_acc) {
       constexpr bool ACC = decltype(with_acc)::value;
       u32x4 ain[ACC ? NB : 1][NS];
-      if constexpr (ACC) load_rows(a.acc, tile, ain);
+      if constexpr (ACC) {
+        if constexpr (PA) {
+#pragma unroll
+          for (int n = 0; n < NB; ++n)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) ain[n][s] = ainp[n][s];
+        } else {
+          load_rows(a.acc, tile, ain);
+        }
+      }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         const int r = lr * NB + n - RR_HALO;
@@ -643,14 +658,14 @@ static int rr3w_launch(RrArgs a, int B, hipStream_t st) {
   VO_RETURN_LAUNCH();
 }
 
-template <int C, int NB, int NWV, bool PF>
+template <int C, int NB, int NWV, bool PF, bool PA = false, bool PL = false>
 static int rr3_launch(RrArgs a, int B, hipStream_t st) {
   constexpr int OR = 16 * NB - 2 * RR_HALO;
   constexpr size_t lds = (size_t)6 * 3 * (C / 32) * (C / 16) * 1024 + 6 * C * sizeof(float);
   static_assert(lds <= 160 * 1024, "LDS");
   a.tiles_per_b = (a.T + OR - 1) / OR;
   a.ntiles = a.tiles_per_b * B;
-  auto kern = mrf_rr3_kernel<C, NB, NWV, PF>;
+  auto kern = mrf_rr3_kernel<C, NB, NWV, PF, PA, PL>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -918,6 +933,9 @@ int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, 
     if (cfg == 85) return rr3_launch<32, 7, 8, true>(a, B, st);
     if (cfg == 86) return rr3_launch<32, 6, 12, false>(a, B, st);
     if (cfg == 87) return rr3_launch<32, 10, 8, false>(a, B, st);
+    if (cfg == 88) return rr3_launch<32, 8, 8, false, true>(a, B, st);
+    if (cfg == 89) return rr3_launch<32, 8, 8, false, true, true>(a, B, st);
+    if (cfg == 79) return rr3_launch<32, 8, 8, false, false, true>(a, B, st);
   } else {
     if (cfg == 80) return rr3_launch<64, 6, 4, false>(a, B, st);
     if (cfg == 81) return rr3_launch<64, 6, 4, true>(a, B, st);
