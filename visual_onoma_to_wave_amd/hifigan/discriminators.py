@@ -269,8 +269,7 @@ def feature_loss(fmap_r, fmap_g):
 def discriminator_loss(disc_real_outputs, disc_generated_outputs):
     """(sum of mean((1 - D(y))^2) + mean(D(G(x))^2), [real terms], [generated terms])."""
     n = len(disc_real_outputs)
-    t = G.gan_loss_terms([(dr, None, ops.GAN_ONE_MINUS_SQ, 1.0 / dr.numel()) for dr in disc_real_outputs]
-                         + [(dg, None, ops.GAN_SQ, 1.0 / dg.numel()) for dg in disc_generated_outputs])
+    t = G.gan_split_terms(disc_real_outputs, disc_generated_outputs, ops.GAN_ONE_MINUS_SQ, ops.GAN_SQ)
     return t.sum(), list(t[:n].unbind()), list(t[n:].unbind())
 
 

@@ -78,11 +78,17 @@ def _pack_grouped(w, dtype, groups, ci_pad, slot):
                                                                       dtype, w.device))
 
 
-def _bias(b, spec, n):
-    b = b.detach().float()
-    if b.numel() < n:
-        b = F.pad(b, (0, n - b.numel()))
-    return b.contiguous()
+def _bias(b, spec, n, wkey=None):
+    """The bias as an fp32 vector of n (>= its length: padded output channels get 0).  A padded bias
+    is cached at the parameter's version (the D step and the G step's two passes run each conv_post
+    three times per step: one pad launch pair instead of three; capture-aware like the weight packs)."""
+    pad = lambda: F.pad(b.detach().float(), (0, n - b.numel())).contiguous()  # noqa: E731
+    if b.numel() >= n:
+        return b.detach().float().contiguous()
+    if wkey is None:
+        return pad()
+    # keyed on the conv module (a tensor key would be compared with ==, a device op) and the bias version
+    return _cached((wkey[0], b._version), f"bias{n}", pad)
 
 
 def out_len(spec, T_in):
@@ -175,7 +181,7 @@ def _conv_fwd(x, w, b, res1, res2, spec, cdt, wkey=None):
                           pre_slope=spec.pre_slope or 0.0, transposed=dict(stride=s, pad=p, cout=cout),
                           res1=res1, res2=res2, out_scale=spec.out_scale, out_dtype=x.dtype, compute_dtype=cdt)
     Co = wp.shape[1]
-    return ops.conv1d(x, wp, _bias(b, spec, Co), Co=Co, K=spec.K, dil=spec.dil, pad=spec.pad,
+    return ops.conv1d(x, wp, _bias(b, spec, Co, wkey), Co=Co, K=spec.K, dil=spec.dil, pad=spec.pad,
                       T_out=out_len(spec, x.shape[1]),
                       pre_act=ops.ACT_LRELU if spec.pre_slope is not None else ops.ACT_NONE,
                       pre_slope=spec.pre_slope or 0.0, post_act=_POST[spec.post], post_slope=spec.post_slope,
@@ -718,6 +724,74 @@ class GanLossTermsFn(torch.autograd.Function):
 
 
 _SCALES = {}  # (scales, device) -> fp32 vector (made outside graph capture, reused inside)
+
+
+class GanSplitTermsFn(torch.autograd.Function):
+    """The discriminator loss over score tensors that hold the real batch in their first half and
+    the generated batch in their second (the D step runs both as one batch): terms
+    scale * reduce(kind_first, S[:h]) for every S, then scale * reduce(kind_second, S[h:]).  Taking
+    the whole S keeps the halves' slice views out of the autograd graph: their backward was a zero
+    fill and a copy per half plus an add per tensor (16 + 16 + 8 launches per C5 step); here one
+    gradient tensor per S is written half by half."""
+
+    @staticmethod
+    def forward(ctx, kinds, sv, *bases):
+        n = len(bases)
+        out = torch.zeros(2 * n, dtype=torch.float32, device=bases[0].device)
+        for i, s in enumerate(bases):
+            h = s.shape[0] // 2
+            ops.gan_reduce(kinds[0], s[:h], None, out=out[i])
+            ops.gan_reduce(kinds[1], s[h:], None, out=out[n + i])
+        ctx.kinds = kinds
+        ctx.save_for_backward(sv, *bases)
+        return out * sv
+
+    @staticmethod
+    def backward(ctx, g):
+        sv, *bases = ctx.saved_tensors
+        n = len(bases)
+        gs = g.float() * sv
+        grads = []
+        for i, s in enumerate(bases):
+            if not ctx.needs_input_grad[2 + i]:
+                grads.append(None)
+                continue
+            h = s.shape[0] // 2
+            gsb = torch.empty_like(s, memory_format=torch.contiguous_format)
+            ops.gan_reduce_grad(ctx.kinds[0], s[:h], None, gs[i], out=gsb[:h])
+            ops.gan_reduce_grad(ctx.kinds[1], s[h:], None, gs[n + i], out=gsb[h:])
+            grads.append(gsb)
+        return (None, None, *grads)
+
+
+def _halves_of(a, b):
+    """The tensor whose first / second half along dim 0 are the views a / b, else None."""
+    base = a._base
+    if base is None or b._base is not base or not base.is_contiguous() or base.shape[0] % 2:
+        return None
+    h = base.shape[0] // 2
+    if a.shape[0] != h or b.shape[0] != h or a.data_ptr() != base.data_ptr() or \
+            b.data_ptr() != base[h:].data_ptr() or not (a.is_contiguous() and b.is_contiguous()):
+        return None
+    return base
+
+
+def gan_split_terms(firsts, seconds, kind_first, kind_second):
+    """gan_loss_terms([(f, None, kind_first, 1 / f.numel())] + [(s, None, kind_second, 1 / s.numel())])
+    -- through GanSplitTermsFn when every (f, s) pair is the two halves of one tensor."""
+    bases = [_halves_of(f, s) for f, s in zip(firsts, seconds)]
+    items = ([(f, None, kind_first, 1.0 / f.numel()) for f in firsts]
+             + [(s, None, kind_second, 1.0 / s.numel()) for s in seconds])
+    if any(bs is None for bs in bases):
+        return gan_loss_terms(items)
+    dev = firsts[0].device
+    key = (tuple(float(it[3]) for it in items), dev)
+    sv = _SCALES.get(key)
+    if sv is None:
+        if torch.cuda.is_current_stream_capturing():
+            return gan_loss_terms(items)
+        sv = _SCALES[key] = torch.tensor(key[0], dtype=torch.float32, device=dev)
+    return GanSplitTermsFn.apply((kind_first, kind_second), sv, *bases)
 
 
 def gan_loss_terms(items):

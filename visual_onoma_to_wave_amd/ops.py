@@ -910,13 +910,19 @@ def gan_reduce(kind, a, b=None, out=None):
     return out
 
 
-def gan_reduce_grad(kind, a, b, scale):
-    """d(scale * sum)/da in a contiguous tensor shaped like a (scale: fp32 device scalar)."""
+def gan_reduce_grad(kind, a, b, scale, out=None):
+    """d(scale * sum)/da in a contiguous tensor shaped like a (scale: fp32 device scalar); ``out``: a
+    contiguous tensor of a's dtype and size to write it into (returned reshaped like a)."""
     la, rows, width, lda = _rows_view(a)
     ldb = 0
     if b is not None:
         b, _, _, ldb = _rows_view(b)
-    ga = torch.empty((rows, width), dtype=a.dtype, device=a.device)
+    if out is not None:
+        if not out.is_contiguous() or out.numel() != rows * width or out.dtype != a.dtype:
+            raise ValueError("gan_reduce_grad: out must be contiguous, of a's dtype and size")
+        ga = out
+    else:
+        ga = torch.empty((rows, width), dtype=a.dtype, device=a.device)
     _lib.check(_lib.lib().vo_gan_reduce_grad(kind, _ptr(la), lda, _ptr(b), ldb, rows, width, vo_dtype(a),
                                              _ptr(scale.float().contiguous()), _ptr(ga), width, _stream(a)),
                "vo_gan_reduce_grad")
