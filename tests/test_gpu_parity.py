@@ -457,8 +457,7 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-# cfg 0: the shipped dispatch (register-resident frames for C = 32 at d = 1 and C = 64 k = 7 at d = 1 / 3);
-# 93: the LDS-tile kernels
+# cfg 0: the shipped dispatch (register-resident frames for C = 64 k = 7); 93: the LDS-tile kernels
 @pytest.mark.parametrize("cfg", [0, 93])
 @pytest.mark.parametrize("with_acc", [True, False])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),

@@ -645,7 +645,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
-  {  // round 4: register-resident frames (resblock_rr.hip): C = 32 at d = 1, C = 64 k = 7 at d = 1 / 3; pair_cfg 90-96 (A/B)
+  {  // round 4: register-resident frames (resblock_rr.hip) for C = 64 k = 7; pair_cfg 90-99 (A/B)
     int handled = 0;
     const int rc = vo_pair_rr_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;

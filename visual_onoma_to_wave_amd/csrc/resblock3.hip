@@ -603,7 +603,7 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
-  {  // round 4: register-resident frames (resblock_rr.hip) for C = 32, dilations (1, 3, 5); rb3_cfg 79-89 (A/B)
+  {  // round 4: register-resident frames (resblock_rr.hip) for C = 32, dilations (1, 3, 5); rb3_cfg 77-89 (A/B)
     int handled = 0;
     const int rc = vo_rb3_rr_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, cfg, st, &handled);
     if (handled) return rc;

@@ -941,6 +941,8 @@ int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, 
     if (cfg == 81) return rr3_launch<64, 6, 4, true>(a, B, st);
     if (cfg == 82) return rr3w_launch<64, 4, 4, false>(a, B, st);
     if (cfg == 83) return rr3w_launch<64, 4, 4, true>(a, B, st);
+    if (cfg == 78) return rr3_launch<64, 6, 4, false, true>(a, B, st);
+    if (cfg == 77) return rr3_launch<64, 6, 4, false, true, true>(a, B, st);
   }
   *handled = 0;
 #endif
@@ -970,27 +972,28 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
   if (C == 32 && cfg == 91) return K == 7 ? rrp_launch_d<32, 7, 16, 4>(a, B, dil, st) : rrp_launch_d<32, 11, 16, 4>(a, B, dil, st);
   if (C == 32 && cfg == 92) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 10, 8>(a, B, dil, st);
   if (C == 32 && cfg == 93) return K == 7 ? rrp_launch_d<32, 7, 8, 8>(a, B, dil, st) : rrp_launch_d<32, 11, 8, 8>(a, B, dil, st);
+  if (C == 32 && cfg == 99) return K == 7 ? rrp_launch<32, 7, 1, 8, 8>(a, B, st) : rrp_launch<32, 11, 1, 8, 8>(a, B, st);
   *handled = 0;
   if (C == 64) {  // k = 7 (k = 11's two convs, 176 KiB, do not fit the LDS)
     *handled = 1;
     if (cfg == 94) return rrp_launch_d<64, 7, 10, 4>(a, B, dil, st);
     if (cfg == 95) return rrp_launch_d<64, 7, 8, 4>(a, B, dil, st);
     if (cfg == 96) return rrp_launch_d<64, 7, 12, 4>(a, B, dil, st);
+    if (cfg == 97) return rrp_launch_d<64, 7, 7, 4>(a, B, dil, st);
     *handled = 0;
-    return VO_OK;
   }
 #endif
   if (cfg != 0) return VO_OK;
   if (C == 64) {
-    // k = 7 at dilations 1 / 3, one wave per SIMD, 128-row frames: 0.312 -> 0.258 / 0.278 ms; at d = 5
-    // (18 halo rows per side) no faster (pair_cfg 95, round 4)
-    if (K != 7 || dil == 5) return VO_OK;
+    // k = 7, one wave per SIMD, 144-row frames (9 blocks): 0.326 -> 0.264 / 0.293 / 0.313 ms at d = 1 / 3 / 5
+    // (pair_cfg 0 / 98 before the switch; 128-row frames, pair_cfg 95: 0.262 / 0.289 / 0.328)
+    if (K != 7) return VO_OK;
     *handled = 1;
-    return dil == 1 ? rrp_launch<64, 7, 1, 8, 4>(a, B, st) : rrp_launch<64, 7, 3, 8, 4>(a, B, st);
+    return rrp_launch_d<64, 7, 9, 4>(a, B, dil, st);
   }
-  // C = 32: dilation 1 only (the halo, (K - 1) / 2 * (d + 1) rows per side, costs more than the
-  // frames save at d = 3 / 5): k = 7 0.197 -> 0.187 ms, k = 11 0.238 -> 0.217 (pair_cfg 93, round 4)
-  if (dil != 1) return VO_OK;
-  *handled = 1;
-  return K == 7 ? rrp_launch<32, 7, 1, 8, 8>(a, B, st) : rrp_launch<32, 11, 1, 8, 8>(a, B, st);
+  // C = 32 keeps the LDS-tile kernels: at d = 1 the frames (pair_cfg 93 in the A/B library) measure
+  // faster alone (k = 7 0.197 -> 0.187 ms, k = 11 0.238 -> 0.217) but ~9 us per launch slower inside the
+  // bench step (tools/bench_ab.sh: s3 0.1947 vs 0.1921 ms per launch, two rounds); at d = 3 / 5 the
+  // halo, (K - 1) / 2 * (d + 1) rows per side, costs more than the frames save
+  return VO_OK;
 }
