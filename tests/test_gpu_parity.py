@@ -10,6 +10,8 @@ Tolerances (relative L2 unless stated):
 """
 
 import numpy as np
+import os
+
 import pytest
 import torch
 
@@ -457,8 +459,12 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-# cfg 0: the shipped dispatch (register-resident frames for C = 64 k = 7); 93: the LDS-tile kernels
-@pytest.mark.parametrize("cfg", [0, 93])
+# cfg 0: the shipped dispatch (register-resident frames for C = 64 k = 7); 93: the LDS-tile kernels;
+# VO_PARITY_PAIR_CFGS=94,95 adds A/B candidates of the ablation build
+_PAIR_CFGS = [0, 93] + [int(c) for c in os.environ.get("VO_PARITY_PAIR_CFGS", "").split(",") if c]
+
+
+@pytest.mark.parametrize("cfg", _PAIR_CFGS)
 @pytest.mark.parametrize("with_acc", [True, False])
 @pytest.mark.parametrize("C,T,k,d", [(32, 1000, 11, 5), (64, 777, 7, 3), (32, 5, 3, 1), (64, 1, 11, 1),
                                      (32, 246 * 3, 11, 5), (64, 4096, 3, 5), (64, 502, 11, 3),

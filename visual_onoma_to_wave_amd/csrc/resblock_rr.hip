@@ -695,20 +695,27 @@ struct RrpArgs {
   float slope, out_scale;
 };
 
-template <int C, int K, int D, int NB, int NWV>
+// RT: each conv's centre tap held in registers (loaded once per kernel) and only the other K - 1 taps in
+// LDS -- C = 64, K = 11: 160 instead of 176 KiB of fragments
+template <int C, int K, int D, int NB, int NWV, bool RT = false>
 __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
   constexpr int NS = C / 32, NCB = C / 16, NT = NWV * 64, F = 16 * NB;
   constexpr int HK = (K - 1) / 2;
   constexpr int HALO = HK * (D + 1);
   constexpr int OR = F - 2 * HALO;
-  constexpr int NFR = 2 * K * NS * NCB;
-  constexpr int NST = K * NS;  // steps per conv
+  constexpr int KL = RT ? K - 1 : K;       // taps per conv in LDS
+  constexpr int NFR = 2 * KL * NS * NCB;   // LDS fragments
   static_assert(OR > 0 && HK * D < 16 * NB, "frame too small for the halo");
-  static_assert((2 * NST) % 2 == 0, "fragment parity repeats per tile");
+  static_assert((2 * KL * NS) % 2 == 0, "fragment parity repeats per tile");
+  // LDS fragment of (conv, tap, K-step, co-block) (RT: never the centre tap)
+  auto lfi = [](int cv, int k, int s, int cb) constexpr {
+    const int kl = RT ? (k < (K - 1) / 2 ? k : k - 1) : k;
+    return ((cv * KL + kl) * NS + s) * NCB + cb;
+  };
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   u32x4* wfr = reinterpret_cast<u32x4*>(smem_raw);
-  float* sb = reinterpret_cast<float*>(smem_raw + NFR * 1024);
+  float* sb = reinterpret_cast<float*>(smem_raw + NFR * 1024);  // (RT: the biases live in registers)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -718,12 +725,14 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
 
   for (int i = tid; i < NFR * 64; i += NT) {
     const int f = i >> 6, l = i & 63;
-    const int b = f % NCB, s = (f / NCB) % NS, k = (f / (NCB * NS)) % K, cv = f / (NCB * NS * K);
+    const int b = f % NCB, s = (f / NCB) % NS, kl = (f / (NCB * NS)) % KL, cv = f / (NCB * NS * KL);
+    const int k = RT ? (kl < HK ? kl : kl + 1) : kl;
     const int m = l & 15;
     const int co = 32 * (b >> 1) + 8 * (m >> 2) + 4 * (b & 1) + (m & 3);
     wfr[i] = *reinterpret_cast<const u32x4*>(a.w[cv] + k * C * C + co * C + 32 * s + 8 * (l >> 4));
   }
-  for (int i = tid; i < 2 * C; i += NT) sb[i] = a.bias[i / C][i % C];
+  if constexpr (!RT)
+    for (int i = tid; i < 2 * C; i += NT) sb[i] = a.bias[i / C][i % C];
   __syncthreads();
 
   const int gw = blockIdx.x * NWV + wave, nw = gridDim.x * NWV;
@@ -748,9 +757,32 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
   // tap of step j of a conv: the centre tap first (no shift), then 0 .. K - 1 without it
   auto tap_of = [](int j) constexpr { return j == 0 ? (K - 1) / 2 : (j <= (K - 1) / 2 ? j - 1 : j); };
 
-  u32x4 af[2][NCB];
+  // the centre taps (RT), straight from the packed weights: lane layout of an A fragment
+  u32x4 ctap[RT ? 2 : 1][NS][NCB];
+  if constexpr (RT) {
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) af[0][cb] = wfr[((HK * NS) * NCB + cb) * 64 + lane];  // (c1, centre, 0)
+    for (int cv = 0; cv < 2; ++cv)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int m = lane & 15;
+          const int co = 32 * (cb >> 1) + 8 * (m >> 2) + 4 * (cb & 1) + (m & 3);
+          ctap[cv][s][cb] = *reinterpret_cast<const u32x4*>(a.w[cv] + HK * C * C + co * C + 32 * s + 8 * lq);
+        }
+  }
+  f32x4 breg[RT ? 2 : 1][NCB];  // RT: the lane's bias values of both convs (the LDS is full)
+  if constexpr (RT) {
+#pragma unroll
+    for (int cv = 0; cv < 2; ++cv)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        breg[cv][cb] = *reinterpret_cast<const f32x4*>(a.bias[cv] + 32 * (cb >> 1) + 8 * lq + 4 * (cb & 1));
+  }
+  u32x4 af[2][NCB];
+  // the first LDS step of c1: the centre tap (or, RT, tap 0)
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) af[0][cb] = wfr[lfi(0, RT ? 0 : HK, 0, cb) * 64 + lane];
 
   for (; tile < tile_end; ++tile) {
     const int b = tile / a.tiles_per_b;
@@ -774,7 +806,11 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
       constexpr int d = cv == 0 ? D : 1;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + cv * C + 32 * (cb >> 1) + 8 * lq + 4 * (cb & 1));
+        f32x4 bv;
+        if constexpr (RT)
+          bv = breg[cv][cb];
+        else
+          bv = *reinterpret_cast<const f32x4*>(sb + cv * C + 32 * (cb >> 1) + 8 * lq + 4 * (cb & 1));
 #pragma unroll
         for (int n = 0; n < NB; ++n) acc[n][cb] = bv;
       }
@@ -782,22 +818,32 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
         constexpr int j = decltype(jc)::value;
         constexpr int k = tap_of(j);
         constexpr int O = (k - HK) * d;
+        constexpr bool REG = RT && j == 0;  // the centre tap from registers
         auto ks = [&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          constexpr int g = cv * NST + j * NS + s;
-          constexpr int fn = s + 1 < NS ? (((cv * K + k) * NS + s + 1) * NCB)
-                                        : (j + 1 < K ? (((cv * K + tap_of(j + 1)) * NS) * NCB)
-                                                     : ((((cv + 1) % 2 * K + HK) * NS) * NCB));
+          // LDS step index within the tile (its parity picks the fragment buffer) and the next LDS step
+          constexpr int g = cv * KL * NS + (RT ? j - 1 : j) * NS + s;
+          constexpr int fn = s + 1 < NS ? lfi(cv, k, s + 1, 0)
+                                        : (j + 1 < K ? lfi(cv, tap_of(j + 1), 0, 0)
+                                                     : lfi((cv + 1) % 2, tap_of(RT ? 1 : 0), 0, 0));
+          if constexpr (!REG) {
 #pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) af[(g + 1) & 1][cb] = wl[(fn + cb) * 64];
+            for (int cb = 0; cb < NCB; ++cb) af[(g + 1) & 1][cb] = wl[(fn + cb) * 64];
+          }
           __builtin_amdgcn_sched_barrier(0);
           auto blk = [&](auto nc) {
             constexpr int n = decltype(nc)::value;
             const bf16x8 bv = __builtin_bit_cast(bf16x8, shifted<O, NB, NS, n>(in, s));
 #pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-              acc[n][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[g & 1][cb]), bv,
-                                                                  acc[n][cb], 0, 0, 0);
+            for (int cb = 0; cb < NCB; ++cb) {
+              u32x4 A;
+              if constexpr (REG)
+                A = ctap[RT ? cv : 0][s][cb];
+              else
+                A = af[g & 1][cb];
+              acc[n][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A), bv, acc[n][cb], 0,
+                                                                  0, 0);
+            }
           };
           static_for<NB>(blk);
         };
@@ -877,14 +923,14 @@ __global__ void __launch_bounds__(NWV * 64, 1) mrf_rrp_kernel(RrpArgs a) {
   }
 }
 
-template <int C, int K, int D, int NB, int NWV>
+template <int C, int K, int D, int NB, int NWV, bool RT = false>
 static int rrp_launch(RrpArgs a, int B, hipStream_t st) {
   constexpr int OR = 16 * NB - 2 * ((K - 1) / 2) * (D + 1);
-  constexpr size_t lds = (size_t)2 * K * (C / 32) * (C / 16) * 1024 + 2 * C * sizeof(float);
+  constexpr size_t lds = (size_t)2 * (RT ? K - 1 : K) * (C / 32) * (C / 16) * 1024 + (RT ? 0 : 2 * C * sizeof(float));
   static_assert(lds <= 160 * 1024, "LDS");
   a.tiles_per_b = (a.T + OR - 1) / OR;
   a.ntiles = a.tiles_per_b * B;
-  auto kern = mrf_rrp_kernel<C, K, D, NB, NWV>;
+  auto kern = mrf_rrp_kernel<C, K, D, NB, NWV, RT>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -896,11 +942,11 @@ static int rrp_launch(RrpArgs a, int B, hipStream_t st) {
   VO_RETURN_LAUNCH();
 }
 
-template <int C, int K, int NB, int NWV>
+template <int C, int K, int NB, int NWV, bool RT = false>
 static int rrp_launch_d(RrpArgs a, int B, int dil, hipStream_t st) {
-  if (dil == 1) return rrp_launch<C, K, 1, NB, NWV>(a, B, st);
-  if (dil == 3) return rrp_launch<C, K, 3, NB, NWV>(a, B, st);
-  return rrp_launch<C, K, 5, NB, NWV>(a, B, st);
+  if (dil == 1) return rrp_launch<C, K, 1, NB, NWV, RT>(a, B, st);
+  if (dil == 3) return rrp_launch<C, K, 3, NB, NWV, RT>(a, B, st);
+  return rrp_launch<C, K, 5, NB, NWV, RT>(a, B, st);
 }
 
 }  // namespace vo
@@ -959,7 +1005,7 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
                    const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                    hipStream_t st, int* handled) {
   *handled = 0;
-  if (!(C == 32 || (C == 64 && K == 7)) || !(K == 7 || K == 11) || !(dil == 1 || dil == 3 || dil == 5)) return VO_OK;
+  if (!(C == 32 || C == 64) || !(K == 7 || K == 11) || !(dil == 1 || dil == 3 || dil == 5)) return VO_OK;
   if ((int64_t)T * C * 2 >= (int64_t)1 << 31) return VO_OK;
   RrpArgs a;
   a.x = (const bf16_t*)x;
@@ -976,10 +1022,17 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
   *handled = 0;
   if (C == 64) {  // k = 7 (k = 11's two convs, 176 KiB, do not fit the LDS)
     *handled = 1;
-    if (cfg == 94) return rrp_launch_d<64, 7, 10, 4>(a, B, dil, st);
-    if (cfg == 95) return rrp_launch_d<64, 7, 8, 4>(a, B, dil, st);
-    if (cfg == 96) return rrp_launch_d<64, 7, 12, 4>(a, B, dil, st);
-    if (cfg == 97) return rrp_launch_d<64, 7, 7, 4>(a, B, dil, st);
+    if (K == 7 && cfg == 94) return rrp_launch_d<64, 7, 10, 4>(a, B, dil, st);
+    if (K == 7 && cfg == 95) return rrp_launch_d<64, 7, 8, 4>(a, B, dil, st);
+    if (K == 7 && cfg == 96) return rrp_launch_d<64, 7, 12, 4>(a, B, dil, st);
+    if (K == 7 && cfg == 97) return rrp_launch_d<64, 7, 7, 4>(a, B, dil, st);
+    if (K == 11 && cfg == 94) return rrp_launch_d<64, 11, 8, 4, true>(a, B, dil, st);
+    if (K == 11 && cfg == 95) return rrp_launch_d<64, 11, 10, 4, true>(a, B, dil, st);
+    // 98: 128-row frames for k = 7 at d = 1 / 3, 144-row at d = 5; k = 11 d = 1 with the centre taps in registers
+    if (cfg == 98) {
+      if (K == 7) return dil == 5 ? rrp_launch_d<64, 7, 9, 4>(a, B, dil, st) : rrp_launch_d<64, 7, 8, 4>(a, B, dil, st);
+      if (dil == 1) return rrp_launch<64, 11, 1, 8, 4, true>(a, B, st);
+    }
     *handled = 0;
   }
 #endif
