@@ -95,11 +95,6 @@ typedef struct vo_conv1d_desc {
                          reduction over workgroups and add the fp32 partials in a fixed
                          order (deterministic)                                           */
   int64_t workspace_bytes;
-  const void* xmask;  /* optional, x's layout and dtype (bf16): the input row value v is staged
-                         as v * (xmask > 0 ? 1 : xmask_slope) -- the leaky-ReLU backward of
-                         the layer that produced xmask, applied to dY while it is staged (the
-                         HiFi-GAN discriminators' input gradients; no separate mask pass)   */
-  float xmask_slope;
 } vo_conv1d_desc;
 int vo_conv1d(const vo_conv1d_desc* d, void* stream);
 /* scratch bytes the split-reduction path of vo_conv1d wants for d (0 = it does not split d) */
@@ -424,15 +419,6 @@ int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb
                          int M, int N, int K, int S, int dil, int pad, int groups, int pre_a,
                          int pre_b, float slope, int dtype, float* dw, float* db, float* workspace,
                          void* stream);
-/* vo_conv1d_wgrad_bias with A = dY staged through a leaky-ReLU backward mask: A[r, c] *
- * (amask[r, c] > 0 ? 1 : mslope), amask in A's layout (the layer's output), bf16 only; the bias
- * gradient (db non-NULL) sums the masked values.  Replaces the separate vo_lrelu_mask pass over
- * the discriminators' post-activation gradients (autograd of F.leaky_relu after each conv of
- * HiFi-GAN's DiscriminatorP / DiscriminatorS). */
-int vo_conv1d_wgrad_masked(const void* a, const void* amask, float mslope, int lda, int T_A, const void* b,
-                           int ldb, int T_B, int B, int M, int N, int K, int S, int dil, int pad, int groups,
-                           int pre_b, float slope, int dtype, float* dw, float* db, float* workspace,
-                           void* stream);
 int64_t vo_colsum_workspace_size(int64_t rows, int C);
 int vo_colsum(const void* x, int64_t rows, int C, int ld, int dtype, float* out, float* workspace, void* stream);
 

@@ -692,84 +692,3 @@ def test_trainer_with_multi_resolution_stft_loss():
     assert "stft" in le and np.isfinite(le["stft"]) and le["stft"] > 0
     assert abs(le["gen"] - (le["adv"] + le["fm"] + le["mel"] + le["stft"])) < 1e-3 * le["gen"]
     assert torch.equal(gg, ge) and lg == le
-
-
-def _masked_pair(shape, gen):
-    """dY and the layer output it is masked by (exact zeros, negatives and positives)"""
-    gy = torch.randn(*shape, generator=gen).to(torch.bfloat16)
-    y = torch.randn(*shape, generator=gen)
-    y[..., ::7] = 0.0
-    return gy, y.to(torch.bfloat16)
-
-
-@pytest.mark.parametrize("B,T,Ci,Co,K,s,g,pad", [
-    (2, 1000, 128, 128, 41, 2, 4, 20), (2, 777, 128, 256, 41, 2, 16, 20), (2, 64, 1024, 1024, 41, 1, 16, 20),
-    (4, 2731, 32, 128, 5, 3, 1, 2), (6, 100, 512, 1024, 5, 3, 1, 2), (2, 5, 1024, 1024, 5, 1, 1, 2),
-    (1, 4000, 1024, 1024, 5, 1, 1, 2), (2, 300, 8, 32, 5, 3, 1, 2), (2, 13, 128, 256, 41, 4, 16, 20)])
-def test_masked_dgrad_wgrad_bit_identical(B, T, Ci, Co, K, s, g, pad):
-    """The discriminators' leaky-ReLU backward folded into the dY staging (vo_conv1d xmask through
-    gan_ops._dgrad / the plain input-gradient conv, vo_conv1d_wgrad_masked with the fused bias)
-    equals the separate vo_lrelu_mask pass followed by the unmasked kernels, bit for bit."""
-    from visual_onoma_to_wave_amd import ops
-    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
-    gen = torch.Generator().manual_seed(B * T + Co + s)
-    x = torch.randn(B, T, Ci, generator=gen).to(torch.bfloat16).cuda()
-    w = (torch.randn(Co, Ci // g, K, generator=gen) / (Ci // g * K) ** 0.5).cuda()
-    T_out = (T + 2 * pad - K) // s + 1
-    gy, y = (t.cuda() for t in _masked_pair((B, T_out, Co), gen))
-    gz = ops.lrelu_mask(gy, y, 0.1)
-    spec = G.ConvSpec(K=K, pad=pad, stride=s, groups=g)
-    if spec.plain():
-        wd = ops.pack_dgrad_weight(w, torch.bfloat16)
-        kw = dict(Co=Ci, K=K, pad=K - 1 - pad, T_out=T, compute_dtype=torch.bfloat16)
-        want = ops.conv1d(gz, wd, None, **kw)
-        got = ops.conv1d(gy, wd, None, xmask=y, xmask_slope=0.1, **kw)
-    else:
-        want = G._dgrad(gz, w, spec, x, torch.bfloat16)
-        got = G._dgrad(gy, w, spec, x, torch.bfloat16, xmask=y, xmask_slope=0.1)
-    assert torch.equal(got, want)
-    ww, wb = ops.conv1d_wgrad(gz, x, K, S=s, pad=pad, groups=g, with_bias=True)
-    gw, gb = ops.conv1d_wgrad(gy, x, K, S=s, pad=pad, groups=g, with_bias=True, amask=y, mslope=0.1)
-    assert torch.equal(gw, ww) and torch.equal(gb, wb)
-
-
-def test_discriminator_mask_fold_bit_identical():
-    """MPD + MSD in bf16: the D-step parameter gradients and the G-step gradient wrt the generated
-    wav (adversarial + feature-matching losses) with the folded post-activation masks
-    (gan_ops.MASK_FOLD) equal those of the separate mask pass, bit for bit."""
-    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
-    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
-                                                                  discriminator_loss, feature_loss, generator_loss)
-    from visual_onoma_to_wave_amd.hifigan.train import _single
-    torch.manual_seed(3)
-    # eval: the spectral norm without its power iteration, so both runs see the same weights
-    mpd = MultiPeriodDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
-    msd = MultiScaleDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
-    y = torch.tanh(torch.randn(2, 8192) * 0.3).cuda()
-    yh = torch.tanh(torch.randn(2, 8192) * 0.3).cuda()
-    params = list(mpd.parameters()) + list(msd.parameters())
-
-    def run(fold):
-        G.MASK_FOLD = fold
-        r1, g1, _, _ = mpd(y, yh)
-        r2, g2, _, _ = msd(y, yh)
-        ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
-        gd = torch.autograd.grad(ld, params)
-        yg = yh.clone().requires_grad_(True)
-        _, fr_f = _single(mpd, y, False)
-        _, fr_s = _single(msd, y, False)
-        sg_f, fg_f = _single(mpd, yg, True)
-        sg_s, fg_s = _single(msd, yg, True)
-        lg = generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
-        (gw,) = torch.autograd.grad(lg, [yg])
-        return float(ld), gd, float(lg), gw
-
-    try:
-        ld0, gd0, lg0, gw0 = run(False)
-        ld1, gd1, lg1, gw1 = run(True)
-    finally:
-        G.MASK_FOLD = True
-    assert ld0 == ld1 and lg0 == lg1
-    for i, (a, b) in enumerate(zip(gd0, gd1)):
-        assert torch.equal(a, b), i
-    assert torch.equal(gw0, gw1)

@@ -42,7 +42,6 @@ class Conv1dDesc(ctypes.Structure):
         ("variant", c_int),
         ("stride", c_int), ("groups", c_int),
         ("workspace", c_void_p), ("workspace_bytes", ctypes.c_int64),
-        ("xmask", c_void_p), ("xmask_slope", c_float),
     ]
 
 
@@ -136,9 +135,6 @@ _SIGNATURES = {
     "vo_conv1d_wgrad_bias": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
                                      c_void_p, c_void_p]),
-    "vo_conv1d_wgrad_masked": (c_int, [c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_int, c_int, c_int,
-                                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
-                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_lrelu_mask": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, ctypes.c_int64, c_int, c_float,
                               c_void_p, c_int, c_void_p]),
     "vo_colsum_workspace_size": (c_int64, [c_int64, c_int]),

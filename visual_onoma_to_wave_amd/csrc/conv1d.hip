@@ -48,8 +48,6 @@ struct ConvArgs {
   int cig, cog;  // channels per group (in / out): grouped conv = block-diagonal packed weights
   float* partial;  // split reduction: fp32 partials [splits][B][T_out][Co] (null = off)
   int kcs;         // 32-channel chunks per split (grid z = split)
-  const void* xmask;  // XM kernels: x staged as x * (xmask > 0 ? 1 : xmask_slope) (x's layout)
-  float xmask_slope;
 };
 
 template <typename T> struct Raw8;  // 8 elements of T held in registers
@@ -314,11 +312,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // (issued one chunk ahead, they got one step to land); and the step barriers are bare s_barrier
 // (LDS writes drained by lgkmcnt): __syncthreads' workgroup release fence waits vmcnt(0) too.
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2, bool XM = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
-  // XM: the input is dY of a leaky-ReLU layer, masked by that layer's output as it is staged
-  static_assert(!XM || (sizeof(TIN) == 2 && sizeof(TC) == 2 && !GL && !RS), "conv1d XM: bf16 register staging only");
   constexpr int NT = WCO * WT * 64;
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -355,7 +351,6 @@ conv1d_kernel(ConvArgs a) {
   const int co_blk = blockIdx.y * BCO;
 
   const TIN* __restrict__ X = reinterpret_cast<const TIN*>(a.x) + (int64_t)b * a.xbs;
-  const TIN* __restrict__ XMK = XM ? reinterpret_cast<const TIN*>(a.xmask) + (int64_t)b * a.xbs : X;
   const TC* __restrict__ Wp = reinterpret_cast<const TC*>(a.w);
   // grouped conv: this block's output channels [co_blk, co_blk + BCO) read only input
   // channels [ci_lo, ci_hi) of their groups (32-aligned; the packed weights are
@@ -370,7 +365,7 @@ conv1d_kernel(ConvArgs a) {
     n_chunks = min(a.kcs, n_chunks - z0);
   }
   const int tsteps = (a.K + TPS - 1) / TPS;
-  const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE && !XM;
+  const bool raw_window = std::is_same<TIN, TC>::value && a.pre_act == VO_ACT_NONE;
   // prologue activation as one select: none -> slope 1, relu -> 0, lrelu -> slope
   const float pre_s = a.pre_act == VO_ACT_RELU ? 0.f : (a.pre_act == VO_ACT_LRELU ? a.pre_slope : 1.f);
   const int64_t tap_stride = (int64_t)a.Co * a.Ci;
@@ -406,7 +401,7 @@ conv1d_kernel(ConvArgs a) {
     wl[s] = t * BCO * P + Lds<TC>::template off<SHW>(col, q);
   }
 
-  Raw8<TIN> win_r[MAXV], win_m[XM ? MAXV : 1];
+  Raw8<TIN> win_r[MAXV];
   constexpr int NW = NT / 64;
   constexpr int NWW = SPLIT ? NW / 2 : NW;  // waves issuing the weight DMA
   constexpr int GLN = DMA ? (TPS * BCO * VPR) / (64 * NWW) : 1;  // DMA instructions per wave per step
@@ -498,7 +493,6 @@ conv1d_kernel(ConvArgs a) {
         if (c > 0) { win_r[s].zero(); continue; }
       }
       win_r[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
-      if constexpr (XM) win_m[s].load(XMK + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
     }
   };
   auto store_window = [&](int buf, int rb = 0, bool young = false) {
@@ -537,15 +531,8 @@ conv1d_kernel(ConvArgs a) {
       }
       float f[8];
       win_r[s].to_f32(f);
-      if constexpr (XM) {  // as vo_lrelu_mask: g * (m > 0 ? 1 : slope), rounded once when stored
-        float m[8];
-        win_m[s].to_f32(m);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = m[e] > 0.f ? f[e] : f[e] * a.xmask_slope;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
-      }
+      for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
       store8(dst, f);
     }
   };
@@ -757,7 +744,7 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2, bool XM = false>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -776,7 +763,6 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   a.tiles_per_b = (d->T_out + BT - 1) / BT;
   a.co_tiles = (d->Co + BCO - 1) / BCO;
   a.B = d->B;
-  a.xmask = d->xmask; a.xmask_slope = d->xmask_slope;
   const int groups = d->groups > 1 ? d->groups : 1;
   a.cig = d->Ci / groups;
   a.cog = d->Co / groups;
@@ -791,8 +777,8 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS, EJ, XM>
-                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S, false, false, 2, XM>;
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS, EJ>
+                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
   a.partial = nullptr;
   a.kcs = 0;
   int splits = 1;
@@ -899,28 +885,6 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }
 
-// dY staged through the leaky-ReLU mask (xmask): the discriminators' input gradients, stride 1 (the
-// strided layers' gradients are stride-1 phase convs), dense or grouped -- the tiles launch_disc and
-// launch_types pick for those shapes, bf16 in and out
-static int launch_masked(const vo_conv1d_desc* d, hipStream_t st) {
-  typedef bf16_t T;
-  const int groups = d->groups > 1 ? d->groups : 1;
-  const int cog = d->Co / groups;
-  const int64_t rows = (int64_t)d->B * d->T_out;
-  if (groups > 1 || d->Co <= 64) {
-    if (d->Co <= 32 || cog <= 32) return launch_cfg_s<T, T, T, 2, 1, 1, 4, 4, 0, 0, 0, 1, false, false, 2, true>(d, st);
-    if (d->Co <= 64 || cog <= 64) return launch_cfg_s<T, T, T, 4, 1, 1, 4, 4, 0, 0, 0, 1, false, false, 2, true>(d, st);
-    return launch_cfg_s<T, T, T, 4, 2, 2, 2, 2, 0, 0, 0, 1, false, false, 2, true>(d, st);
-  }
-  if (rows <= 2048) return launch_cfg_s<T, T, T, 2, 2, 2, 2, 2, 0, 0, 0, 1, false, false, 2, true>(d, st);
-  const int64_t t256 = (int64_t)d->B * ((d->T_out + 255) / 256) * (d->Co / 256);
-  if (d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128)
-    return launch_cfg_s<T, T, T, 4, 8, 4, 2, 2, 0, 0, 0, 1, false, false, 2, true>(d, st);  // 256 x 256
-  if (d->Co >= 512 && d->Co < 768 && d->Co % 128 == 0)
-    return launch_cfg_s<T, T, T, 4, 4, 2, 4, 2, 0, 0, 0, 1, false, false, 2, true>(d, st);  // 128 x 256
-  return launch_cfg_s<T, T, T, 4, 4, 2, 2, 2, 0, 0, 0, 1, false, false, 2, true>(d, st);    // 128 x 128
-}
-
 }  // namespace vo
 
 using namespace vo;
@@ -959,15 +923,6 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
     VO_CHECK_ARG(d->Co % 16 == 0 || d->Co == 80 || d->Co <= 32, "conv1d: unsupported Co %d", d->Co);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(const_cast<void*>(stream));
-  if (d->xmask) {
-    VO_CHECK_ARG(!d->transposed && d->variant == 0 && (d->stride <= 1) && d->pre_act == VO_ACT_NONE &&
-                     d->compute_dtype == VO_BF16 && d->x_dtype == VO_BF16 && d->y_dtype == VO_BF16 &&
-                     d->xmask_slope >= 0.f && d->xmask_slope <= 1.f,
-                 "conv1d: xmask needs a stride-1 bf16 conv without a prologue activation, slope in [0, 1]");
-    VO_CHECK_ARG(d->groups <= 1 || (d->Ci % d->groups == 0 && d->Co % d->groups == 0),
-                 "conv1d: Ci %d / Co %d not divisible by groups %d", d->Ci, d->Co, d->groups);
-    return launch_masked(d, st);
-  }
   if (d->transposed) {  // narrow upsamplers: the persistent streaming kernel (upsample.hip)
     int handled = 0;
     const int rc = vo_ups_try(d, st, &handled);

@@ -88,7 +88,7 @@ static const char* const kSymbols[] = {
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
     "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
-    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_conv1d_wgrad_masked", "vo_lrelu_mask", "vo_conv1d_workspace_size",
+    "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask", "vo_conv1d_workspace_size",
     "vo_bn_workspace_size", "vo_bn_train_fwd", "vo_bn_bwd", "vo_vfe_conv_workspace_size", "vo_vfe_conv_fwd",
     "vo_vfe_conv_bwd", "vo_stft_mel_bwd_workspace_size", "vo_stft_mel_bwd", "vo_period_fold_bwd", "vo_wav_cl8_bwd",
     "vo_avgpool_wav_bwd", "vo_weight_norm", "vo_weight_norm_bwd", "vo_pack_dgrad_phase", "vo_pack_batch", "vo_seq_remap", "vo_lrelu_mask_add", "vo_spectral_norm", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size", "vo_stft_mag",

@@ -45,8 +45,6 @@ struct WgradArgs {
   bool bias;  // bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
   int abl;  // timing ablation (wgrad_cfg 11): 2 = no loads
   int gpt;  // groups per tile (grouped convs with narrow groups, per-tap kernel): see wgrad_gpt
-  const void* amask;  // AM kernels: A is staged as A * (amask > 0 ? 1 : mslope) (amask: A's layout)
-  float mslope;
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
 // and B columns [g N, (g+1) N) and writes block g of the (groups, K, M, N) result
@@ -61,22 +59,10 @@ __device__ __forceinline__ uint32_t lrelu_pack(uint32_t w, float s) {
   const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
   return pk_bf16(lrelu_max(lo, s), lrelu_max(hi, s));
 }
-// leaky-ReLU backward of a packed bf16 pair by the sign of the layer output m: w * (m > 0 ? 1 : s),
-// rounded as vo_lrelu_mask rounds its output (the staged operand is bit-identical to the masked tensor)
-__device__ __forceinline__ uint32_t mask_pack(uint32_t w, uint32_t m, float s) {
-  const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
-  const float mlo = __uint_as_float(m << 16), mhi = __uint_as_float(m & 0xffff0000u);
-  return pk_bf16(mlo > 0.f ? lo : lo * s, mhi > 0.f ? hi : hi * s);
-}
-__device__ __forceinline__ u32x4_t mask_pack4(u32x4_t w, u32x4_t m, float s) {
-  return u32x4_t{mask_pack(w.x, m.x, s), mask_pack(w.y, m.y, s), mask_pack(w.z, m.z, s), mask_pack(w.w, m.w, s)};
-}
 
 // 4 waves as 2 x 2, each a 32 x 32 sub-tile = 2 x 2 MFMA tiles
-// AM (bf16): dY masked while it is staged (WgradArgs::amask)
-template <typename TC, bool AM = false>
+template <typename TC>
 __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
-  static_assert(!AM || sizeof(TC) == 2, "wgrad: the staged mask is bf16 only");
   constexpr int P = WgTile<TC>::PITCH;
   __shared__ __attribute__((aligned(16))) TC sa[WG_R * P];
   __shared__ __attribute__((aligned(16))) TC sb[WG_R * P];
@@ -92,7 +78,6 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   const int64_t r_begin = (int64_t)blockIdx.x * p.rows_per_split;
   const int64_t r_end = min(rows, r_begin + p.rows_per_split);
   const TC* A = reinterpret_cast<const TC*>(p.a) + (int64_t)grp * p.M;
-  const TC* Am = AM ? reinterpret_cast<const TC*>(p.amask) + (int64_t)grp * p.M : A;
   const TC* Bs = reinterpret_cast<const TC*>(p.bsrc) + (int64_t)grp * p.N;
   float* dw = p.part + (int64_t)blockIdx.x * p.n_tot;
   constexpr int EV = 16 / sizeof(TC);       // elements per 16-byte vector
@@ -112,7 +97,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 
   for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
     // ---- stage 64 rows of A (rows r0..) and of B (gathered rows of the same utterances)
-    u32x4_t va[NV], vb[NV], vm[AM ? NV : 1];
+    u32x4_t va[NV], vb[NV];
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       const int v = tid + s * 256;
@@ -128,7 +113,6 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
         va[s] = vb[s] = u32x4_t{(unsigned)tb, (unsigned)ma, 1u, 1u};
       } else {
         va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + ma);
-        if constexpr (AM) vm[s] = *reinterpret_cast<const u32x4_t*>(Am + ((int64_t)b * p.T_A + t) * p.lda + ma);
         vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + min(max(tb, 0), p.T_B - 1)) * p.ldb + nb);
       }
       if (!qok || m0 + c >= Mv) va[s] = u32x4_t{0u, 0u, 0u, 0u};
@@ -140,7 +124,6 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       const int v = tid + s * 256;
       const int r = v / VPR, c = (v % VPR) * EV;
       u32x4_t x = va[s], y = vb[s];
-      if constexpr (AM) x = mask_pack4(x, vm[s], p.mslope);
       if constexpr (sizeof(TC) == 2) {
         if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
         if (p.pre_b) y = u32x4_t{lrelu_pack(y.x, p.slope), lrelu_pack(y.y, p.slope), lrelu_pack(y.z, p.slope), lrelu_pack(y.w, p.slope)};
@@ -256,7 +239,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
 constexpr int WM_R = 64;       // rows per chunk
 constexpr int WM_MAXW = 128;   // window rows: 64 + (nk - 1) * dil <= 128
 
-template <int TM, int KG, bool AM = false>
+template <int TM, int KG>
 __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunks_per_b, int chunks_per_split,
                                                          int ntg) {
   constexpr int P = TM == 64 ? 72 : 48;  // pitch (elements): the 4 rows of a transposed read on distinct banks
@@ -277,7 +260,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
   const int c_begin = blockIdx.x * chunks_per_split;
   const int c_end = min(p.Bn * chunks_per_b, c_begin + chunks_per_split);
   const bf16_t* A = reinterpret_cast<const bf16_t*>(p.a) + (int64_t)grp * p.M;
-  const bf16_t* Am = AM ? reinterpret_cast<const bf16_t*>(p.amask) + (int64_t)grp * p.M : A;
   const bf16_t* Bs = reinterpret_cast<const bf16_t*>(p.bsrc) + (int64_t)grp * p.N;
   float* dw = p.part + (int64_t)blockIdx.x * p.n_tot;
 
@@ -293,18 +275,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
 
   // two register sets, alternated by the 2x-unrolled chunk loop: a chunk's loads are issued two
   // chunks of MFMAs before its LDS store (one chunk was too short to cover the load latency)
-  constexpr int NVA2 = AM ? 2 * NVA : NVA;  // AM: the mask vectors of the same A rows follow
-  u32x4_t va0[NVA2], vb0[NVB], va1[NVA2], vb1[NVB];
-  auto load = [&](int c, u32x4_t (&va)[NVA2], u32x4_t (&vb)[NVB]) {  // chunk c -> registers (unconditional
+  u32x4_t va0[NVA], vb0[NVB], va1[NVA], vb1[NVB];
+  auto load = [&](int c, u32x4_t (&va)[NVA], u32x4_t (&vb)[NVB]) {  // chunk c -> registers (unconditional
                                                                    // loads, clamped; zeroed when stored)
     const int b = c / chunks_per_b, t0 = (c - b * chunks_per_b) * WM_R;
 #pragma unroll
     for (int s = 0; s < NVA; ++s) {
       const int v = tid + s * 256, r = v / VPR, col = (v % VPR) * 8;
       const int t = min(t0 + r, p.T_A - 1);
-      const int64_t off = ((int64_t)b * p.T_A + t) * p.lda + min(m0 + col, p.M - 8);
-      va[s] = *reinterpret_cast<const u32x4_t*>(A + off);
-      if constexpr (AM) va[NVA + s] = *reinterpret_cast<const u32x4_t*>(Am + off);
+      va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + min(m0 + col, p.M - 8));
     }
     const int tb0 = t0 - p.pad + k0 * p.dil;
 #pragma unroll
@@ -314,7 +293,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
       vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + tb) * p.ldb + min(n0 + col, p.N - 8));
     }
   };
-  auto store = [&](int c, const u32x4_t (&va)[NVA2], const u32x4_t (&vb)[NVB]) {
+  auto store = [&](int c, const u32x4_t (&va)[NVA], const u32x4_t (&vb)[NVB]) {
     const int b = c / chunks_per_b, t0 = (c - b * chunks_per_b) * WM_R;
     (void)b;
 #pragma unroll
@@ -322,7 +301,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
       const int v = tid + s * 256, r = v / VPR, col = (v % VPR) * 8;
       u32x4_t x = va[s];
       if (t0 + r >= p.T_A || m0 + col >= p.M) x = u32x4_t{0u, 0u, 0u, 0u};
-      if constexpr (AM) x = mask_pack4(x, va[NVA + s], p.mslope);
       if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
       *reinterpret_cast<u32x4_t*>(sa + r * P + col) = x;
     }
@@ -585,11 +563,7 @@ extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, 
 template <int TM, int KG>
 static void wgrad_mt_launch(const WgradArgs& p, const MtPlan& pl, int groups, hipStream_t st) {
   const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
-  if (p.amask)
-    hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG, true>), dim3((unsigned)pl.splits, (unsigned)tiles, (unsigned)(pl.ntg * groups)),
-                       dim3(256), 0, st, p, pl.chunks_per_b, pl.cps, pl.ntg);
-  else
-    hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG>), dim3((unsigned)pl.splits, (unsigned)tiles, (unsigned)(pl.ntg * groups)),
+  hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG>), dim3((unsigned)pl.splits, (unsigned)tiles, (unsigned)(pl.ntg * groups)),
                      dim3(256), 0, st, p, pl.chunks_per_b, pl.cps, pl.ntg);
 }
 template <int TM>
@@ -613,12 +587,10 @@ static void wgrad_mt_dispatch(const WgradArgs& p, const MtPlan& pl, int groups, 
   }
 }
 
-static int wgrad_run(const void* a, const void* amask, float mslope, int lda, int T_A, const void* b, int ldb, int T_B,
-                     int B, int M, int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b, float slope,
-                     int dtype, float* dw, float* db, float* workspace, void* stream) {
+extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
+                                    int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
+                                    float slope, int dtype, float* dw, float* db, float* workspace, void* stream) {
   VO_CHECK_ARG(a && b && dw && workspace, "conv1d_wgrad: null pointer");
-  VO_CHECK_ARG(!amask || (dtype == VO_BF16 && !pre_a && mslope >= 0.f && mslope <= 1.f),
-               "conv1d_wgrad: the dY mask needs bf16 operands, pre_a off and a slope in [0, 1]");
   VO_CHECK_ARG(!db || !pre_a, "conv1d_wgrad: the fused bias gradient sums A as stored (pre_a must be off)");
   VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1 && groups >= 1, "conv1d_wgrad: bad sizes");
   const int ev = dtype == VO_BF16 ? 8 : 4;
@@ -635,7 +607,6 @@ static int wgrad_run(const void* a, const void* amask, float mslope, int lda, in
   p.n_tot = p.n_w + (db ? (int64_t)groups * M : 0);
   p.abl = vo_tune_get("wgrad_cfg") == 11 ? 2 : 0;  // 11: no loads (timing)
   p.gpt = 1;
-  p.amask = amask; p.mslope = mslope;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // stride-1 bf16 convs: the multi-tap kernel (wgrad_mt 1 = the per-tap kernel, A/B)
   // (K >= 2 and utterances of >= 8 whole chunks' worth: the per-utterance chunks of short sequences --
@@ -661,30 +632,12 @@ static int wgrad_run(const void* a, const void* amask, float mslope, int lda, in
   wgrad_plan(B, T_A, M, N, K, groups, &splits, &p.rows_per_split);
   VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");
   dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)zk);
-  if (dtype == VO_BF16 && amask)
-    hipLaunchKernelGGL((wgrad_kernel<bf16_t, true>), grid, dim3(256), 0, st, p);
-  else if (dtype == VO_BF16)
+  if (dtype == VO_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   wgrad_reduce_launch(workspace, (int)splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
   VO_RETURN_LAUNCH();
-}
-
-extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,
-                                    int N, int K, int S, int dil, int pad, int groups, int pre_a, int pre_b,
-                                    float slope, int dtype, float* dw, float* db, float* workspace, void* stream) {
-  return wgrad_run(a, nullptr, 0.f, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, groups, pre_a, pre_b, slope, dtype,
-                   dw, db, workspace, stream);
-}
-
-extern "C" int vo_conv1d_wgrad_masked(const void* a, const void* amask, float mslope, int lda, int T_A, const void* b,
-                                      int ldb, int T_B, int B, int M, int N, int K, int S, int dil, int pad, int groups,
-                                      int pre_b, float slope, int dtype, float* dw, float* db, float* workspace,
-                                      void* stream) {
-  VO_CHECK_ARG(amask, "conv1d_wgrad_masked: null mask");
-  return wgrad_run(a, amask, mslope, lda, T_A, b, ldb, T_B, B, M, N, K, S, dil, pad, groups, 0, pre_b, slope, dtype,
-                   dw, db, workspace, stream);
 }
 
 extern "C" int vo_conv1d_wgrad_grouped(const void* a, int lda, int T_A, const void* b, int ldb, int T_B, int B, int M,

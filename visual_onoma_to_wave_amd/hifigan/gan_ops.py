@@ -189,12 +189,11 @@ def _conv_fwd(x, w, b, res1, res2, spec, cdt, wkey=None):
                       stride=spec.stride, groups=spec.groups)
 
 
-def _dgrad(gz, w, spec, x, cdt, wkey=None, xmask=None, xmask_slope=0.0):
+def _dgrad(gz, w, spec, x, cdt, wkey=None):
     """Input gradient of a strided and/or grouped conv (dil 1) on the HIP conv kernel, by phase:
     input row i = S m + r receives taps k = k_r + S j (k_r = (r + pad) mod S) from output rows
     m + c_r - j, so each residue r is a stride-1 grouped conv over dY with those taps reversed and
-    the channel roles swapped, written to rows r, r + S, ... of dX (row-strided output view).
-    ``xmask``: dY is read through the leaky-ReLU mask of the layer output (see ConvFn.backward)."""
+    the channel roles swapped, written to rows r, r + S, ... of dX (row-strided output view)."""
     S, K, pad, g = spec.stride, spec.K, spec.pad, spec.groups
     if spec.dil != 1:
         raise NotImplementedError("strided / grouped input gradient with dilation")
@@ -205,8 +204,6 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None, xmask=None, xmask_slope=0.0):
     if ci_out > Ci and g != 1:
         raise NotImplementedError("strided / grouped input gradient: padded input channels with groups")
     gzp = _pad_channels(gz.to(cdt))
-    if xmask is not None and gzp.shape != xmask.shape:
-        raise ValueError("_dgrad: the dY mask must match dY")
     co_in = gzp.shape[-1]  # >= Co (Co = 1 padded to 8); extra channels multiply zero weights
     B, T_in = x.shape[0], x.shape[1]
     out = torch.empty((B, T_in, ci_out), dtype=x.dtype, device=x.device)
@@ -231,7 +228,7 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None, xmask=None, xmask_slope=0.0):
             return ops.pack_dgrad_phase(w, g, S, k_r, J, ci_out, co_in, cdt, out=out)
         wp = _cached(wkey, tag, build)
         ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,
-                   groups=g if ci_out == Ci else 1, xmask=xmask, xmask_slope=xmask_slope)
+                   groups=g if ci_out == Ci else 1)
     return out
 
 
@@ -248,10 +245,6 @@ def _ncw(t):
 
 
 RES_LINK = os.environ.get("VO_RES_LINK", "1") != "0"  # 0: autograd sums the residual gradients (A/B)
-# the post-activation leaky-ReLU backward of a conv (the discriminators' layers) applied by the input-
-# and weight-gradient kernels as they stage dY (vo_conv1d xmask, vo_conv1d_wgrad_masked) instead of a
-# vo_lrelu_mask pass; bit-identical (the staged values are the masked tensor's).  0: the separate pass
-MASK_FOLD = os.environ.get("VO_MASK_FOLD", "1") != "0"
 
 
 class ResLink:
@@ -300,28 +293,17 @@ class ConvFn(torch.autograd.Function):
         lk, role = ctx.link if ctx.link is not None else (None, None)
         if role == "res" and g_res1 is not None:  # the residual's gradient goes to the linked input conv
             lk.g, g_res1 = g_res1, None
-        ci = w.shape[0] if spec.transposed is not None else w.shape[1] * spec.groups
-        need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
-        g = spec.groups
-        grouped_ok = g == 1 or (spec.transposed is None and x.shape[-1] == ci and (ci // g) % 8 == 0
-                                and (w.shape[0] // g) % 8 == 0)
-        # the mask folded into the dY staging of every consumer below: the dgrad conv (plain or the
-        # strided / grouped phase convs) and the weight gradient with the bias summed in its launch
-        fold = (MASK_FOLD and spec.post == "lrelu" and spec.transposed is None and spec.co_pad is None
-                and cdt == torch.bfloat16 and gz.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
-                and y.shape == gz.shape and y.is_contiguous() and gz.is_contiguous() and gz.shape[-1] % 8 == 0
-                and (not need_x or spec.plain() or spec.dil == 1)
-                and (not (need_w or need_b) or (need_w and grouped_ok)))
-        ym = y if fold else None
-        if spec.post == "lrelu" and not fold:
+        if spec.post == "lrelu":
             gz = ops.lrelu_mask(gz, y, spec.post_slope)
         elif spec.post == "tanh":
             yf = y.float()
             gz = (gz.float() * (1.0 - yf * yf)).to(gz.dtype)
         if spec.co_pad is not None:
             gz = gz[..., : w.shape[0]].contiguous()
+        ci = w.shape[0] if spec.transposed is not None else w.shape[1] * spec.groups
         xin = x[..., :ci] if x.shape[-1] != ci else x
         gx = gw = gb = None
+        need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         ga = None
         if need_x and spec.plain():
             # cached per parameter version: a discriminator's next D step runs its backward at the
@@ -329,10 +311,10 @@ class ConvFn(torch.autograd.Function):
             wd = _cached(ctx.wkey, (spec, cdt, "dgrad_plain"), lambda: ops.pack_dgrad_weight(w, cdt))
             ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
                             pad=(spec.K - 1) * spec.dil - spec.pad, T_out=x.shape[1], out_dtype=x.dtype,
-                            compute_dtype=cdt, xmask=ym, xmask_slope=spec.post_slope if fold else 0.0)
+                            compute_dtype=cdt)
             need_x = False
         elif need_x and spec.transposed is None and spec.dil == 1:
-            ga = _dgrad(gz, w, spec, x, cdt, ctx.wkey, xmask=ym, xmask_slope=spec.post_slope if fold else 0.0)
+            ga = _dgrad(gz, w, spec, x, cdt, ctx.wkey)
             if ga.shape[-1] != ci:
                 ga = ga[..., :ci]
             need_x = False
@@ -343,6 +325,9 @@ class ConvFn(torch.autograd.Function):
             ga = ops.conv1d(gz.to(cdt), wc, None, Co=w.shape[0], K=spec.K, pad=p, stride=s, T_out=x.shape[1],
                             out_dtype=x.dtype, compute_dtype=cdt)
             need_x = False
+        g = spec.groups
+        grouped_ok = g == 1 or (spec.transposed is None and x.shape[-1] == ci and (ci // g) % 8 == 0
+                                and (w.shape[0] // g) % 8 == 0)
         if (need_w or need_b) and grouped_ok:
             # weight / bias gradient on MFMA (vo_conv1d_wgrad[_grouped], vo_colsum)
             gzc = _pad_channels(gz.to(x.dtype))
@@ -357,7 +342,7 @@ class ConvFn(torch.autograd.Function):
                     fuse_b = need_b and gz.dtype == x.dtype
                     dw = ops.conv1d_wgrad(gzc, _pad_channels(x) if g == 1 else x, spec.K, S=spec.stride,
                                           dil=spec.dil, pad=spec.pad, pre_b=spec.pre_slope, groups=g,
-                                          with_bias=fuse_b, amask=ym, mslope=spec.post_slope if fold else 0.0)
+                                          with_bias=fuse_b)
                     if fuse_b:
                         dw, db = dw
                         gb = db[: w.shape[0]]

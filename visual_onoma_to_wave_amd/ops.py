@@ -47,7 +47,7 @@ def _contig(t, name):
 def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_dtype=None,
            pre_act=ACT_NONE, pre_slope=0.0, post_act=ACT_NONE, post_slope=0.0, res1=None,
            res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None, variant=0,
-           tag=None, stride=1, groups=1, xmask=None, xmask_slope=0.0):
+           tag=None, stride=1, groups=1):
     """Channels-last conv: x (B, T_in, Ci) -> y (B, T_out, Co).
 
     ``w_packed``: [K][Co][Ci] in ``compute_dtype`` (see pack_conv_weight).
@@ -55,8 +55,6 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     ConvTranspose1d; then Co = s*C_out, K = 2, pad = 1 and y is (B, s*T_in, C_out).
     ``stride`` / ``groups``: strided and grouped convs (HiFi-GAN discriminators); grouped
     weights are packed dense with zeros outside the diagonal blocks (pack_conv_weight groups=).
-    ``xmask`` (x's shape and strides, bf16): x is read as x * (xmask > 0 ? 1 : xmask_slope) -- dY of
-    a leaky-ReLU layer masked by that layer's output while it is staged (stride-1 bf16 convs).
     """
     if x.dim() == 2:
         x = x.unsqueeze(0)
@@ -110,12 +108,6 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
     d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
     d.stride, d.groups = stride, groups
-    if xmask is not None:
-        if xmask.dim() == 2:
-            xmask = xmask.unsqueeze(0)
-        if xmask.shape != x.shape or xmask.stride() != x.stride() or xmask.dtype != x.dtype:
-            raise ValueError("conv1d: xmask must match x (shape, strides, dtype)")
-        d.xmask, d.xmask_slope = xmask.data_ptr(), float(xmask_slope)
     ws = None
     if compute_dtype == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
         # split-reduction scratch for the short fp32 convs (stream-ordered: freed after enqueue)
@@ -1015,14 +1007,12 @@ def char_features(energy, fstats, durations, n_bins):
 
 # ----------------------------------------------------------------------------- training backward
 
-def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1, with_bias=False,
-                 amask=None, mslope=0.0):
+def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1, with_bias=False):
     """Weight gradient on MFMA (vo_conv1d_wgrad).  Conv1d: a = dY (B, T_out, Co), b = x (B, T_in, Ci)
     -> dW (Co, Ci / groups, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY
     (B, T_up, Co) -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand
     (None = identity).  with_bias (conv form): also the bias gradient, column sums of a, from the
-    same launch (vo_conv1d_wgrad_bias) -> (dW, db).  ``amask`` (a's shape, bf16): a is read as
-    a * (amask > 0 ? 1 : mslope), the bias gradient sums those values (vo_conv1d_wgrad_masked)."""
+    same launch (vo_conv1d_wgrad_bias) -> (dW, db)."""
     _contig(a, "a")
     _contig(b, "b")
     if a.dtype != b.dtype:
@@ -1042,14 +1032,6 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
-    if amask is not None:
-        _contig(amask, "amask")
-        if amask.shape != a.shape or amask.dtype != a.dtype or pre_a is not None or transposed:
-            raise ValueError("conv1d_wgrad: amask must match a (conv form, no pre_a)")
-        _lib.check(L.vo_conv1d_wgrad_masked(_ptr(a), _ptr(amask), float(mslope), M, T_A, _ptr(b), N, T_B, B, mg, ng,
-                                            K, S, dil, pad, groups, int(pre_b is not None), float(slope), vo_dtype(a),
-                                            _ptr(w), _ptr(db), _ptr(ws), _stream(a)), "vo_conv1d_wgrad_masked")
-        return (w, db) if with_bias else w
     _lib.check(L.vo_conv1d_wgrad_bias(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K, S, dil, pad, groups,
                                       int(pre_a is not None), int(pre_b is not None), float(slope), vo_dtype(a),
                                       _ptr(w), _ptr(db), _ptr(ws), _stream(a)), "vo_conv1d_wgrad")
