@@ -375,7 +375,8 @@ int vo_weight_norm_bwd(int n, const void* const* v, const void* const* g, const 
  * forward; the HiFi-GAN V1 MSD's first scale in C5) for n layers per call.  Layer: W = weight_orig
  * (rows x L fp32), buffers u (rows) / v (L) updated in place when power != 0 (v = normalize(W^T u),
  * u = normalize(W v), normalize(x) = x / max(|x|, eps)), copies of the u / v used written to
- * u_out / v_out, sigma = u . W v, w = W / sigma; vraw (L) and s (rows) are scratch.  Replaces the
+ * u_out / v_out, sigma = u . W v, w = W / sigma; vraw (L) and s (rows) are scratch, and so is w
+ * until it is written (it must not alias W).  Replaces the
  * per-layer PyTorch hook (two gemv, norms, clamps, divides, clones and a dot per layer). */
 typedef struct vo_sn_layer {
   const float* W;

@@ -3,7 +3,9 @@
 // HiFi-GAN V1 MSD, config C5) for MANY layers per launch.  PyTorch's hook ran ~13 kernels per layer
 // and forward (two rocBLAS gemv, norms, clamps, divides, clones, a dot): 8 layers x 3 discriminator
 // passes per C5 step.  Here five launches cover every layer of a pass:
-//   1. vraw = W^T u           one thread per column, 4 waves over interleaved rows, LDS sum in order
+//   1. vraw = W^T u           one thread per column over a 64-row slab per workgroup (the partial
+//                             sums of the slabs in w, the output's own storage), then the slabs
+//                             added in order per column
 //   2. s = W vraw / max(|vraw|, eps)   one wave per row (|vraw| summed in a fixed order per block)
 //   3. per layer: u = s / max(|s|, eps), sigma = u . s, v = vraw / max(|vraw|, eps)  (buffers + copies)
 //   4. w = W / sigma
@@ -42,19 +44,38 @@ __device__ __forceinline__ int sn_layer(const SnArgs& a, int b) {
   return table_find(a.blk0, a.n, b);
 }
 
-// 1. vraw[c] = sum_r W[r][c] u[r]: 64 columns per workgroup, wave w sums rows w, w + 4, ...
+// 1a. slab sums: workgroup (column block cb, slab sp) sums rows [64 sp, 64 sp + 64) of 64 columns,
+// wave w rows 64 sp + w, + 4, ... -> w[sp][c] (scratch: the slabs of a layer, rows / 64 x L floats,
+// fit in its rows x L output, written only by step 4).  The first version ran one workgroup per 64
+// columns over every row: 80 workgroups for the MSD's 1024 x 5120 layer, 111 us per pass.
+constexpr int SN_SLAB = 64;
 __global__ void __launch_bounds__(256) sn_wtu_kernel(SnArgs a) {
   __shared__ float part[4][64];
   const int li = sn_layer(a, blockIdx.x);
   const SnLayer L = a.l[li];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = (blockIdx.x - a.blk0[li]) * 64 + lane;
+  const int ncb = (L.L + 63) / 64, b = blockIdx.x - a.blk0[li];
+  const int sp = b / ncb, c = (b - sp * ncb) * 64 + lane;
+  const int r1 = min(L.rows, (sp + 1) * SN_SLAB);
   float acc = 0.f;
   if (c < L.L)
-    for (int r = wv; r < L.rows; r += 4) acc += L.W[(int64_t)r * L.L + c] * L.u[r];
+#pragma unroll 4
+    for (int r = sp * SN_SLAB + wv; r < r1; r += 4) acc += L.W[(int64_t)r * L.L + c] * L.u[r];
   part[wv][lane] = acc;
   __syncthreads();
-  if (wv == 0 && c < L.L) L.vraw[c] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (wv == 0 && c < L.L) L.w[(int64_t)sp * L.L + c] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+// 1b. vraw[c] = the slab sums of column c added in slab order
+__global__ void __launch_bounds__(256) sn_vsum_kernel(SnArgs a) {
+  const int li = sn_layer(a, blockIdx.x);
+  const SnLayer L = a.l[li];
+  const int c = (blockIdx.x - a.blk0[li]) * 256 + threadIdx.x;
+  if (c >= L.L) return;
+  const int ns = (L.rows + SN_SLAB - 1) / SN_SLAB;
+  float v = 0.f;
+  for (int sp = 0; sp < ns; ++sp) v += L.w[(int64_t)sp * L.L + c];
+  L.vraw[c] = v;
 }
 
 __device__ __forceinline__ float sn_block_sumsq(const float* x, int n, float* red) {
@@ -67,13 +88,13 @@ __device__ __forceinline__ float sn_block_sumsq(const float* x, int n, float* re
   return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// 2. s[r] = (W[r] . vraw) / nv, one wave per row, 4 rows per workgroup
+// 2. s[r] = W[r] . vraw (divided by nv = max(|vraw|, eps) in step 3, which computes nv anyway: the
+// first version had every workgroup of this kernel re-reduce |vraw|), one wave per row, 4 rows per
+// workgroup
 __global__ void __launch_bounds__(256) sn_wv_kernel(SnArgs a) {
-  __shared__ float red[4];
   const int li = sn_layer(a, blockIdx.x);
   const SnLayer L = a.l[li];
   const float* vr = a.power ? L.vraw : L.v;
-  const float nv = a.power ? fmaxf(sqrtf(sn_block_sumsq(vr, L.L, red)), a.eps) : 1.f;
   const int lane = threadIdx.x & 63;
   const int r = (blockIdx.x - a.blk0[li]) * 4 + (threadIdx.x >> 6);
   if (r >= L.rows) return;
@@ -81,7 +102,7 @@ __global__ void __launch_bounds__(256) sn_wv_kernel(SnArgs a) {
   float acc = 0.f;
   for (int c = lane; c < L.L; c += 64) acc += row[c] * vr[c];
   acc = wave_sum(acc);
-  if (lane == 0) L.s[r] = acc / nv;
+  if (lane == 0) L.s[r] = acc;
 }
 
 // 3. one workgroup per layer: u, sigma, v
@@ -90,8 +111,10 @@ __global__ void __launch_bounds__(256) sn_finish_kernel(SnArgs a) {
   const SnLayer L = a.l[blockIdx.x];
   float dot;
   if (a.power) {
-    const float nu = fmaxf(sqrtf(sn_block_sumsq(L.s, L.rows, red)), a.eps);
     const float nv = fmaxf(sqrtf(sn_block_sumsq(L.vraw, L.L, red)), a.eps);
+    for (int i = threadIdx.x; i < L.rows; i += 256) L.s[i] = L.s[i] / nv;  // s = W v, v = vraw / nv
+    __syncthreads();
+    const float nu = fmaxf(sqrtf(sn_block_sumsq(L.s, L.rows, red)), a.eps);
     float d = 0.f;
     for (int i = threadIdx.x; i < L.rows; i += 256) {
       const float u = L.s[i] / nu;
@@ -155,6 +178,7 @@ extern "C" int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float
                    "spectral_norm: layer %d: null pointer", i0 + i);
       VO_CHECK_ARG(s.rows > 0 && s.L > 0 && (int64_t)s.rows * s.L < (1LL << 31),
                    "spectral_norm: layer %d: bad size", i0 + i);
+      VO_CHECK_ARG(s.w != s.W, "spectral_norm: layer %d: w must not alias W (it holds the W^T u slab sums)", i0 + i);
       a.l[i] = SnLayer{s.W, s.u, s.v, s.u_out, s.v_out, s.vraw, s.s, s.sigma, s.w, s.rows, s.L};
     }
     auto launch = [&](void (*k)(SnArgs), int (*blocks)(const SnLayer&)) -> int {
@@ -173,7 +197,13 @@ extern "C" int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float
       return VO_OK;
     };
     int rc;
-    if (a.power && (rc = launch(sn_wtu_kernel, [](const SnLayer& l) { return (l.L + 63) / 64; })) != VO_OK) return rc;
+    if (a.power) {
+      if ((rc = launch(sn_wtu_kernel, [](const SnLayer& l) {
+             return (l.L + 63) / 64 * ((l.rows + SN_SLAB - 1) / SN_SLAB);
+           })) != VO_OK)
+        return rc;
+      if ((rc = launch(sn_vsum_kernel, [](const SnLayer& l) { return (l.L + 255) / 256; })) != VO_OK) return rc;
+    }
     if ((rc = launch(sn_wv_kernel, [](const SnLayer& l) { return (l.rows + 3) / 4; })) != VO_OK) return rc;
     hipLaunchKernelGGL(sn_finish_kernel, dim3((unsigned)a.n), dim3(256), 0, st, a);
     if ((rc = launch(sn_scale_kernel, [](const SnLayer& l) {
