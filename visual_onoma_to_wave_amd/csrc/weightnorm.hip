@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) weight_norm_kernel(WnArgs a) {
   float ss = 0.f, dot = 0.f;
   const float* dw = BWD ? L.dw + base : nullptr;
   if (vec) {
+#pragma unroll 4  // several row loads in flight per wave (the loop was latency-bound)
     for (int i = lane * 4; i < len; i += 256) {
       const float4 x = *reinterpret_cast<const float4*>(v + i);
       ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
@@ -71,6 +72,7 @@ __global__ void __launch_bounds__(256) weight_norm_kernel(WnArgs a) {
   if constexpr (!BWD) {
     float* w = L.w + base;
     if (vec) {
+#pragma unroll 4
       for (int i = lane * 4; i < len; i += 256) {
         const float4 x = *reinterpret_cast<const float4*>(v + i);
         *reinterpret_cast<float4*>(w + i) = make_float4(x.x * s, x.y * s, x.z * s, x.w * s);
@@ -84,6 +86,7 @@ __global__ void __launch_bounds__(256) weight_norm_kernel(WnArgs a) {
     const float c = dot / ss;
     float* dv = L.dv + base;
     if (vec) {
+#pragma unroll 4
       for (int i = lane * 4; i < len; i += 256) {
         const float4 x = *reinterpret_cast<const float4*>(v + i);
         const float4 d = *reinterpret_cast<const float4*>(dw + i);
