@@ -352,6 +352,17 @@ int vo_pack_batch(int n, const VoPackJob* jobs, int dst_dtype, void* stream);
  * the discriminators' short period columns (hifigan/gan_ops._conv_joined) and its adjoint. */
 int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_t dst_rows, int row_bytes, int Td,
                  int64_t Ss, int lo, int hi, int shift, void* stream);
+/* One or two remaps in one launch (rows of whole 16-byte units).  Job: dst row r (n = r / Td, t =
+ * r mod Td) = src row n Ss + t + shift [+ src2 row n Ss2 + t + shift2, added in dtype (bf16 / fp32)
+ * when src2 is non-NULL] for lo <= t < hi, else zeros; src_rows / src2_rows bound the reads.  One
+ * joined discriminator conv feeding the next: the split output and the next joined input from one
+ * read, and the backward's two gathers plus autograd's add of them (hifigan/gan_ops.RejoinFn). */
+typedef struct vo_remap_job {
+  const void* src; const void* src2; void* dst;
+  int64_t src_rows, src2_rows, dst_rows, Ss, Ss2;
+  int Td, lo, hi, shift, shift2;
+} VoRemapJob;
+int vo_seq_remap2(int n, const VoRemapJob* jobs, int row_bytes, int dtype, void* stream);
 int vo_period_fold(const float* wav, int B, int T, int P, void* out, int dtype, void* stream);
 int vo_wav_cl8(const float* wav, int64_t n, void* out, int dtype, void* stream);
 int vo_avgpool_wav(const float* x, int B, int T, float* y, void* stream);

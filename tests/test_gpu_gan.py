@@ -692,3 +692,66 @@ def test_trainer_with_multi_resolution_stft_loss():
     assert "stft" in le and np.isfinite(le["stft"]) and le["stft"] > 0
     assert abs(le["gen"] - (le["adv"] + le["fm"] + le["mel"] + le["stft"])) < 1e-3 * le["gen"]
     assert torch.equal(gg, ge) and lg == le
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_seq_remap2_two_jobs_and_add(dt):
+    """vo_seq_remap2: two remaps in one launch equal vo_seq_remap of each; a job with a second source
+    equals the two gathers added in the dtype (autograd's add)."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(5)
+    N, S_out, T, pad, S_in, C = 7, 13, 11, 2, 15, 64
+    yj = torch.randn(N * S_out, C, generator=g).to(dt).cuda()
+    y, xj = ops.seq_remap2([dict(src=yj, dst_rows=N * T, Td=T, Ss=S_out, lo=0, hi=T, shift=0),
+                            dict(src=yj, dst_rows=N * S_in, Td=S_in, Ss=S_out, lo=pad, hi=pad + T, shift=-pad)])
+    assert torch.equal(y, ops.seq_remap(yj, N * T, T, S_out, 0, T, 0))
+    assert torch.equal(xj, ops.seq_remap(yj, N * S_in, S_in, S_out, pad, pad + T, -pad))
+    gy = torch.randn(N * T, C, generator=g).to(dt).cuda()
+    gx = torch.randn(N * S_in, C, generator=g).to(dt).cuda()
+    (got,) = ops.seq_remap2([dict(src=gy, Ss=T, shift=0, src2=gx, Ss2=S_in, shift2=pad, dst_rows=N * S_out, Td=S_out,
+                                  lo=0, hi=T)])
+    a = ops.seq_remap(gy, N * S_out, S_out, T, 0, T, 0)
+    b = ops.seq_remap(ops.seq_remap(gx, N * T, T, S_in, 0, T, pad), N * S_out, S_out, T, 0, T, 0)
+    assert torch.equal(got, a + b)
+
+
+def test_discriminator_rejoin_bit_identical():
+    """MPD + MSD in bf16 with the consecutive joined convs handing their joined outputs over
+    (gan_ops.RejoinFn) against split + join per layer: scores, feature maps, the D-step parameter
+    gradients and the G-step gradient wrt the generated wav, bit for bit."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
+                                                                  discriminator_loss, feature_loss, generator_loss)
+    from visual_onoma_to_wave_amd.hifigan.train import _single
+    torch.manual_seed(4)
+    mpd = MultiPeriodDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    msd = MultiScaleDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    y = torch.tanh(torch.randn(8, 8192) * 0.3).cuda()
+    yh = torch.tanh(torch.randn(8, 8192) * 0.3).cuda()
+    params = list(mpd.parameters()) + list(msd.parameters())
+
+    def run(rejoin):
+        G.REJOIN = rejoin
+        r1, g1, f1, _ = mpd(y, yh)
+        r2, g2, _, _ = msd(y, yh)
+        ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
+        gd = torch.autograd.grad(ld, params)
+        yg = yh.clone().requires_grad_(True)
+        _, fr_f = _single(mpd, y, False)
+        _, fr_s = _single(msd, y, False)
+        sg_f, fg_f = _single(mpd, yg, True)
+        sg_s, fg_s = _single(msd, yg, True)
+        lg = generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
+        (gw,) = torch.autograd.grad(lg, [yg])
+        return [t.detach() for t in r1 + g1 + [f for fs in f1 for f in fs]], gd, float(lg), gw
+
+    try:
+        o0, gd0, lg0, gw0 = run(False)
+        o1, gd1, lg1, gw1 = run(True)
+    finally:
+        G.REJOIN = True
+    assert len(o0) == len(o1) and all(torch.equal(a, b) for a, b in zip(o0, o1))
+    assert lg0 == lg1
+    for i, (a, b) in enumerate(zip(gd0, gd1)):
+        assert torch.equal(a, b), i
+    assert torch.equal(gw0, gw1)

@@ -52,6 +52,13 @@ class PackJob(ctypes.Structure):
                              "tstep", "src_rows")]
 
 
+class RemapJob(ctypes.Structure):
+    """VoRemapJob (include/vonoma.h, vo_seq_remap2)."""
+    _fields_ = [("src", c_void_p), ("src2", c_void_p), ("dst", c_void_p)] + [
+        (f, ctypes.c_int64) for f in ("src_rows", "src2_rows", "dst_rows", "Ss", "Ss2")] + [
+        (f, c_int) for f in ("Td", "lo", "hi", "shift", "shift2")]
+
+
 class SnLayer(ctypes.Structure):
     """VoSnLayer (include/vonoma.h, vo_spectral_norm)."""
     _fields_ = [(f, c_void_p) for f in ("W", "u", "v", "u_out", "v_out", "vraw", "s", "sigma", "w")] + [
@@ -156,6 +163,7 @@ _SIGNATURES = {
                                   c_float, c_void_p, c_int, c_void_p]),
     "vo_spectral_norm": (c_int, [c_int, c_void_p, c_int, c_float, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),
+    "vo_seq_remap2": (c_int, [c_int, c_void_p, c_int, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_weight_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),

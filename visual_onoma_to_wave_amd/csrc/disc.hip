@@ -196,6 +196,58 @@ __global__ void __launch_bounds__(256) seq_remap_kernel(const U* __restrict__ sr
   }
 }
 
+// Two remaps in one launch (grid y = job), and a job may add a second gathered source (same
+// row map, its own sequence stride / shift) in the tensor's dtype: where one joined conv feeds the
+// next (gan_ops.RejoinFn) the forward writes the split output and the next joined input from one
+// read of the joined output, and the backward adds the two gradients as it gathers them (bit for
+// bit autograd's bf16 / fp32 add of the split and join adjoints, which were 2-3 launches).
+struct RemapJob {
+  const void* src; const void* src2; void* dst;
+  int64_t dst_rows, Ss, Ss2;
+  int Td, lo, hi, shift, shift2;
+};
+struct RemapArgs { RemapJob j[2]; int uv; };
+
+template <int DT>  // 16 bytes of bf16 (DT 1) or fp32 (DT 2) added, rounded as the dtype's add
+__device__ __forceinline__ uint4 add16(uint4 a, uint4 b) {
+  if constexpr (DT == 1) {
+    const uint32_t x[4] = {a.x, a.y, a.z, a.w}, y[4] = {b.x, b.y, b.z, b.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = pk_bf16(__uint_as_float(x[i] << 16) + __uint_as_float(y[i] << 16),
+                     __uint_as_float(x[i] & 0xffff0000u) + __uint_as_float(y[i] & 0xffff0000u));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+    return make_uint4(__float_as_uint(__uint_as_float(a.x) + __uint_as_float(b.x)),
+                      __float_as_uint(__uint_as_float(a.y) + __uint_as_float(b.y)),
+                      __float_as_uint(__uint_as_float(a.z) + __uint_as_float(b.z)),
+                      __float_as_uint(__uint_as_float(a.w) + __uint_as_float(b.w)));
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) seq_remap2_kernel(RemapArgs a) {
+  const RemapJob& J = a.j[blockIdx.y];
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(J.src);
+  const uint4* __restrict__ src2 = reinterpret_cast<const uint4*>(J.src2);
+  uint4* __restrict__ dst = reinterpret_cast<uint4*>(J.dst);
+  const int uv = a.uv;
+  const int64_t n_units = J.dst_rows * uv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_units; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / uv;
+    const int c = (int)(i - r * uv);
+    const int64_t n = r / J.Td;
+    const int t = (int)(r - n * J.Td);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (t >= J.lo && t < J.hi) {
+      v = src[(n * J.Ss + t + J.shift) * uv + c];
+      if (src2) v = add16<DT>(v, src2[(n * J.Ss2 + t + J.shift2) * uv + c]);
+    }
+    dst[i] = v;
+  }
+}
+
 // wav (B, T) fp32 -> (B * P, H, 8) channels-last, H = ceil(T / P): row h of column c holds the
 // reflect-padded sample h * P + c in channel 0 (channels 1..7 zero)
 template <typename TD>
@@ -624,6 +676,42 @@ extern "C" int vo_seq_remap(const void* src, int64_t src_rows, void* dst, int64_
   else
     hipLaunchKernelGGL(seq_remap_kernel<uint32_t>, g, dim3(256), 0, st, (const uint32_t*)src, (uint32_t*)dst,
                        dst_rows, uv, Td, Ss, lo, hi, shift);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_seq_remap2(int n, const VoRemapJob* jobs, int row_bytes, int dtype, void* stream) {
+  VO_CHECK_ARG(n >= 1 && n <= 2 && jobs, "seq_remap2: 1 or 2 jobs");
+  VO_CHECK_ARG(row_bytes > 0 && row_bytes % 16 == 0 && (dtype == VO_BF16 || dtype == VO_F32),
+               "seq_remap2: rows of whole 16-byte units (got %d bytes), bf16 or fp32", row_bytes);
+  RemapArgs a;
+  a.uv = row_bytes / 16;
+  int64_t units = 0;
+  for (int i = 0; i < n; ++i) {
+    const VoRemapJob& s = jobs[i];
+    VO_CHECK_ARG(s.src && s.dst && s.src != s.dst && s.src2 != s.dst, "seq_remap2: job %d: null or aliased pointers", i);
+    VO_CHECK_ARG(((reinterpret_cast<uintptr_t>(s.src) | reinterpret_cast<uintptr_t>(s.dst) |
+                   reinterpret_cast<uintptr_t>(s.src2)) & 15) == 0, "seq_remap2: job %d: pointers not 16-byte aligned", i);
+    VO_CHECK_ARG(s.dst_rows >= 0 && s.Td >= 1 && s.Ss >= 0 && s.Ss2 >= 0 && 0 <= s.lo && s.lo <= s.hi && s.hi <= s.Td,
+                 "seq_remap2: job %d: bad layout", i);
+    if (s.dst_rows > 0 && s.lo < s.hi) {  // every row read lies in its source
+      const int64_t n_last = (s.dst_rows - 1) / s.Td;
+      const int t_hi = (int)std::min<int64_t>(s.hi, n_last == 0 ? s.dst_rows : s.Td) - 1;
+      VO_CHECK_ARG(s.lo + s.shift >= 0 && n_last * s.Ss + t_hi + s.shift < s.src_rows,
+                   "seq_remap2: job %d: reads outside the %lld source rows", i, (long long)s.src_rows);
+      VO_CHECK_ARG(!s.src2 || (s.lo + s.shift2 >= 0 && n_last * s.Ss2 + t_hi + s.shift2 < s.src2_rows),
+                   "seq_remap2: job %d: reads outside the %lld rows of the second source", i, (long long)s.src2_rows);
+    }
+    a.j[i] = RemapJob{s.src, s.src2, s.dst, s.dst_rows, s.Ss, s.Ss2, s.Td, s.lo, s.hi, s.shift, s.shift2};
+    units = std::max<int64_t>(units, s.dst_rows * a.uv);
+  }
+  if (n == 1) a.j[1] = a.j[0];
+  if (units == 0) return VO_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g((unsigned)grid_for(units), (unsigned)n);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(seq_remap2_kernel<1>, g, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(seq_remap2_kernel<2>, g, dim3(256), 0, st, a);
   VO_RETURN_LAUNCH();
 }
 

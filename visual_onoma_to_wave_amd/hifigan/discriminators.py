@@ -152,11 +152,8 @@ class DiscriminatorP(_DiscBase):
         if W is None:
             W = _prepare(self, [layers], wav.requires_grad)
         x = G.PeriodFoldFn.apply(wav, self.period, adt)
-        fmap = []
-        for m, sp, _ in layers:
-            x = G.conv(x, _w(m, W)[..., 0], m.bias, sp, cdt, wkey=G.weight_key(m))
-            fmap.append(x)
-        score = x[..., 0].contiguous()
+        fmap = G.conv_layers(x, [(_w(m, W)[..., 0], m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
+        score = fmap[-1][..., 0].contiguous()
         fmap[-1] = score
         return score, fmap
 
@@ -218,11 +215,8 @@ class DiscriminatorS(_DiscBase):
         if W is None:
             W = _prepare(self, [layers], wav.requires_grad)
         x = G.WavCl8Fn.apply(wav, adt)
-        fmap = []
-        for m, sp, _ in layers:
-            x = G.conv(x, _w(m, W), m.bias, sp, cdt, wkey=G.weight_key(m))
-            fmap.append(x)
-        score = x[..., 0].contiguous()
+        fmap = G.conv_layers(x, [(_w(m, W), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
+        score = fmap[-1][..., 0].contiguous()
         fmap[-1] = score
         return score, fmap
 

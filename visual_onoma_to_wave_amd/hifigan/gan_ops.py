@@ -429,20 +429,95 @@ class SplitSeqFn(torch.autograd.Function):
         return ops.seq_remap(g.contiguous(), R, S_out, T_out, 0, T_out, 0).view(1, R, C), None, None, None
 
 
-def _conv_joined(x, w, b, spec, cdt, wkey):
+REJOIN = os.environ.get("VO_REJOIN", "1") != "0"  # 0: split + join between consecutive joined convs (A/B)
+
+
+class RejoinFn(torch.autograd.Function):
+    """One joined conv feeding the next: (1, R, C) joined output -> ((N, T, C) its split output, (1,
+    N S_in, C) the next conv's joined input, each sequence at offset ``pad`` of its S_in rows) in one
+    vo_seq_remap2 launch; the backward gathers both gradients and adds them in the same launch (the
+    split and join adjoints plus autograd's add of the two, bit for bit)."""
+
+    @staticmethod
+    def forward(ctx, yj, N, S_out, T, pad, S_in):
+        C = yj.shape[-1]
+        ctx.dims = (yj.shape[1], N, S_out, T, pad, S_in)
+        y, xj = ops.seq_remap2([dict(src=yj, dst_rows=N * T, Td=T, Ss=S_out, lo=0, hi=T, shift=0),
+                                dict(src=yj, dst_rows=N * S_in, Td=S_in, Ss=S_out, lo=pad, hi=pad + T, shift=-pad)])
+        return y.view(N, T, C), xj.view(1, N * S_in, C)
+
+    @staticmethod
+    def backward(ctx, gy, gxj):
+        R, N, S_out, T, pad, S_in = ctx.dims
+        job = dict(dst_rows=R, Td=S_out, lo=0, hi=T)
+        if gy is not None:
+            job.update(src=gy.contiguous(), Ss=T, shift=0)
+            if gxj is not None:
+                job.update(src2=gxj.contiguous(), Ss2=S_in, shift2=pad)
+        elif gxj is not None:
+            job.update(src=gxj.contiguous(), Ss=S_in, shift=pad)
+        else:
+            return None, None, None, None, None, None
+        (g,) = ops.seq_remap2([job])
+        return g.view(1, R, g.shape[-1]), None, None, None, None, None
+
+
+def _join_plan(spec, T):
+    """(T_out, S_out, S_in) of a joined conv over sequences of T rows: output slots and input rows
+    per sequence (its padding, then zeros)."""
+    S_out = -(-(T + 2 * spec.pad) // spec.stride)
+    return out_len(spec, T), S_out, spec.stride * S_out
+
+
+def _join_input(x, spec):
     N, T, C = x.shape
-    st = spec.stride
-    T_out = out_len(spec, T)
-    S_out = -(-(T + 2 * spec.pad) // st)     # output slots per sequence
-    S_in = st * S_out                         # input rows per sequence: its padding, then zeros
+    _, _, S_in = _join_plan(spec, T)
     if (C * x.element_size()) % 4:  # vo_seq_remap moves whole 4-byte words
-        xj = F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
-    else:
-        xj = JoinSeqFn.apply(x, spec.pad, S_in)
-    yj = ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey)  # slot u S_out + t <- rows u S_in + st t + k
+        return F.pad(x, (0, 0, spec.pad, S_in - T - spec.pad)).reshape(1, N * S_in, C)
+    return JoinSeqFn.apply(x, spec.pad, S_in)
+
+
+def _split_output(yj, N, S_out, T_out):
     if (yj.shape[-1] * yj.element_size()) % 4:
         return F.pad(yj, (0, 0, 0, N * S_out - yj.shape[1])).reshape(N, S_out, -1)[:, :T_out].contiguous()
     return SplitSeqFn.apply(yj, N, S_out, T_out)
+
+
+def _conv_joined(x, w, b, spec, cdt, wkey):
+    T_out, S_out, _ = _join_plan(spec, x.shape[1])
+    xj = _join_input(x, spec)
+    yj = ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey)  # slot u S_out + t <- rows u S_in + st t + k
+    return _split_output(yj, x.shape[0], S_out, T_out)
+
+
+def conv_layers(x, convs):
+    """The outputs of ``convs`` [(w, b, spec, cdt, wkey)] applied in order, as ``conv`` per layer;
+    where one joined conv feeds the next, RejoinFn hands its joined output over (one remap launch
+    each way instead of a split and a join)."""
+    outs, pend = [], None  # pend: (yj, N, S_out, T_out) of a joined conv whose output is not split yet
+    for w, b, spec, cdt, wkey in convs:
+        if pend is not None:
+            yj, N, S_out, T = pend
+            pend = None
+            C = yj.shape[-1]
+            if REJOIN and _joined((N, T, C), spec) and (C * yj.element_size()) % 16 == 0:
+                T_out2, S_out2, S_in2 = _join_plan(spec, T)
+                y, xj = RejoinFn.apply(yj, N, S_out, T, spec.pad, S_in2)
+                outs.append(y)
+                pend = (ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey), N, S_out2, T_out2)
+                continue
+            x = _split_output(yj, N, S_out, T)
+            outs.append(x)
+        if _joined(x.shape, spec):
+            T_out, S_out, _ = _join_plan(spec, x.shape[1])
+            yj = ConvFn.apply(_join_input(x, spec), w, b, None, None, replace(spec, pad=0), cdt, wkey)
+            pend = (yj, x.shape[0], S_out, T_out)
+        else:
+            x = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey)
+            outs.append(x)
+    if pend is not None:
+        outs.append(_split_output(pend[0], pend[1], pend[2], pend[3]))
+    return outs
 
 
 def _joined(shape, spec, has_res=False):

@@ -722,6 +722,38 @@ def seq_remap(src, dst_rows, Td, Ss, lo, hi, shift):
     return dst
 
 
+def seq_remap2(jobs):
+    """One or two remaps in one launch (vo_seq_remap2): each job a dict(src, dst_rows, Td, Ss, lo, hi,
+    shift[, src2, Ss2, shift2]) -> its (dst_rows, C) tensor: row r = (n, t) (n = r // Td, t = r % Td)
+    = src row n Ss + t + shift (+ src2 row n Ss2 + t + shift2, added in the dtype) for lo <= t < hi,
+    else 0.  Sources contiguous with the same row (C) and dtype, rows of whole 16-byte units."""
+    if not 1 <= len(jobs) <= 2:
+        raise ValueError("seq_remap2: one or two jobs")
+    ref = jobs[0]["src"]
+    C = ref.shape[-1]
+    arr = (_lib.RemapJob * len(jobs))()
+    outs = []
+    for i, j in enumerate(jobs):
+        src, src2 = j["src"], j.get("src2")
+        for t in (src, src2):
+            if t is not None:
+                _contig(t, "src")
+                if t.shape[-1] != C or t.dtype != ref.dtype:
+                    raise ValueError("seq_remap2: sources must share the row and dtype")
+        dst = torch.empty((j["dst_rows"], C), dtype=ref.dtype, device=ref.device)
+        outs.append(dst)
+        a = arr[i]
+        a.src, a.dst = src.data_ptr(), dst.data_ptr()
+        a.src2 = src2.data_ptr() if src2 is not None else None
+        a.src_rows = src.numel() // C
+        a.src2_rows = src2.numel() // C if src2 is not None else 0
+        a.dst_rows, a.Td, a.Ss, a.lo, a.hi, a.shift = j["dst_rows"], j["Td"], j["Ss"], j["lo"], j["hi"], j["shift"]
+        a.Ss2, a.shift2 = j.get("Ss2", 0), j.get("shift2", 0)
+    _lib.check(_lib.lib().vo_seq_remap2(len(jobs), arr, C * ref.element_size(), vo_dtype(ref), _stream(ref)),
+               "vo_seq_remap2")
+    return outs
+
+
 def pack_dgrad_phase(w, groups, S, k_r, J, ci_out, co_in, dtype, out=None):
     """Stride phase k_r of a strided / grouped conv's input gradient: w (Co, Ci/groups, K) -> packed
     [J][ci_out][co_in] (taps k_r + S (J - 1 - t), channel roles swapped per group, zero padding).
