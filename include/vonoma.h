@@ -444,6 +444,11 @@ int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* ref, int ldr,
  * in one pass; add has g's dtype; rows of 8-element vectors, 16-byte aligned). */
 int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, const void* add,
                       int lda, int64_t rows, int width, float slope, void* out, int ldo, void* stream);
+/* out = round(round(g + add) * (ref > 0 ? 1 : slope)): two gradients of a leaky-ReLU output (the next
+ * conv's input gradient and a feature-matching loss's, HiFi-GAN discriminators) summed as autograd
+ * sums them and masked in one pass (same layout rules as vo_lrelu_mask_add). */
+int vo_lrelu_mask_sum(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype, const void* add,
+                      int lda, int64_t rows, int width, float slope, void* out, int ldo, void* stream);
 
 /* ------------------------------------------------------------------ training glue (round 2)
  * BatchNorm with batch statistics over channels-last x (M rows x C channels, VO_F32 / VO_BF16):

@@ -755,3 +755,58 @@ def test_discriminator_rejoin_bit_identical():
     for i, (a, b) in enumerate(zip(gd0, gd1)):
         assert torch.equal(a, b), i
     assert torch.equal(gw0, gw1)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_lrelu_mask_sum_exact(dt):
+    """vo_lrelu_mask_sum: the mask of the two gradients' sum, rounded as autograd's add then the mask."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(9)
+    a, b = (torch.randn(5, 77, 64, generator=g).to(dt) for _ in range(2))
+    ref = torch.randn(5, 77, 64, generator=g).to(dt)
+    want = ops.lrelu_mask((a.cuda() + b.cuda()), ref.cuda(), 0.1)
+    got = ops.lrelu_mask(a.cuda(), ref.cuda(), 0.1, summand=b.cuda())
+    assert torch.equal(got, want)
+
+
+def test_discriminator_fmap_tap_bit_identical():
+    """The non-joined discriminator convs hand out their feature map as a second output
+    (ConvFn tap) whose gradient joins the next conv's in the mask pass: the G-step gradient wrt the
+    generated wav equals autograd summing the two first (plain per-layer ConvFn), bit for bit."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
+                                                                  feature_loss, generator_loss)
+    from visual_onoma_to_wave_amd.hifigan.train import _single
+    torch.manual_seed(6)
+    mpd = MultiPeriodDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    msd = MultiScaleDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    for p in list(mpd.parameters()) + list(msd.parameters()):
+        p.requires_grad_(False)
+    y = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
+    yh = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
+    orig = G.conv_layers
+
+    def plain_layers(x, convs):  # the per-layer path: conv() per layer, autograd sums the fan-out
+        outs = []
+        for w, b, spec, cdt, wkey in convs:
+            x = G.conv(x, w, b, spec, cdt, wkey=wkey)
+            outs.append(x)
+        return outs
+
+    def run():
+        yg = yh.clone().requires_grad_(True)
+        _, fr_f = _single(mpd, y, False)
+        _, fr_s = _single(msd, y, False)
+        sg_f, fg_f = _single(mpd, yg, True)
+        sg_s, fg_s = _single(msd, yg, True)
+        lg = generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
+        (gw,) = torch.autograd.grad(lg, [yg])
+        return float(lg), gw
+
+    try:
+        G.conv_layers = plain_layers
+        lg0, gw0 = run()
+    finally:
+        G.conv_layers = orig
+    lg1, gw1 = run()
+    assert lg0 == lg1 and torch.equal(gw0, gw1)

@@ -161,6 +161,8 @@ _SIGNATURES = {
     "vo_pack_batch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "vo_lrelu_mask_add": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
                                   c_float, c_void_p, c_int, c_void_p]),
+    "vo_lrelu_mask_sum": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
+                                  c_float, c_void_p, c_int, c_void_p]),
     "vo_spectral_norm": (c_int, [c_int, c_void_p, c_int, c_float, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),
     "vo_seq_remap2": (c_int, [c_int, c_void_p, c_int, c_int, c_void_p]),

@@ -441,9 +441,11 @@ __global__ void __launch_bounds__(256) gan_reduce_grad_v8_kernel(int kind, const
   }
 }
 
-// ADD: out = round(masked) + add[r, c] (then rounded): a residual's gradient summed in the same
-// pass -- bit for bit the masked tensor followed by autograd's add of the two gradients
-template <typename TG, typename TR, bool FLAT, bool ADD = false>
+// ADD 1: out = round(masked) + add[r, c] (then rounded): a residual's gradient summed in the same
+// pass -- bit for bit the masked tensor followed by autograd's add of the two gradients.
+// ADD 2: out = mask(round(g + add)): two gradients of the activation's output (the next conv's and a
+// feature-matching loss's) summed as autograd sums them, then masked
+template <typename TG, typename TR, bool FLAT, int ADD = 0>
 __global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict__ g, int ldg,
                                                             const TR* __restrict__ ref, int ldr, int64_t rows,
                                                             int width, float slope, TG* __restrict__ out, int ldo,
@@ -464,9 +466,15 @@ __global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict
     float x[8], q[8];
     load8(g + og, x);
     load8(ref + orf, q);
+    if constexpr (ADD == 2) {
+      float a[8];
+      load8(add + oa, a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = to_f32(from_f32<TG>(x[e] + a[e]));
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = q[e] > 0.f ? x[e] : x[e] * slope;
-    if constexpr (ADD) {
+    if constexpr (ADD == 1) {
       float a[8];
       load8(add + oa, a);
 #pragma unroll
@@ -850,9 +858,9 @@ extern "C" int vo_lrelu_mask(const void* g, int ldg, int g_dtype, const void* re
   VO_RETURN_LAUNCH();
 }
 
-extern "C" int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
-                                 const void* add, int lda, int64_t rows, int width, float slope, void* out, int ldo,
-                                 void* stream) {
+static int lrelu_mask_add_run(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
+                              const void* add, int lda, int64_t rows, int width, float slope, void* out, int ldo,
+                              bool presum, void* stream) {
   VO_CHECK_ARG(g && ref && add && out, "lrelu_mask_add: null pointer");
   VO_CHECK_ARG(rows > 0 && width > 0 && ldg >= width && ldr >= width && ldo >= width && lda >= width,
                "lrelu_mask_add: bad shape");
@@ -860,9 +868,13 @@ extern "C" int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void
                "lrelu_mask_add: rows must be 8-element vectors, 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int gv = grid_for(rows * (width / 8));
-#define VO_LMA(TG, TR)                                                                                          \
-  hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, false, true>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg, \
-                     (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo, (const TG*)add, lda)
+#define VO_LMA(TG, TR)                                                                                                 \
+  if (presum)                                                                                                          \
+    hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, false, 2>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg,         \
+                       (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo, (const TG*)add, lda);                   \
+  else                                                                                                                 \
+    hipLaunchKernelGGL((lrelu_mask_v8_kernel<TG, TR, false, 1>), dim3(gv), dim3(256), 0, st, (const TG*)g, ldg,         \
+                       (const TR*)ref, ldr, rows, width, slope, (TG*)out, ldo, (const TG*)add, lda)
   if (g_dtype == VO_BF16 && ref_dtype == VO_BF16) VO_LMA(bf16_t, bf16_t);
   else if (g_dtype == VO_F32 && ref_dtype == VO_F32) VO_LMA(float, float);
   else if (g_dtype == VO_BF16 && ref_dtype == VO_F32) VO_LMA(bf16_t, float);
@@ -873,6 +885,18 @@ extern "C" int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void
   }
 #undef VO_LMA
   VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_lrelu_mask_add(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
+                                 const void* add, int lda, int64_t rows, int width, float slope, void* out, int ldo,
+                                 void* stream) {
+  return lrelu_mask_add_run(g, ldg, g_dtype, ref, ldr, ref_dtype, add, lda, rows, width, slope, out, ldo, false, stream);
+}
+
+extern "C" int vo_lrelu_mask_sum(const void* g, int ldg, int g_dtype, const void* ref, int ldr, int ref_dtype,
+                                 const void* add, int lda, int64_t rows, int width, float slope, void* out, int ldo,
+                                 void* stream) {
+  return lrelu_mask_add_run(g, ldg, g_dtype, ref, ldr, ref_dtype, add, lda, rows, width, slope, out, ldo, true, stream);
 }
 
 extern "C" int vo_period_fold_bwd(const void* g, int dtype, int B, int T, int P, float* gwav, void* stream) {

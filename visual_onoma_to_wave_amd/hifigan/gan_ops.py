@@ -261,10 +261,13 @@ class ResLink:
 
 class ConvFn(torch.autograd.Function):
     """y = (post(conv(pre(x), w) + b) + res1) * out_scale + res2, channels-last.  ``link``:
-    (ResLink, "in" | "res"): this conv's input ("in") / res1 ("res") is the linked tensor."""
+    (ResLink, "in" | "res"): this conv's input ("in") / res1 ("res") is the linked tensor.  ``tap``
+    (leaky-ReLU post-activation): also return y a second time (same storage) for a second consumer
+    (a discriminator feature map): the backward gets the two gradients apart and sums them in its
+    mask pass (vo_lrelu_mask_sum) instead of autograd adding them first."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None, link=None):
+    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None, link=None, tap=False):
         if spec.post is not None and (res1 is not None or res2 is not None):
             raise ValueError("ConvFn: post-activation with residual inputs is not differentiable here")
         y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt, wkey)
@@ -280,12 +283,22 @@ class ConvFn(torch.autograd.Function):
                 ctx.link = (lk, "res")
         ctx.has = (res1 is not None, res2 is not None)
         ctx.save_for_backward(x, w, y if spec.post is not None else None)
+        if tap:
+            if spec.post != "lrelu" or res1 is not None or res2 is not None or spec.out_scale != 1.0:
+                raise ValueError("ConvFn: tap needs a leaky-ReLU post-activation and no residuals")
+            ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zero fill)
+            return y, y.detach()
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, *tap_g):
         x, w, y = ctx.saved_tensors
         spec, cdt = ctx.spec, ctx.cdt
+        gf = tap_g[0] if tap_g else None
+        if gy is None:
+            gy, gf = gf, None
+        if gy is None:
+            return (None,) * 10
         gy = gy.contiguous()
         g_res2 = gy if ctx.has[1] and ctx.needs_input_grad[4] else None
         gz = gy * spec.out_scale if spec.out_scale != 1.0 else gy
@@ -294,7 +307,10 @@ class ConvFn(torch.autograd.Function):
         if role == "res" and g_res1 is not None:  # the residual's gradient goes to the linked input conv
             lk.g, g_res1 = g_res1, None
         if spec.post == "lrelu":
-            gz = ops.lrelu_mask(gz, y, spec.post_slope)
+            ok = gf is not None and gf.dtype == gz.dtype and gf.shape == gz.shape and gz.shape[-1] % 8 == 0
+            if gf is not None and not ok:
+                gz, gf = gz + gf, None
+            gz = ops.lrelu_mask(gz, y, spec.post_slope, summand=gf)
         elif spec.post == "tanh":
             yf = y.float()
             gz = (gz.float() * (1.0 - yf * yf)).to(gz.dtype)
@@ -383,7 +399,7 @@ class ConvFn(torch.autograd.Function):
             gw = None
         if not ctx.needs_input_grad[2]:
             gb = None
-        return gx, gw, gb, g_res1, g_res2, None, None, None, None
+        return gx, gw, gb, g_res1, g_res2, None, None, None, None, None
 
 
 # Many short sequences (the MPD's period columns: 96-352 sequences of 10-51 rows at C5): the conv
@@ -512,6 +528,9 @@ def conv_layers(x, convs):
             T_out, S_out, _ = _join_plan(spec, x.shape[1])
             yj = ConvFn.apply(_join_input(x, spec), w, b, None, None, replace(spec, pad=0), cdt, wkey)
             pend = (yj, x.shape[0], S_out, T_out)
+        elif spec.post == "lrelu":  # the feature map and the next conv's input: their gradients meet in the mask pass
+            x, f = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey, None, True)
+            outs.append(f)
         else:
             x = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey)
             outs.append(x)
@@ -698,7 +717,7 @@ def spectral_norm_all(mods):
     return out
 
 
-# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)
+# VO_BATCHED_WN=0: per-layer torch._weight_norm instead (A/B)
 BATCHED_WN = os.environ.get("VO_BATCHED_WN", "1") != "0"
 BATCHED_SN = os.environ.get("VO_BATCHED_SN", "1") != "0"  # 0: torch's spectral-norm hook per conv (A/B)
 

@@ -1070,12 +1070,25 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     return (w, db) if with_bias else w
 
 
-def lrelu_mask(g, ref, slope, out=None, add=None):
+def lrelu_mask(g, ref, slope, out=None, add=None, summand=None):
     """g * (ref > 0 ? 1 : slope) (leaky-ReLU / ReLU backward); g, ref (..., C) with row-contiguous
     last dims (ref may be a channel slice of a wider tensor).  out=g computes in place.  ``add``
-    (g's shape and dtype): that rounded result plus ``add`` in the same pass (vo_lrelu_mask_add)."""
+    (g's shape and dtype): that rounded result plus ``add`` in the same pass (vo_lrelu_mask_add).
+    ``summand`` (g's shape and dtype): the mask of round(g + summand) (vo_lrelu_mask_sum)."""
     if g.shape != ref.shape:
         raise ValueError("lrelu_mask: g and ref shapes differ")
+    if add is not None and summand is not None:
+        raise ValueError("lrelu_mask: add or summand, not both")
+    if summand is not None:
+        if summand.shape != g.shape or summand.dtype != g.dtype:
+            raise ValueError("lrelu_mask: summand must match g")
+        C = g.shape[-1]
+        g, ref, summand = g.contiguous(), ref.contiguous(), summand.contiguous()
+        out = torch.empty_like(g) if out is None else _contig(out, "out")
+        _lib.check(_lib.lib().vo_lrelu_mask_sum(_ptr(g), C, vo_dtype(g), _ptr(ref), C, vo_dtype(ref), _ptr(summand),
+                                                C, g.numel() // C, C, float(slope), _ptr(out), C, _stream(g)),
+                   "vo_lrelu_mask_sum")
+        return out
     if add is not None:
         if add.shape != g.shape or add.dtype != g.dtype:
             raise ValueError("lrelu_mask: add must match g")
