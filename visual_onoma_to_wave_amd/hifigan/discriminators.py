@@ -69,7 +69,7 @@ def _weight(m):
 
 
 def _conv_w(m, w):
-    return w[..., 0] if w.dim() == 4 else w  # Conv2d (k, 1) weights as Conv1d
+    return w.squeeze(-1) if w.dim() == 4 else w  # Conv2d (k, 1) weights as Conv1d
 
 
 def _prepare(root, layers, dgrad_first):
@@ -132,7 +132,7 @@ class DiscriminatorP(_DiscBase):
         specs = [G.ConvSpec(K=k, pad=get_padding(5, 1), stride=s, post="lrelu", post_slope=LRELU_SLOPE,
                             ci_pad=8 if i == 0 else None) for i in range(4)]
         specs.append(G.ConvSpec(K=k, pad=2, post="lrelu", post_slope=LRELU_SLOPE))
-        return specs, G.ConvSpec(K=3, pad=1, co_pad=4)
+        return specs, G.ConvSpec(K=3, pad=1, co_pad=8)  # 8: dY needs no channel padding in the backward
 
     def _layers(self, B, T):
         """[(module, spec, input shape (N, T, C))] of ``forward``'s convs for a (B, T) wav batch."""
@@ -152,7 +152,9 @@ class DiscriminatorP(_DiscBase):
         if W is None:
             W = _prepare(self, [layers], wav.requires_grad)
         x = G.PeriodFoldFn.apply(wav, self.period, adt)
-        fmap = G.conv_layers(x, [(_w(m, W)[..., 0], m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
+        # squeeze, not [..., 0]: its adjoint is a view of the 3-D weight gradient (select's was a zero
+        # fill and a copy per conv and D step)
+        fmap = G.conv_layers(x, [(_w(m, W).squeeze(-1), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
         score = fmap[-1][..., 0].contiguous()
         fmap[-1] = score
         return score, fmap
@@ -205,7 +207,7 @@ class DiscriminatorS(_DiscBase):
                             ci_pad=8 if ci == 1 else None)
             out.append((m, sp, (B, T, C)))
             T, C = G.out_len(sp, T), co
-        out.append((self.conv_post, G.ConvSpec(K=3, pad=1, co_pad=4), (B, T, C)))
+        out.append((self.conv_post, G.ConvSpec(K=3, pad=1, co_pad=8), (B, T, C)))
         return out
 
     def forward(self, wav, W=None):

@@ -314,7 +314,9 @@ class ConvFn(torch.autograd.Function):
         elif spec.post == "tanh":
             yf = y.float()
             gz = (gz.float() * (1.0 - yf * yf)).to(gz.dtype)
-        if spec.co_pad is not None:
+        if spec.co_pad is not None and (gz.shape[-1] % 8 or spec.groups != 1 or spec.transposed is not None):
+            # (a dY of whole 8-channel vectors goes on as it is: the padded rows' input-gradient weights
+            # are zero and their weight / bias gradient rows are dropped below)
             gz = gz[..., : w.shape[0]].contiguous()
         ci = w.shape[0] if spec.transposed is not None else w.shape[1] * spec.groups
         xin = x[..., :ci] if x.shape[-1] != ci else x
