@@ -395,6 +395,16 @@ typedef struct vo_sn_layer {
   int rows, L;
 } VoSnLayer;
 int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float eps, void* stream);
+/* Its backward (u, v, sigma as the forward used them, held constant, as torch's autograd of the
+ * hook does): gW = g / sigma - (sum(g * W) / sigma^2) u v^T for n layers in three launches; the sum
+ * in a fixed order (deterministic).  workspace: vo_spectral_norm_bwd_workspace_size bytes. */
+typedef struct vo_sn_bwd_layer {
+  const float *g, *W, *u, *v, *sigma;
+  float* gW;
+  int rows, L;
+} VoSnBwdLayer;
+int64_t vo_spectral_norm_bwd_workspace_size(int n, const VoSnBwdLayer* layers);
+int vo_spectral_norm_bwd(int n, const VoSnBwdLayer* layers, float* workspace, void* stream);
 int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows, int width,
                   int dtype, float* out, float* workspace, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,

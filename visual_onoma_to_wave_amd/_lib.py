@@ -59,6 +59,11 @@ class RemapJob(ctypes.Structure):
         (f, c_int) for f in ("Td", "lo", "hi", "shift", "shift2")]
 
 
+class SnBwdLayer(ctypes.Structure):
+    """VoSnBwdLayer (include/vonoma.h, vo_spectral_norm_bwd)."""
+    _fields_ = [(f, c_void_p) for f in ("g", "W", "u", "v", "sigma", "gW")] + [("rows", c_int), ("L", c_int)]
+
+
 class SnLayer(ctypes.Structure):
     """VoSnLayer (include/vonoma.h, vo_spectral_norm)."""
     _fields_ = [(f, c_void_p) for f in ("W", "u", "v", "u_out", "v_out", "vraw", "s", "sigma", "w")] + [
@@ -164,6 +169,8 @@ _SIGNATURES = {
     "vo_lrelu_mask_sum": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
                                   c_float, c_void_p, c_int, c_void_p]),
     "vo_spectral_norm": (c_int, [c_int, c_void_p, c_int, c_float, c_void_p]),
+    "vo_spectral_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
+    "vo_spectral_norm_bwd_workspace_size": (c_int64, [c_int, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),
     "vo_seq_remap2": (c_int, [c_int, c_void_p, c_int, c_int, c_void_p]),
     "vo_weight_norm": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

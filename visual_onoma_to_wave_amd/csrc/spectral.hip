@@ -160,9 +160,113 @@ __global__ void __launch_bounds__(256) sn_scale_kernel(SnArgs a) {
   }
 }
 
+// ---- backward (torch.nn.utils.spectral_norm's autograd with u, v held constant):
+//   gW = g / sigma - (d / sigma^2) u v^T,  d = sum(g * W)
+// for every layer of a pass in three launches (the per-layer PyTorch chain was a multiply, a sum, a
+// divide, an outer product, a multiply and a subtract per layer): block partials of d (4096 elements
+// per workgroup), their sum per layer in block order, then the elementwise update.
+constexpr int SNB_ELEMS = 4096;
+struct SnBwdArgs {
+  VoSnBwdLayer l[SN_MAX];
+  int blk0[SN_MAX + 1];
+  int n;
+  float* part;  // [blocks] partials, then [n] d values
+};
+
+__device__ __forceinline__ float snb_block_sum(float x, float* red) {
+  x = wave_sum(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void __launch_bounds__(256) sn_bwd_dot_kernel(SnBwdArgs a) {
+  __shared__ float red[4];
+  const int li = table_find(a.blk0, a.n, blockIdx.x);
+  const VoSnBwdLayer& L = a.l[li];
+  const int64_t n = (int64_t)L.rows * L.L;
+  const int64_t i0 = (int64_t)(blockIdx.x - a.blk0[li]) * SNB_ELEMS + threadIdx.x;
+  float acc = 0.f;
+#pragma unroll 4
+  for (int k = 0; k < SNB_ELEMS / 256; ++k) {
+    const int64_t i = i0 + k * 256;
+    if (i < n) acc += L.g[i] * L.W[i];
+  }
+  const float s = snb_block_sum(acc, red);
+  if (threadIdx.x == 0) a.part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) sn_bwd_sum_kernel(SnBwdArgs a) {
+  __shared__ float red[4];
+  const int li = blockIdx.x;
+  float acc = 0.f;
+  for (int b = a.blk0[li] + threadIdx.x; b < a.blk0[li + 1]; b += 256) acc += a.part[b];
+  const float s = snb_block_sum(acc, red);
+  if (threadIdx.x == 0) a.part[a.blk0[a.n] + li] = s;
+}
+
+__global__ void __launch_bounds__(256) sn_bwd_apply_kernel(SnBwdArgs a) {
+  const int li = table_find(a.blk0, a.n, blockIdx.x);
+  const VoSnBwdLayer& L = a.l[li];
+  const int64_t n = (int64_t)L.rows * L.L;
+  const int64_t i0 = (int64_t)(blockIdx.x - a.blk0[li]) * SNB_ELEMS + threadIdx.x;
+  const float sg = L.sigma[0];
+  const float c = a.part[a.blk0[a.n] + li] / (sg * sg);
+  for (int k = 0; k < SNB_ELEMS / 256; ++k) {
+    const int64_t i = i0 + k * 256;
+    if (i < n) {
+      const int64_t r = i / L.L;
+      L.gW[i] = L.g[i] / sg - c * (L.u[r] * L.v[i - r * L.L]);
+    }
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
+
+extern "C" int64_t vo_spectral_norm_bwd_workspace_size(int n, const VoSnBwdLayer* layers) {
+  if (n <= 0 || !layers) return 0;
+  int64_t f = 0;
+  for (int i0 = 0; i0 < n; i0 += SN_MAX) {
+    int64_t blocks = 0;
+    const int m = std::min(SN_MAX, n - i0);
+    for (int i = 0; i < m; ++i) blocks += ((int64_t)layers[i0 + i].rows * layers[i0 + i].L + SNB_ELEMS - 1) / SNB_ELEMS;
+    f = std::max(f, blocks + m);
+  }
+  return f * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_spectral_norm_bwd(int n, const VoSnBwdLayer* layers, float* workspace, void* stream) {
+  VO_CHECK_ARG(n >= 0 && (n == 0 || (layers && workspace)), "spectral_norm_bwd: null table / workspace");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += SN_MAX) {
+    SnBwdArgs a;
+    a.n = std::min(SN_MAX, n - i0);
+    a.part = workspace;
+    int total = 0;
+    for (int i = 0; i < a.n; ++i) {
+      const VoSnBwdLayer& s = layers[i0 + i];
+      VO_CHECK_ARG(s.g && s.W && s.u && s.v && s.sigma && s.gW, "spectral_norm_bwd: layer %d: null pointer", i0 + i);
+      VO_CHECK_ARG(s.rows > 0 && s.L > 0 && (int64_t)s.rows * s.L < (1LL << 31), "spectral_norm_bwd: layer %d: bad size",
+                   i0 + i);
+      a.l[i] = s;
+      a.blk0[i] = total;
+      total += (int)(((int64_t)s.rows * s.L + SNB_ELEMS - 1) / SNB_ELEMS);
+    }
+    a.blk0[a.n] = total;
+    hipLaunchKernelGGL(sn_bwd_dot_kernel, dim3((unsigned)total), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sn_bwd_sum_kernel, dim3((unsigned)a.n), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sn_bwd_apply_kernel, dim3((unsigned)total), dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      vo_set_error("spectral_norm_bwd: launch failed: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+  }
+  return VO_OK;
+}
 
 extern "C" int vo_spectral_norm(int n, const VoSnLayer* layers, int power, float eps, void* stream) {
   VO_CHECK_ARG(n >= 0 && (n == 0 || layers), "spectral_norm: null table");

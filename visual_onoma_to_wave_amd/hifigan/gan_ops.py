@@ -680,14 +680,16 @@ class SpectralNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gws):
         n, sv = ctx.n, ctx.saved_tensors
-        out = []
-        for W, u, v, sg, g in zip(sv[:n], sv[n:2 * n], sv[2 * n:3 * n], sv[3 * n:], gws):
-            if g is None:
-                out.append(None)
-                continue
-            gm, Wm = g.reshape(W.shape[0], -1), W.reshape(W.shape[0], -1)
-            d = (gm * Wm).sum()  # dL/dsigma = -d / sigma^2; dsigma/dW = u v^T
-            out.append((gm / sg - (d / (sg * sg)) * torch.outer(u, v)).view_as(W))
+        # gW = g / sigma - (sum(g W) / sigma^2) u v^T (dL/dsigma = -d / sigma^2; dsigma/dW = u v^T), every
+        # layer with a gradient in one vo_spectral_norm_bwd call
+        idx = [i for i in range(n) if gws[i] is not None]
+        out = [None] * n
+        if idx:
+            Ws = [sv[i].detach() for i in idx]
+            res = ops.spectral_norm_bwd([gws[i] for i in idx], Ws, [sv[n + i] for i in idx],
+                                        [sv[2 * n + i] for i in idx], [sv[3 * n + i] for i in idx])
+            for i, r in zip(idx, res):
+                out[i] = r
         return (None, None, None, None, *out)
 
 

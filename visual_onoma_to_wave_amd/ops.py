@@ -873,6 +873,32 @@ def spectral_norm(Ws, us, vs, power, eps=1e-12):
     return [o["w"] for o in outs], [o["u_out"] for o in outs], [o["v_out"] for o in outs], [o["sigma"] for o in outs]
 
 
+def spectral_norm_bwd(gs, Ws, us, vs, sigmas):
+    """Gradients wrt weight_orig of spectral_norm's weights (vo_spectral_norm_bwd): gs / Ws (rows, ...)
+    fp32, us / vs / sigmas as the forward used them -> [gW] (gW = g / s - (sum(g W) / s^2) u v^T)."""
+    n = len(gs)
+    arr = (_lib.SnBwdLayer * n)()
+    outs = []
+    keep = []
+    for e, g, W, u, v, sg in zip(arr, gs, Ws, us, vs, sigmas):
+        g = g.float().contiguous()
+        for t, name in ((W, "W"), (u, "u"), (v, "v"), (sg, "sigma")):
+            _contig(t, name)
+        if g.shape != W.shape:
+            raise ValueError("spectral_norm_bwd: gradient and weight shapes differ")
+        o = torch.empty_like(W)
+        outs.append(o)
+        keep.append(g)
+        e.g, e.W, e.u, e.v, e.sigma, e.gW = g.data_ptr(), W.data_ptr(), u.data_ptr(), v.data_ptr(), sg.data_ptr(), o.data_ptr()
+        e.rows, e.L = W.shape[0], W.numel() // W.shape[0]
+    L = _lib.lib()
+    p = ctypes.cast(arr, ctypes.c_void_p)
+    ws = torch.empty(max(1, int(L.vo_spectral_norm_bwd_workspace_size(n, p)) // 4), dtype=torch.float32,
+                     device=Ws[0].device)
+    _lib.check(L.vo_spectral_norm_bwd(n, p, _ptr(ws), _stream(Ws[0])), "vo_spectral_norm_bwd")
+    return outs
+
+
 def weight_norm_bwd(vs, gs, dws):
     """Backward of ``weight_norm``: lists of dL/dw -> (dL/dv list, dL/dg list)."""
     if not vs:
