@@ -409,6 +409,17 @@ int vo_gan_reduce(int kind, const void* a, int lda, const void* b, int ldb, int6
                   int dtype, float* out, float* workspace, void* stream);
 int vo_gan_reduce_grad(int kind, const void* a, int lda, const void* b, int ldb, int64_t rows,
                        int width, int dtype, const float* scale, void* ga, int ldg, void* stream);
+/* Many terms per launch (the C5 G step's feature-matching / adversarial terms, the D step's halves):
+ * vo_gan_reduce_multi writes out[i] = sum_i * scale[i] (scale NULL: 1), each sum bit for bit
+ * vo_gan_reduce's (workspace: vo_gan_reduce_multi_workspace_size(n) bytes); vo_gan_reduce_grad_multi
+ * writes term i's gradient ga_i = scale[i] * d(sum_i)/da_i (ga, ldg per term).  scale: n device floats. */
+typedef struct vo_gan_term {
+  int kind; const void* a; int lda; const void* b; int ldb; int64_t rows; int width; void* ga; int ldg;
+} VoGanTerm;
+int64_t vo_gan_reduce_multi_workspace_size(int n);
+int vo_gan_reduce_multi(int n, const VoGanTerm* terms, int dtype, const float* scale, float* out, float* workspace,
+                        void* stream);
+int vo_gan_reduce_grad_multi(int n, const VoGanTerm* terms, int dtype, const float* scale, void* stream);
 
 /* ------------------------------------------------------------------ training backward
  * Weight gradient of a channels-last conv on MFMA (replaces the MIOpen weight pass of the

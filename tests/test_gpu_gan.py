@@ -810,3 +810,73 @@ def test_discriminator_fmap_tap_bit_identical():
         G.conv_layers = orig
     lg1, gw1 = run()
     assert lg0 == lg1 and torch.equal(gw0, gw1)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_gan_reduce_multi_bit_identical(dt):
+    """vo_gan_reduce_multi / _grad_multi (every term in one launch pair / one launch, > 32 terms so
+    the table is split) against vo_gan_reduce / _grad per term: sums and gradients bit for bit, on
+    vector (8-wide) and scalar (odd width, strided) terms of all three kinds."""
+    from visual_onoma_to_wave_amd import ops
+    g = torch.Generator().manual_seed(11)
+    kinds, As, Bs = [], [], []
+    for i in range(37):
+        k = i % 3
+        if i % 4 == 3:  # scalar path: odd width, a strided row view
+            base = torch.randn(20 + i, 13, generator=g).to(dt).cuda()
+            a = base[:, :11]
+        else:
+            a = torch.randn(3, 50 + 7 * i, 64, generator=g).to(dt).cuda()
+        b = (torch.randn(a.shape, generator=g).to(dt).cuda()) if k == 0 else None
+        kinds.append(k)
+        As.append(a)
+        Bs.append(b)
+    sv = torch.rand(37, generator=g).cuda() + 0.5
+    got = ops.gan_reduce_multi(kinds, As, Bs, sv)
+    want = torch.zeros(37, device="cuda")
+    for i in range(37):
+        ops.gan_reduce(kinds[i], As[i], Bs[i], out=want[i])
+    assert torch.equal(got, want * sv)
+    gs = torch.rand(37, generator=g).cuda()
+    gm = ops.gan_reduce_grad_multi(kinds, As, Bs, gs)
+    for i in range(37):
+        assert torch.equal(gm[i], ops.gan_reduce_grad(kinds[i], As[i], Bs[i], gs[i])), i
+
+
+def test_gan_loss_terms_multi_bit_identical():
+    """The D and G losses of a bf16 step and their gradients with the batched loss-term launches
+    (gan_ops.GAN_MULTI) against the per-term launches, bit for bit."""
+    from visual_onoma_to_wave_amd.hifigan import gan_ops as G
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
+                                                                  discriminator_loss, feature_loss, generator_loss)
+    from visual_onoma_to_wave_amd.hifigan.train import _single
+    torch.manual_seed(7)
+    mpd = MultiPeriodDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    msd = MultiScaleDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    y = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
+    yh = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
+    params = list(mpd.parameters()) + list(msd.parameters())
+
+    def run(multi):
+        G.GAN_MULTI = multi
+        r1, g1, _, _ = mpd(y, yh)
+        r2, g2, _, _ = msd(y, yh)
+        ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
+        gd = torch.autograd.grad(ld, params)
+        yg = yh.clone().requires_grad_(True)
+        _, fr_f = _single(mpd, y, False)
+        _, fr_s = _single(msd, y, False)
+        sg_f, fg_f = _single(mpd, yg, True)
+        sg_s, fg_s = _single(msd, yg, True)
+        lg = generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
+        (gw,) = torch.autograd.grad(lg, [yg])
+        return float(ld), gd, float(lg), gw
+
+    try:
+        ld0, gd0, lg0, gw0 = run(False)
+        ld1, gd1, lg1, gw1 = run(True)
+    finally:
+        G.GAN_MULTI = True
+    assert ld0 == ld1 and lg0 == lg1
+    assert all(torch.equal(a, b) for a, b in zip(gd0, gd1))
+    assert torch.equal(gw0, gw1)

@@ -59,6 +59,12 @@ class RemapJob(ctypes.Structure):
         (f, c_int) for f in ("Td", "lo", "hi", "shift", "shift2")]
 
 
+class GanTerm(ctypes.Structure):
+    """VoGanTerm (include/vonoma.h, vo_gan_reduce_multi / vo_gan_reduce_grad_multi)."""
+    _fields_ = [("kind", c_int), ("a", c_void_p), ("lda", c_int), ("b", c_void_p), ("ldb", c_int),
+                ("rows", ctypes.c_int64), ("width", c_int), ("ga", c_void_p), ("ldg", c_int)]
+
+
 class SnBwdLayer(ctypes.Structure):
     """VoSnBwdLayer (include/vonoma.h, vo_spectral_norm_bwd)."""
     _fields_ = [(f, c_void_p) for f in ("g", "W", "u", "v", "sigma", "gW")] + [("rows", c_int), ("L", c_int)]
@@ -169,6 +175,9 @@ _SIGNATURES = {
     "vo_lrelu_mask_sum": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int64, c_int,
                                   c_float, c_void_p, c_int, c_void_p]),
     "vo_spectral_norm": (c_int, [c_int, c_void_p, c_int, c_float, c_void_p]),
+    "vo_gan_reduce_multi": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_gan_reduce_multi_workspace_size": (c_int64, [c_int]),
+    "vo_gan_reduce_grad_multi": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "vo_spectral_norm_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p]),
     "vo_spectral_norm_bwd_workspace_size": (c_int64, [c_int, c_void_p]),
     "vo_seq_remap": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int64, c_int, c_int, c_int, c_void_p]),

@@ -484,6 +484,149 @@ __global__ void __launch_bounds__(256) lrelu_mask_v8_kernel(const TG* __restrict
   }
 }
 
+// Many loss terms per launch (the C5 G step's 54 feature-matching L1 terms and 8 adversarial ones,
+// the D step's 16 halves): term i's blocks are blk0[i] .. blk0[i + 1] - 1 of one grid, each doing what
+// block b of the single-term kernel's g_i-block grid does (same elements per thread, same sums), so
+// the partials, and the per-term sums of them added by one wave each, are those of vo_gan_reduce bit
+// for bit; the sums are written times the term's scale.  The gradient kernel likewise covers every
+// term's elements in one launch.  (Each term was a reduction, a final sum, and backward a gradient
+// launch: ~230 launches of 3-6 us per C5 step.)
+constexpr int GT_MAX = 32;
+struct GanTerm {
+  const void* a; const void* b; void* ga;
+  int64_t rows;
+  int kind, width, lda, ldb, ldg, v8, g;
+};
+struct GanArgs {
+  GanTerm t[GT_MAX];
+  int blk0[GT_MAX + 1];
+  int n;
+};
+
+template <typename TA>
+__global__ void __launch_bounds__(256) gan_multi_reduce_kernel(GanArgs A, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int li = table_find(A.blk0, A.n, blockIdx.x);
+  const GanTerm& T = A.t[li];
+  const int64_t bi = blockIdx.x - A.blk0[li], gs = (int64_t)T.g * 256;
+  const TA* a = reinterpret_cast<const TA*>(T.a);
+  const TA* b = reinterpret_cast<const TA*>(T.b);
+  float s = 0.f;
+  if (T.v8) {
+    const RowMap rm{T.width / 8};
+    const int64_t nv = T.rows * rm.wv;
+    const bool flat = T.lda == T.width && (!b || T.ldb == T.width);
+    for (int64_t v = bi * 256 + threadIdx.x; v < nv; v += gs) {
+      int64_t oa = v * 8, ob = v * 8;
+      if (!flat) {
+        int64_t r;
+        int c;
+        rm.at(v, &r, &c);
+        oa = r * T.lda + c;
+        ob = r * T.ldb + c;
+      }
+      float x[8];
+      load8(a + oa, x);
+      if (T.kind == 0) {
+        float y[8];
+        load8(b + ob, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += fabsf(x[e] - y[e]);
+      } else if (T.kind == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (1.f - x[e]) * (1.f - x[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += x[e] * x[e];
+      }
+    }
+  } else {
+    const int64_t n = T.rows * T.width;
+    for (int64_t i = bi * 256 + threadIdx.x; i < n; i += gs) {
+      const int64_t r = i / T.width;
+      const int c = (int)(i - r * T.width);
+      const float x = to_f32(a[r * T.lda + c]);
+      if (T.kind == 0) {
+        s += fabsf(x - to_f32(b[r * T.ldb + c]));
+      } else if (T.kind == 1) {
+        s += (1.f - x) * (1.f - x);
+      } else {
+        s += x * x;
+      }
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// one wave per term: its partials added as gan_reduce_final_kernel adds them, times the term's scale
+__global__ void __launch_bounds__(64) gan_multi_final_kernel(GanArgs A, const float* __restrict__ part,
+                                                             const float* __restrict__ scale, float* __restrict__ out) {
+  const int li = blockIdx.x;
+  const int p0 = A.blk0[li], n = A.blk0[li + 1] - p0;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 64) s += part[p0 + i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[li] = (0.f + s) * (scale ? scale[li] : 1.f);
+}
+
+template <typename TA>
+__global__ void __launch_bounds__(256) gan_multi_grad_kernel(GanArgs A, const float* __restrict__ scale) {
+  const int li = table_find(A.blk0, A.n, blockIdx.x);
+  const GanTerm& T = A.t[li];
+  const int64_t bi = blockIdx.x - A.blk0[li], gs = (int64_t)(A.blk0[li + 1] - A.blk0[li]) * 256;
+  const TA* a = reinterpret_cast<const TA*>(T.a);
+  const TA* b = reinterpret_cast<const TA*>(T.b);
+  TA* ga = reinterpret_cast<TA*>(T.ga);
+  const float sc = scale[li];
+  if (T.v8) {
+    const RowMap rm{T.width / 8};
+    const int64_t nv = T.rows * rm.wv;
+    for (int64_t v = bi * 256 + threadIdx.x; v < nv; v += gs) {
+      int64_t r;
+      int c;
+      rm.at(v, &r, &c);
+      float x[8], g[8];
+      load8(a + r * T.lda + c, x);
+      if (T.kind == 0) {
+        float y[8];
+        load8(b + r * T.ldb + c, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = x[e] - y[e];
+          g[e] = d > 0.f ? sc : (d < 0.f ? -sc : 0.f);
+        }
+      } else if (T.kind == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = -2.f * (1.f - x[e]) * sc;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 2.f * x[e] * sc;
+      }
+      store8(ga + r * T.ldg + c, g);
+    }
+  } else {
+    const int64_t n = T.rows * T.width;
+    for (int64_t i = bi * 256 + threadIdx.x; i < n; i += gs) {
+      const int64_t r = i / T.width;
+      const int c = (int)(i - r * T.width);
+      const float x = to_f32(a[r * T.lda + c]);
+      float g;
+      if (T.kind == 0) {
+        const float d = x - to_f32(b[r * T.ldb + c]);
+        g = d > 0.f ? sc : (d < 0.f ? -sc : 0.f);
+      } else if (T.kind == 1) {
+        g = -2.f * (1.f - x) * sc;
+      } else {
+        g = 2.f * x * sc;
+      }
+      ga[r * T.ldg + c] = from_f32<TA>(g);
+    }
+  }
+}
+
 static bool v8_ok(const void* p, int64_t ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % 8 == 0); }
 
 
@@ -782,6 +925,74 @@ extern "C" int vo_gan_reduce(int kind, const void* a, int lda, const void* b, in
                        (const float*)b, ldb, rows, width, workspace);
   }
   hipLaunchKernelGGL(gan_reduce_final_kernel, dim3(1), dim3(64), 0, st, workspace, g, out);
+  VO_RETURN_LAUNCH();
+}
+
+// the term table of one launch: the block grid of each term as the single-term entry points size it
+static int gan_multi_args(const VoGanTerm* terms, int n, bool grad, GanArgs* A, int* blocks) {
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    const VoGanTerm& s = terms[i];
+    VO_CHECK_ARG(s.a && s.kind >= 0 && s.kind <= 2 && (s.kind != 0 || s.b) && (!grad || s.ga),
+                 "gan_reduce_multi: term %d: bad arguments", i);
+    VO_CHECK_ARG(s.rows > 0 && s.width > 0 && s.lda >= s.width && (s.kind != 0 || s.ldb >= s.width) &&
+                     (!grad || s.ldg >= s.width),
+                 "gan_reduce_multi: term %d: bad shape", i);
+    GanTerm& t = A->t[i];
+    t.a = s.a; t.b = s.b; t.ga = s.ga; t.rows = s.rows;
+    t.kind = s.kind; t.width = s.width; t.lda = s.lda; t.ldb = s.ldb; t.ldg = s.ldg;
+    t.v8 = s.width % 8 == 0 && v8_ok(s.a, s.lda) && v8_ok(s.b, s.ldb) && (!grad || v8_ok(s.ga, s.ldg));
+    const int64_t units = t.v8 ? s.rows * (s.width / 8) : s.rows * s.width;
+    t.g = grad ? grid_for(units) : std::min(grid_for(units), 512);
+    A->blk0[i] = total;
+    total += t.g;
+  }
+  A->blk0[n] = total;
+  A->n = n;
+  *blocks = total;
+  return VO_OK;
+}
+
+extern "C" int64_t vo_gan_reduce_multi_workspace_size(int n) {
+  return n <= 0 ? 0 : (int64_t)std::min(n, GT_MAX) * 512 * (int64_t)sizeof(float);
+}
+
+extern "C" int vo_gan_reduce_multi(int n, const VoGanTerm* terms, int dtype, const float* scale, float* out,
+                                   float* workspace, void* stream) {
+  VO_CHECK_ARG(n >= 0 && (n == 0 || (terms && out && workspace)) && (dtype == VO_BF16 || dtype == VO_F32),
+               "gan_reduce_multi: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += GT_MAX) {
+    GanArgs A;
+    int blocks;
+    const int m = std::min(GT_MAX, n - i0);
+    const int rc = gan_multi_args(terms + i0, m, false, &A, &blocks);
+    if (rc != VO_OK) return rc;
+    if (dtype == VO_BF16)
+      hipLaunchKernelGGL(gan_multi_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, A, workspace);
+    else
+      hipLaunchKernelGGL(gan_multi_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, A, workspace);
+    hipLaunchKernelGGL(gan_multi_final_kernel, dim3(m), dim3(64), 0, st, A, workspace, scale ? scale + i0 : nullptr,
+                       out + i0);
+  }
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_gan_reduce_grad_multi(int n, const VoGanTerm* terms, int dtype, const float* scale, void* stream) {
+  VO_CHECK_ARG(n >= 0 && (n == 0 || (terms && scale)) && (dtype == VO_BF16 || dtype == VO_F32),
+               "gan_reduce_grad_multi: bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += GT_MAX) {
+    GanArgs A;
+    int blocks;
+    const int m = std::min(GT_MAX, n - i0);
+    const int rc = gan_multi_args(terms + i0, m, true, &A, &blocks);
+    if (rc != VO_OK) return rc;
+    if (dtype == VO_BF16)
+      hipLaunchKernelGGL(gan_multi_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, A, scale + i0);
+    else
+      hipLaunchKernelGGL(gan_multi_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, A, scale + i0);
+  }
   VO_RETURN_LAUNCH();
 }
 

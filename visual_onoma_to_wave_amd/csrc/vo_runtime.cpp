@@ -91,7 +91,7 @@ static const char* const kSymbols[] = {
     "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask", "vo_conv1d_workspace_size",
     "vo_bn_workspace_size", "vo_bn_train_fwd", "vo_bn_bwd", "vo_vfe_conv_workspace_size", "vo_vfe_conv_fwd",
     "vo_vfe_conv_bwd", "vo_stft_mel_bwd_workspace_size", "vo_stft_mel_bwd", "vo_period_fold_bwd", "vo_wav_cl8_bwd",
-    "vo_avgpool_wav_bwd", "vo_weight_norm", "vo_weight_norm_bwd", "vo_pack_dgrad_phase", "vo_pack_batch", "vo_seq_remap", "vo_seq_remap2", "vo_lrelu_mask_add", "vo_lrelu_mask_sum", "vo_spectral_norm", "vo_spectral_norm_bwd", "vo_spectral_norm_bwd_workspace_size", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size", "vo_stft_mag",
+    "vo_avgpool_wav_bwd", "vo_weight_norm", "vo_weight_norm_bwd", "vo_pack_dgrad_phase", "vo_pack_batch", "vo_seq_remap", "vo_seq_remap2", "vo_lrelu_mask_add", "vo_lrelu_mask_sum", "vo_spectral_norm", "vo_gan_reduce_multi", "vo_gan_reduce_multi_workspace_size", "vo_gan_reduce_grad_multi", "vo_spectral_norm_bwd", "vo_spectral_norm_bwd_workspace_size", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size", "vo_stft_mag",
     "vo_stft_mag_bwd_workspace_size", "vo_stft_mag_bwd", "vo_stft_loss", "vo_stft_loss_grad",
     "vo_bucket_embed",   "vo_embed_bwd",     "vo_adam_multi",  "vo_opt_step_increment",
 };

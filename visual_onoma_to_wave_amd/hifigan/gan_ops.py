@@ -794,6 +794,15 @@ class GanLossFn(torch.autograd.Function):
         return ga, None, None, None
 
 
+# every term of a GanLossTermsFn / GanSplitTermsFn in one reduction launch pair and one gradient launch
+# (vo_gan_reduce_multi / _grad_multi, bit-identical to the per-term launches); 0: per term (A/B)
+GAN_MULTI = os.environ.get("VO_GAN_MULTI", "1") != "0"
+
+
+def _one_dtype(ts):
+    return all(t.dtype == ts[0].dtype for t in ts)
+
+
 class GanLossTermsFn(torch.autograd.Function):
     """Many GAN / feature-matching terms scale_i * reduce_i(a_i, b_i) as one (n,) vector: the
     reductions accumulate into one zeroed vector and are scaled by one multiply (the per-term path
@@ -804,11 +813,13 @@ class GanLossTermsFn(torch.autograd.Function):
     def forward(ctx, kinds, sv, *ab):
         n = len(kinds)
         a, b = ab[:n], ab[n:]
+        ctx.kinds = kinds
+        ctx.save_for_backward(sv, *a, *b)
+        if GAN_MULTI and _one_dtype(a):
+            return ops.gan_reduce_multi(kinds, a, b, sv)
         out = torch.zeros(n, dtype=torch.float32, device=a[0].device)
         for i in range(n):
             ops.gan_reduce(kinds[i], a[i], b[i], out=out[i])
-        ctx.kinds = kinds
-        ctx.save_for_backward(sv, *a, *b)
         return out * sv
 
     @staticmethod
@@ -816,8 +827,13 @@ class GanLossTermsFn(torch.autograd.Function):
         sv, *ab = ctx.saved_tensors
         n = len(ctx.kinds)
         gs = g.float() * sv
-        gas = [ops.gan_reduce_grad(ctx.kinds[i], ab[i], ab[n + i], gs[i]) if ctx.needs_input_grad[2 + i] else None
-               for i in range(n)]
+        # (all terms: the scale vector as it is -- indexing it by a host list would copy from the host
+        # inside graph capture)
+        if GAN_MULTI and all(ctx.needs_input_grad[2:2 + n]) and _one_dtype(ab[:n]):
+            gas = ops.gan_reduce_grad_multi(list(ctx.kinds), list(ab[:n]), list(ab[n:]), gs)
+        else:
+            gas = [ops.gan_reduce_grad(ctx.kinds[i], ab[i], ab[n + i], gs[i]) if ctx.needs_input_grad[2 + i] else None
+                   for i in range(n)]
         return (None, None, *gas, *([None] * n))
 
 
@@ -835,13 +851,16 @@ class GanSplitTermsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kinds, sv, *bases):
         n = len(bases)
+        ctx.kinds = kinds
+        ctx.save_for_backward(sv, *bases)
+        if GAN_MULTI and _one_dtype(bases):
+            halves = [s[: s.shape[0] // 2] for s in bases] + [s[s.shape[0] // 2:] for s in bases]
+            return ops.gan_reduce_multi([kinds[0]] * n + [kinds[1]] * n, halves, [None] * (2 * n), sv)
         out = torch.zeros(2 * n, dtype=torch.float32, device=bases[0].device)
         for i, s in enumerate(bases):
             h = s.shape[0] // 2
             ops.gan_reduce(kinds[0], s[:h], None, out=out[i])
             ops.gan_reduce(kinds[1], s[h:], None, out=out[n + i])
-        ctx.kinds = kinds
-        ctx.save_for_backward(sv, *bases)
         return out * sv
 
     @staticmethod
@@ -849,6 +868,13 @@ class GanSplitTermsFn(torch.autograd.Function):
         sv, *bases = ctx.saved_tensors
         n = len(bases)
         gs = g.float() * sv
+        if GAN_MULTI and all(ctx.needs_input_grad[2:2 + n]) and _one_dtype(bases):
+            grads = [torch.empty_like(s, memory_format=torch.contiguous_format) for s in bases]
+            hs = [s.shape[0] // 2 for s in bases]
+            As = [s[:h] for s, h in zip(bases, hs)] + [s[h:] for s, h in zip(bases, hs)]
+            outs = [g_[:h] for g_, h in zip(grads, hs)] + [g_[h:] for g_, h in zip(grads, hs)]
+            ops.gan_reduce_grad_multi([ctx.kinds[0]] * n + [ctx.kinds[1]] * n, As, [None] * (2 * n), gs, outs=outs)
+            return (None, None, *grads)
         grads = []
         for i, s in enumerate(bases):
             if not ctx.needs_input_grad[2 + i]:

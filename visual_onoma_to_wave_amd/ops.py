@@ -987,6 +987,58 @@ def gan_reduce_grad(kind, a, b, scale, out=None):
     return ga.reshape(a.shape)
 
 
+def _gan_terms(kinds, As, Bs, outs=None):
+    arr = (_lib.GanTerm * len(kinds))()
+    keep = []
+    for i, (k, a, b) in enumerate(zip(kinds, As, Bs)):
+        la, rows, width, lda = _rows_view(a)
+        e = arr[i]
+        e.kind, e.a, e.lda, e.rows, e.width = k, la.data_ptr(), lda, rows, width
+        keep.append(la)
+        if b is not None:
+            lb, rb, wb, ldb = _rows_view(b)
+            if (rb, wb) != (rows, width) or b.dtype != a.dtype:
+                raise ValueError("gan_reduce_multi: a / b mismatch")
+            e.b, e.ldb = lb.data_ptr(), ldb
+            keep.append(lb)
+        if outs is not None:
+            o = outs[i]
+            if not o.is_contiguous() or o.numel() != rows * width or o.dtype != a.dtype:
+                raise ValueError("gan_reduce_grad_multi: out must be contiguous, of a's dtype and size")
+            e.ga, e.ldg = o.data_ptr(), width
+    if any(a.dtype != As[0].dtype for a in As):
+        raise ValueError("gan_reduce_multi: one dtype for all terms")
+    return arr, keep
+
+
+def gan_reduce_multi(kinds, As, Bs, scale=None):
+    """[gan_reduce(kinds[i], As[i], Bs[i])] * scale as one (n,) fp32 vector in one launch pair
+    (vo_gan_reduce_multi; each sum bit for bit gan_reduce's).  ``scale``: (n,) fp32 device vector."""
+    n = len(kinds)
+    arr, keep = _gan_terms(kinds, As, Bs)
+    out = torch.empty(n, dtype=torch.float32, device=As[0].device)
+    L = _lib.lib()
+    ws = torch.empty(int(L.vo_gan_reduce_multi_workspace_size(n)) // 4, dtype=torch.float32, device=As[0].device)
+    sc = scale.float().contiguous() if scale is not None else None
+    _lib.check(L.vo_gan_reduce_multi(n, ctypes.cast(arr, ctypes.c_void_p), vo_dtype(As[0]), _ptr(sc), _ptr(out),
+                                     _ptr(ws), _stream(As[0])), "vo_gan_reduce_multi")
+    del keep
+    return out
+
+
+def gan_reduce_grad_multi(kinds, As, Bs, scale, outs=None):
+    """[gan_reduce_grad(kinds[i], As[i], Bs[i], scale[i])] in one launch (vo_gan_reduce_grad_multi);
+    ``outs``: contiguous tensors to write them into (default: new tensors shaped like As)."""
+    if outs is None:
+        outs = [torch.empty(a.shape, dtype=a.dtype, device=a.device) for a in As]
+    arr, keep = _gan_terms(kinds, As, Bs, outs)
+    sc = scale.float().contiguous()
+    _lib.check(_lib.lib().vo_gan_reduce_grad_multi(len(kinds), ctypes.cast(arr, ctypes.c_void_p), vo_dtype(As[0]),
+                                                   _ptr(sc), _stream(As[0])), "vo_gan_reduce_grad_multi")
+    del keep
+    return outs
+
+
 # ----------------------------------------------------------------------------- training input pipeline
 
 def glyph_batch(strips, char_widths, cell, margin, device, W_out=None):
