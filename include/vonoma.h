@@ -95,6 +95,11 @@ typedef struct vo_conv1d_desc {
                          reduction over workgroups and add the fp32 partials in a fixed
                          order (deterministic)                                           */
   int64_t workspace_bytes;
+  const void* ymask;  /* optional, y's layout and dtype (bf16 y, no bias / residual / activation):
+                         each output is stored as round(round(v) * (ymask > 0 ? 1 : ymask_slope))
+                         -- an input gradient masked by the leaky-ReLU output it flows into, as
+                         vo_lrelu_mask would mask it (HiFi-GAN discriminators, D step)          */
+  float ymask_slope;
 } vo_conv1d_desc;
 int vo_conv1d(const vo_conv1d_desc* d, void* stream);
 /* scratch bytes the split-reduction path of vo_conv1d wants for d (0 = it does not split d) */

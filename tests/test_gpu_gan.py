@@ -786,7 +786,7 @@ def test_discriminator_fmap_tap_bit_identical():
     yh = torch.tanh(torch.randn(4, 8192) * 0.3).cuda()
     orig = G.conv_layers
 
-    def plain_layers(x, convs):  # the per-layer path: conv() per layer, autograd sums the fan-out
+    def plain_layers(x, convs, fmaps=True):  # the per-layer path: conv() per layer, autograd sums the fan-out
         outs = []
         for w, b, spec, cdt, wkey in convs:
             x = G.conv(x, w, b, spec, cdt, wkey=wkey)
@@ -880,3 +880,30 @@ def test_gan_loss_terms_multi_bit_identical():
     assert ld0 == ld1 and lg0 == lg1
     assert all(torch.equal(a, b) for a, b in zip(gd0, gd1))
     assert torch.equal(gw0, gw1)
+
+
+def test_discriminator_dstep_epilogue_mask_bit_identical():
+    """D step with fmaps=False (each layer's leaky-ReLU backward applied by the next conv's
+    input-gradient epilogue, vo_conv1d ymask) against fmaps=True (the separate mask pass): the loss and
+    every MPD / MSD parameter gradient bit for bit; the detached feature maps equal the others."""
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MultiPeriodDiscriminator, MultiScaleDiscriminator,
+                                                                  discriminator_loss)
+    torch.manual_seed(8)
+    mpd = MultiPeriodDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    msd = MultiScaleDiscriminator().cuda().eval().set_compute_dtype(torch.bfloat16)
+    y = torch.tanh(torch.randn(8, 8192) * 0.3).cuda()
+    yh = torch.tanh(torch.randn(8, 8192) * 0.3).cuda()
+    params = list(mpd.parameters()) + list(msd.parameters())
+
+    def run(fm):
+        r1, g1, f1, _ = mpd(y, yh, fmaps=fm)
+        r2, g2, f2, _ = msd(y, yh, fmaps=fm)
+        ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
+        return float(ld), torch.autograd.grad(ld, params), [t.detach() for fs in f1 + f2 for t in fs]
+
+    ld0, gd0, f0 = run(True)
+    ld1, gd1, f1 = run(False)
+    assert ld0 == ld1
+    for i, (a, b) in enumerate(zip(gd0, gd1)):
+        assert torch.equal(a, b), i
+    assert all(torch.equal(a, b) for a, b in zip(f0, f1))

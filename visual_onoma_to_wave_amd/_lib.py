@@ -42,6 +42,7 @@ class Conv1dDesc(ctypes.Structure):
         ("variant", c_int),
         ("stride", c_int), ("groups", c_int),
         ("workspace", c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("ymask", c_void_p), ("ymask_slope", c_float),
     ]
 
 

@@ -48,6 +48,8 @@ struct ConvArgs {
   int cig, cog;  // channels per group (in / out): grouped conv = block-diagonal packed weights
   float* partial;  // split reduction: fp32 partials [splits][B][T_out][Co] (null = off)
   int kcs;         // 32-channel chunks per split (grid z = split)
+  const void* ymask;  // outputs stored as round(round(v) * (ymask > 0 ? 1 : ymask_slope)) (y's layout)
+  float ymask_slope;
 };
 
 template <typename T> struct Raw8;  // 8 elements of T held in registers
@@ -121,7 +123,8 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc
   bf16_t* Y = reinterpret_cast<bf16_t*>(a.y) + (int64_t)b * a.ybs;
   const bf16_t* R1 = reinterpret_cast<const bf16_t*>(a.res1 ? a.res1 : a.y) + (int64_t)b * a.ybs;
   const bf16_t* R2 = reinterpret_cast<const bf16_t*>(a.res2 ? a.res2 : a.y) + (int64_t)b * a.ybs;
-  const bool r1 = a.res1 != nullptr, r2 = a.res2 != nullptr;
+  const bool r1 = a.res1 != nullptr, r2 = a.res2 != nullptr, om = a.ymask != nullptr;
+  const bf16_t* YM = reinterpret_cast<const bf16_t*>(om ? a.ymask : a.y) + (int64_t)b * a.ybs;
   float bias[4 * NI];
 #pragma unroll
   for (int e = 0; e < 4 * NI; ++e) bias[e] = a.bias ? a.bias[n0 + e] : 0.f;
@@ -129,7 +132,7 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc
   const bool tanh_act = a.post_act == VO_ACT_TANH;
 #pragma unroll
   for (int j0 = 0; j0 < NJ; j0 += JG) {
-    uint4 rv1[JG][NH], rv2[JG][NH];
+    uint4 rv1[JG][NH], rv2[JG][NH], rvm[JG][NH];
 #pragma unroll
     for (int jj = 0; jj < JG; ++jj) {  // rows past T_out re-read the last row (not stored)
       const int pos = min(t0 + wave_t0 + 16 * (j0 + jj) + lr, a.T_out - 1);
@@ -138,6 +141,7 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc
       for (int h = 0; h < NH; ++h) {
         if (r1) rv1[jj][h] = *reinterpret_cast<const uint4*>(R1 + off + 8 * h);
         if (r2) rv2[jj][h] = *reinterpret_cast<const uint4*>(R2 + off + 8 * h);
+        if (om) rvm[jj][h] = *reinterpret_cast<const uint4*>(YM + off + 8 * h);
       }
     }
 #pragma unroll
@@ -173,6 +177,15 @@ __device__ __forceinline__ void conv_epilogue_vec(const ConvArgs& a, f32x4 (&acc
           v *= a.out_scale;
           if (r2) v += x2[e];
           q[e] = v;
+        }
+        if (om) {  // the leaky-ReLU backward of the layer whose output ymask is, on the stored value
+          const uint32_t w[4] = {rvm[jj][h].x, rvm[jj][h].y, rvm[jj][h].z, rvm[jj][h].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float m = __uint_as_float((e & 1) ? (w[e >> 1] & 0xffff0000u) : (w[e >> 1] << 16));
+            const float r = to_f32(from_f32<bf16_t>(q[e]));
+            q[e] = m > 0.f ? r : r * a.ymask_slope;
+          }
         }
         if (pos < a.T_out) store8(Y + off + 8 * h, q);
       }
@@ -248,6 +261,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[NI
         load4(R2 + off + 4 * h, rr);
 #pragma unroll
         for (int e = 0; e < 4; ++e) q[e] += rr[e];
+      }
+      if (a.ymask) {
+        float mm[4];
+        load4(reinterpret_cast<const TOUT*>(a.ymask) + (int64_t)b * a.ybs + off + 4 * h, mm);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float r = to_f32(from_f32<TOUT>(q[e]));
+          q[e] = mm[e] > 0.f ? r : r * a.ymask_slope;
+        }
       }
       store4(Y + off + 4 * h, q);
     }
@@ -763,6 +785,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   a.tiles_per_b = (d->T_out + BT - 1) / BT;
   a.co_tiles = (d->Co + BCO - 1) / BCO;
   a.B = d->B;
+  a.ymask = d->ymask; a.ymask_slope = d->ymask_slope;
   const int groups = d->groups > 1 ? d->groups : 1;
   a.cig = d->Ci / groups;
   a.cog = d->Co / groups;
@@ -923,6 +946,10 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
     VO_CHECK_ARG(d->Co % 16 == 0 || d->Co == 80 || d->Co <= 32, "conv1d: unsupported Co %d", d->Co);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(const_cast<void*>(stream));
+  VO_CHECK_ARG(!d->ymask || (d->y_dtype == VO_BF16 && !d->transposed && !d->bias && !d->res1 && !d->res2 &&
+                             d->post_act == VO_ACT_NONE && d->out_scale == 1.f && d->variant == 0 &&
+                             d->ymask_slope >= 0.f && d->ymask_slope <= 1.f),
+               "conv1d: ymask needs a bf16 output without bias, residuals, activation or scale, slope in [0, 1]");
   if (d->transposed) {  // narrow upsamplers: the persistent streaming kernel (upsample.hip)
     int handled = 0;
     const int rc = vo_ups_try(d, st, &handled);

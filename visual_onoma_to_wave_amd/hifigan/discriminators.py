@@ -144,8 +144,10 @@ class DiscriminatorP(_DiscBase):
             H, C = G.out_len(sp, H), m.out_channels
         return out
 
-    def forward(self, wav, W=None):
-        """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)]).  ``W``: effective
+    def forward(self, wav, W=None, fmaps=True):
+        """wav (B, T) fp32 -> (score (B * p, H'), fmaps [(B * p, H_l, C_l)]); ``fmaps`` False: the feature
+        maps come back detached (the D step), which lets each layer's leaky-ReLU backward ride in the next
+        conv's input-gradient epilogue (gan_ops.conv_layers).  ``W``: effective
         weights batched (and the convs' weights packed) by the caller (``_prepare``)."""
         cdt, adt = self.compute_dtype, self._act_dtype()
         layers = self._layers(*wav.shape)
@@ -154,7 +156,8 @@ class DiscriminatorP(_DiscBase):
         x = G.PeriodFoldFn.apply(wav, self.period, adt)
         # squeeze, not [..., 0]: its adjoint is a view of the 3-D weight gradient (select's was a zero
         # fill and a copy per conv and D step)
-        fmap = G.conv_layers(x, [(_w(m, W).squeeze(-1), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
+        fmap = G.conv_layers(x, [(_w(m, W).squeeze(-1), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers],
+                             fmaps)
         score = fmap[-1][..., 0].contiguous()
         fmap[-1] = score
         return score, fmap
@@ -170,7 +173,7 @@ class MultiPeriodDiscriminator(_DiscBase):
         layers = [d._layers(*wav.shape) for d in self.discriminators]
         return _prepare(self, layers, wav.requires_grad if dgrad_first is None else dgrad_first)
 
-    def forward(self, y, y_hat):
+    def forward(self, y, y_hat, fmaps=True):
         """Reference call convention: (y_d_rs, y_d_gs, fmap_rs, fmap_gs).  y and y_hat run as one
         batch (one launch per layer for both)."""
         B = y.shape[0]
@@ -179,7 +182,7 @@ class MultiPeriodDiscriminator(_DiscBase):
         rs, gs, frs, fgs = [], [], [], []
         for d in self.discriminators:
             p = d.period
-            s, fm = d(both, W)
+            s, fm = d(both, W, fmaps)
             rs.append(s[: B * p])
             gs.append(s[B * p:])
             frs.append([f[: B * p] for f in fm])
@@ -210,14 +213,14 @@ class DiscriminatorS(_DiscBase):
         out.append((self.conv_post, G.ConvSpec(K=3, pad=1, co_pad=8), (B, T, C)))
         return out
 
-    def forward(self, wav, W=None):
+    def forward(self, wav, W=None, fmaps=True):
         """wav (B, T) fp32 -> (score (B, T'), fmaps [(B, T_l, C_l)])."""
         cdt, adt = self.compute_dtype, self._act_dtype()
         layers = self._layers(*wav.shape)
         if W is None:
             W = _prepare(self, [layers], wav.requires_grad)
         x = G.WavCl8Fn.apply(wav, adt)
-        fmap = G.conv_layers(x, [(_w(m, W), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers])
+        fmap = G.conv_layers(x, [(_w(m, W), m.bias, sp, cdt, G.weight_key(m)) for m, sp, _ in layers], fmaps)
         score = fmap[-1][..., 0].contiguous()
         fmap[-1] = score
         return score, fmap
@@ -239,7 +242,7 @@ class MultiScaleDiscriminator(_DiscBase):
             layers.append(d._layers(B, T))
         return _prepare(self, layers, wav.requires_grad if dgrad_first is None else dgrad_first)
 
-    def forward(self, y, y_hat):
+    def forward(self, y, y_hat, fmaps=True):
         B = y.shape[0]
         x = torch.cat([y, y_hat], 0)
         W = self.prepare(x)
@@ -247,7 +250,7 @@ class MultiScaleDiscriminator(_DiscBase):
         for i, d in enumerate(self.discriminators):
             if i != 0:
                 x = G.AvgPoolFn.apply(x)
-            s, fm = d(x, W)
+            s, fm = d(x, W, fmaps)
             rs.append(s[:B])
             gs.append(s[B:])
             frs.append([f[:B] for f in fm])

@@ -189,11 +189,12 @@ def _conv_fwd(x, w, b, res1, res2, spec, cdt, wkey=None):
                       stride=spec.stride, groups=spec.groups)
 
 
-def _dgrad(gz, w, spec, x, cdt, wkey=None):
+def _dgrad(gz, w, spec, x, cdt, wkey=None, ymask=None, ymask_slope=0.0):
     """Input gradient of a strided and/or grouped conv (dil 1) on the HIP conv kernel, by phase:
     input row i = S m + r receives taps k = k_r + S j (k_r = (r + pad) mod S) from output rows
     m + c_r - j, so each residue r is a stride-1 grouped conv over dY with those taps reversed and
-    the channel roles swapped, written to rows r, r + S, ... of dX (row-strided output view)."""
+    the channel roles swapped, written to rows r, r + S, ... of dX (row-strided output view).
+    ``ymask`` (x's shape, contiguous): dX stored through the leaky-ReLU mask of it (vo_conv1d ymask)."""
     S, K, pad, g = spec.stride, spec.K, spec.pad, spec.groups
     if spec.dil != 1:
         raise NotImplementedError("strided / grouped input gradient with dilation")
@@ -217,6 +218,7 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
         if not taps:
             view.zero_()
             continue
+        mview = ymask[:, r::S] if ymask is not None else None
         J = len(taps)
         c_r = (r + pad - k_r) // S
         tag = (spec, cdt, "dgrad", r, ci_out, co_in)
@@ -228,7 +230,7 @@ def _dgrad(gz, w, spec, x, cdt, wkey=None):
             return ops.pack_dgrad_phase(w, g, S, k_r, J, ci_out, co_in, cdt, out=out)
         wp = _cached(wkey, tag, build)
         ops.conv1d(gzp, wp, None, Co=ci_out, K=J, pad=J - 1 - c_r, T_out=rows, out=view, compute_dtype=cdt,
-                   groups=g if ci_out == Ci else 1)
+                   groups=g if ci_out == Ci else 1, ymask=mview, ymask_slope=ymask_slope)
     return out
 
 
@@ -264,10 +266,13 @@ class ConvFn(torch.autograd.Function):
     (ResLink, "in" | "res"): this conv's input ("in") / res1 ("res") is the linked tensor.  ``tap``
     (leaky-ReLU post-activation): also return y a second time (same storage) for a second consumer
     (a discriminator feature map): the backward gets the two gradients apart and sums them in its
-    mask pass (vo_lrelu_mask_sum) instead of autograd adding them first."""
+    mask pass (vo_lrelu_mask_sum) instead of autograd adding them first.  ``in_mask`` (slope): x is
+    the leaky-ReLU output of the conv before, whose only gradient is this conv's input gradient:
+    that gradient is masked as the input-gradient conv stores it (vo_conv1d ymask); ``out_masked``:
+    the conv after does that for this conv's output, so its backward skips its own mask pass."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None, link=None, tap=False):
+    def forward(ctx, x, w, b, res1, res2, spec, cdt, wkey=None, link=None, tap=False, in_mask=None, out_masked=False):
         if spec.post is not None and (res1 is not None or res2 is not None):
             raise ValueError("ConvFn: post-activation with residual inputs is not differentiable here")
         y = _conv_fwd(x.contiguous(), w, b, res1, res2, spec, cdt, wkey)
@@ -282,6 +287,7 @@ class ConvFn(torch.autograd.Function):
             elif role == "res" and lk.armed and res1 is not None and res1.requires_grad:
                 ctx.link = (lk, "res")
         ctx.has = (res1 is not None, res2 is not None)
+        ctx.in_mask, ctx.out_masked = in_mask, out_masked and spec.post == "lrelu" and not tap
         ctx.save_for_backward(x, w, y if spec.post is not None else None)
         if tap:
             if spec.post != "lrelu" or res1 is not None or res2 is not None or spec.out_scale != 1.0:
@@ -298,7 +304,7 @@ class ConvFn(torch.autograd.Function):
         if gy is None:
             gy, gf = gf, None
         if gy is None:
-            return (None,) * 10
+            return (None,) * 12
         gy = gy.contiguous()
         g_res2 = gy if ctx.has[1] and ctx.needs_input_grad[4] else None
         gz = gy * spec.out_scale if spec.out_scale != 1.0 else gy
@@ -306,7 +312,9 @@ class ConvFn(torch.autograd.Function):
         lk, role = ctx.link if ctx.link is not None else (None, None)
         if role == "res" and g_res1 is not None:  # the residual's gradient goes to the linked input conv
             lk.g, g_res1 = g_res1, None
-        if spec.post == "lrelu":
+        if spec.post == "lrelu" and ctx.out_masked:
+            pass  # gy arrives masked (the next conv's input-gradient epilogue)
+        elif spec.post == "lrelu":
             ok = gf is not None and gf.dtype == gz.dtype and gf.shape == gz.shape and gz.shape[-1] % 8 == 0
             if gf is not None and not ok:
                 gz, gf = gz + gf, None
@@ -323,16 +331,22 @@ class ConvFn(torch.autograd.Function):
         gx = gw = gb = None
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         ga = None
+        im = ctx.in_mask
+        ga_masked = False
         if need_x and spec.plain():
             # cached per parameter version: a discriminator's next D step runs its backward at the
             # versions its G step's backward already packed
             wd = _cached(ctx.wkey, (spec, cdt, "dgrad_plain"), lambda: ops.pack_dgrad_weight(w, cdt))
+            ym = x if (im is not None and x.dtype == torch.bfloat16 and x.is_contiguous()) else None
             ga = ops.conv1d(gz.to(cdt), wd, None, Co=w.shape[1], K=spec.K, dil=spec.dil,
                             pad=(spec.K - 1) * spec.dil - spec.pad, T_out=x.shape[1], out_dtype=x.dtype,
-                            compute_dtype=cdt)
+                            compute_dtype=cdt, ymask=ym, ymask_slope=im or 0.0)
+            ga_masked = ym is not None
             need_x = False
         elif need_x and spec.transposed is None and spec.dil == 1:
-            ga = _dgrad(gz, w, spec, x, cdt, ctx.wkey)
+            ym = x if (im is not None and x.dtype == torch.bfloat16 and x.is_contiguous()) else None
+            ga = _dgrad(gz, w, spec, x, cdt, ctx.wkey, ymask=ym, ymask_slope=im or 0.0)
+            ga_masked = ym is not None
             if ga.shape[-1] != ci:
                 ga = ga[..., :ci]
             need_x = False
@@ -384,6 +398,8 @@ class ConvFn(torch.autograd.Function):
                 gw = gw2.to(w.dtype)
             if need_b:
                 gb = gb2
+        if ga is not None and im is not None and not ga_masked:
+            ga = ops.lrelu_mask(ga, xin, im)
         if ga is not None:
             add = None
             if role == "in" and lk.g is not None:  # this conv reads the linked tensor: its residual gradient joins here
@@ -401,7 +417,7 @@ class ConvFn(torch.autograd.Function):
             gw = None
         if not ctx.needs_input_grad[2]:
             gb = None
-        return gx, gw, gb, g_res1, g_res2, None, None, None, None, None
+        return gx, gw, gb, g_res1, g_res2, None, None, None, None, None, None, None
 
 
 # Many short sequences (the MPD's period columns: 96-352 sequences of 10-51 rows at C5): the conv
@@ -508,12 +524,17 @@ def _conv_joined(x, w, b, spec, cdt, wkey):
     return _split_output(yj, x.shape[0], S_out, T_out)
 
 
-def conv_layers(x, convs):
+def conv_layers(x, convs, fmaps=True):
     """The outputs of ``convs`` [(w, b, spec, cdt, wkey)] applied in order, as ``conv`` per layer;
     where one joined conv feeds the next, RejoinFn hands its joined output over (one remap launch
-    each way instead of a split and a join)."""
+    each way instead of a split and a join).  ``fmaps`` False (the D step: only the last output
+    carries a gradient, the others are returned detached): each leaky-ReLU output's mask is applied
+    by the next conv's input-gradient epilogue (ConvFn in_mask / out_masked), not by a mask pass."""
+    n = len(convs)
+    fold = [not fmaps and i + 1 < n and convs[i][2].post == "lrelu" for i in range(n)]
     outs, pend = [], None  # pend: (yj, N, S_out, T_out) of a joined conv whose output is not split yet
-    for w, b, spec, cdt, wkey in convs:
+    for i, (w, b, spec, cdt, wkey) in enumerate(convs):
+        fl = dict(in_mask=convs[i - 1][2].post_slope if i and fold[i - 1] else None, out_masked=fold[i])
         if pend is not None:
             yj, N, S_out, T = pend
             pend = None
@@ -522,22 +543,26 @@ def conv_layers(x, convs):
                 T_out2, S_out2, S_in2 = _join_plan(spec, T)
                 y, xj = RejoinFn.apply(yj, N, S_out, T, spec.pad, S_in2)
                 outs.append(y)
-                pend = (ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey), N, S_out2, T_out2)
+                pend = (ConvFn.apply(xj, w, b, None, None, replace(spec, pad=0), cdt, wkey, None, False, fl["in_mask"],
+                                     fl["out_masked"]), N, S_out2, T_out2)
                 continue
             x = _split_output(yj, N, S_out, T)
             outs.append(x)
         if _joined(x.shape, spec):
             T_out, S_out, _ = _join_plan(spec, x.shape[1])
-            yj = ConvFn.apply(_join_input(x, spec), w, b, None, None, replace(spec, pad=0), cdt, wkey)
+            yj = ConvFn.apply(_join_input(x, spec), w, b, None, None, replace(spec, pad=0), cdt, wkey, None, False,
+                              fl["in_mask"], fl["out_masked"])
             pend = (yj, x.shape[0], S_out, T_out)
-        elif spec.post == "lrelu":  # the feature map and the next conv's input: their gradients meet in the mask pass
+        elif spec.post == "lrelu" and fmaps:  # the feature map and the next conv's input: their gradients meet in the mask pass
             x, f = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey, None, True)
             outs.append(f)
         else:
-            x = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey)
+            x = ConvFn.apply(x, w, b, None, None, spec, cdt, wkey, None, False, fl["in_mask"], fl["out_masked"])
             outs.append(x)
     if pend is not None:
         outs.append(_split_output(pend[0], pend[1], pend[2], pend[3]))
+    if not fmaps:
+        outs = [o.detach() for o in outs[:-1]] + outs[-1:]
     return outs
 
 

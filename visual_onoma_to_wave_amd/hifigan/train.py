@@ -114,9 +114,11 @@ class HifiGanTrainer:
             p.requires_grad_(True)
         self.optim_d.zero_grad(set_to_none=True)
         yd = y_g_hat.detach()
-        r, g, _, _ = self.mpd(y, yd)
+        # fmaps=False: the feature maps carry no gradient here, so each layer's leaky-ReLU backward
+        # rides in the next conv's input-gradient epilogue (gan_ops.conv_layers)
+        r, g, _, _ = self.mpd(y, yd, fmaps=False)
         loss_disc_f, _, _ = discriminator_loss(r, g)
-        r, g, _, _ = self.msd(y, yd)
+        r, g, _, _ = self.msd(y, yd, fmaps=False)
         loss_disc_s, _, _ = discriminator_loss(r, g)
         loss_disc_all = loss_disc_s + loss_disc_f
         loss_disc_all.backward()

@@ -47,7 +47,7 @@ def _contig(t, name):
 def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_dtype=None,
            pre_act=ACT_NONE, pre_slope=0.0, post_act=ACT_NONE, post_slope=0.0, res1=None,
            res2=None, out_scale=1.0, compute_dtype=torch.bfloat16, transposed=None, variant=0,
-           tag=None, stride=1, groups=1):
+           tag=None, stride=1, groups=1, ymask=None, ymask_slope=0.0):
     """Channels-last conv: x (B, T_in, Ci) -> y (B, T_out, Co).
 
     ``w_packed``: [K][Co][Ci] in ``compute_dtype`` (see pack_conv_weight).
@@ -55,6 +55,9 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     ConvTranspose1d; then Co = s*C_out, K = 2, pad = 1 and y is (B, s*T_in, C_out).
     ``stride`` / ``groups``: strided and grouped convs (HiFi-GAN discriminators); grouped
     weights are packed dense with zeros outside the diagonal blocks (pack_conv_weight groups=).
+    ``ymask`` (the output's shape and strides, bf16): each output stored as
+    round(round(v) * (ymask > 0 ? 1 : ymask_slope)) -- an input gradient put through the leaky-ReLU
+    backward of the layer whose output ymask is (bit for bit vo_lrelu_mask on the stored output).
     """
     if x.dim() == 2:
         x = x.unsqueeze(0)
@@ -108,6 +111,12 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
     d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
     d.stride, d.groups = stride, groups
+    if ymask is not None:
+        if ymask.dim() == 2:
+            ymask = ymask.unsqueeze(0)
+        if ymask.shape != out.shape or ymask.stride() != out.stride() or ymask.dtype != out.dtype:
+            raise ValueError("conv1d: ymask must match the output (shape, strides, dtype)")
+        d.ymask, d.ymask_slope = ymask.data_ptr(), float(ymask_slope)
     ws = None
     if compute_dtype == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
         # split-reduction scratch for the short fp32 convs (stream-ordered: freed after enqueue)
