@@ -40,6 +40,11 @@ enum vo_act { VO_ACT_NONE = 0, VO_ACT_RELU = 1, VO_ACT_LRELU = 2, VO_ACT_TANH = 
 
 /* ------------------------------------------------------------------ runtime */
 const char* vo_last_error(void);
+/* ABI version of this header; vo_version() returns the library's.  A binding checks they are equal
+ * at load time.  2 (round 4): vo_bucket_embed gained n_table (before n), vo_conv1d_desc gained
+ * ymask / ymask_slope at its end -- a version-1 binding would pass shifted arguments or leave the
+ * new fields uninitialised. */
+#define VO_ABI_VERSION 2
 int vo_version(void);
 /* number of entry points and their names (used by the loader test) */
 int vo_num_symbols(void);

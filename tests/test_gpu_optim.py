@@ -226,6 +226,51 @@ def test_capturable_lr_survives_load_state_dict():
             fl.step()
 
 
+def test_step_captured_before_load_state_dict_follows_it():
+    """A step captured BEFORE load_state_dict: the load copies the step count and the moments into the
+    device tensors the graph reads and writes (as it does the learning rate), so the replay continues
+    from the loaded state exactly as an eager optimizer that loaded the same state."""
+    from visual_onoma_to_wave_amd.optim import FusedAdam
+    init = _params(5, 4)
+    grads = [[g.cuda() for g in gs] for gs in _grads(7, init, 3)]
+    ps = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    opt = FusedAdam(ps, lr=torch.tensor(2e-3, device="cuda"), capturable=True)
+    for p, g in zip(ps, grads[0]):
+        p.grad = g.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        opt.step()  # warm-up: creates the state the graph will use
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        opt.step()
+    # a different optimizer history (three steps of other gradients) to resume from
+    src = [torch.nn.Parameter(p.clone().cuda()) for p in init]
+    other = torch.optim.Adam(src, lr=2e-3)
+    for gs in grads:
+        for p, g in zip(src, gs):
+            p.grad = g.clone() * 0.5
+        other.step()
+    sd = other.state_dict()
+    opt.load_state_dict(sd)
+    with torch.no_grad():
+        for p, q in zip(ps, src):
+            p.copy_(q)
+    eager = [torch.nn.Parameter(q.detach().clone()) for q in src]
+    ref = FusedAdam(eager, lr=torch.tensor(2e-3, device="cuda"), capturable=True)
+    ref.load_state_dict(sd)
+    for p, q, g in zip(ps, eager, grads[0]):
+        p.grad.copy_(g)
+        q.grad = g.clone()
+    graph.replay()
+    ref.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ps, eager):
+        assert torch.equal(a.detach(), b.detach())
+    assert float(opt.state[ps[0]]["step"]) == 4.0
+
+
 def test_load_state_dict_refuses_unequal_steps():
     from visual_onoma_to_wave_amd.optim import FusedAdam
     ps = [torch.nn.Parameter(torch.randn(4, device="cuda")) for _ in range(2)]

@@ -25,7 +25,7 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "mrf_common.h"
+#include "mrf_common.h"  // visual_onoma_to_wave_amd/csrc (make abl adds it to the include path)
 
 namespace vo {
 

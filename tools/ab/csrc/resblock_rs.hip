@@ -26,7 +26,7 @@
 #ifdef VO_ABLATIONS  // round-4 C = 128 candidate (register-streamed weights): measured slower, A/B builds only
 #include <type_traits>
 
-#include "mrf_common.h"
+#include "mrf_common.h"  // visual_onoma_to_wave_amd/csrc (make abl adds it to the include path)
 
 namespace vo {
 

@@ -212,6 +212,7 @@ _SIGNATURES = {
                                c_int, c_int, c_void_p, c_void_p]),
 }
 
+ABI_VERSION = 2  # include/vonoma.h VO_ABI_VERSION
 _lib = None
 
 
@@ -228,6 +229,9 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        if handle.vo_version() != ABI_VERSION:  # the signatures above are those of this ABI version
+            raise RuntimeError(f"visual_onoma_to_wave_amd: {LIB_PATH} has ABI version {handle.vo_version()}, "
+                               f"the bindings expect {ABI_VERSION} (include/vonoma.h VO_ABI_VERSION); rebuild it")
         _lib = handle
     return _lib
 

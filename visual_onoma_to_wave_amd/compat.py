@@ -123,9 +123,10 @@ def _load_caller(modname):
         sys.modules[name] = mod
         try:
             spec.loader.exec_module(mod)
-        except Exception as e:
+        except BaseException as e:  # SystemExit / KeyboardInterrupt too: no half-initialised module stays
             del sys.modules[name]
-            _caller_errors[modname] = e
+            if isinstance(e, Exception):  # only ordinary errors are remembered (not retried)
+                _caller_errors[modname] = e
             raise
     _caller_mods[modname] = mod
     return mod

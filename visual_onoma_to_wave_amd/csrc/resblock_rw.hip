@@ -1,0 +1,354 @@
+// HiFi-GAN ResBlock1 pair at C = 128 (MRF stage 1), k = 7 / 11 -- "wave-owned output planes":
+//   y = (x + c2(lrelu(c1_d(lrelu(x), slope), slope))) * out_scale (+ acc)
+// (scripts/hifigan/models.py:96-103, one (c1, c2) iteration; the MRF sum and 1/num_kernels scale of
+// models.py:155-160 ride in the epilogue).
+//
+// Why a new kernel (round 5).  The LDS-tile pair (resblock.hip) shares every streamed weight tap
+// between its 8 waves through LDS, so each of the 2K taps per tile ends in a workgroup barrier; with
+// two waves per SIMD the younger one finishes each tap a tail later (oldest-first arbitration) and
+// every wave waits for it -- 0.43 of the dense bf16 peak for three rounds.  Here the workgroup is 4
+// waves, one per SIMD, and wave w owns the 32 output channels of plane w for ALL 256 rows of the tile:
+//   * its weights (32 co x 128 ci per tap = 8 KiB) go straight from L2 into its own registers, two
+//     taps ahead (a 3-slot ring) -- no wave reads another wave's weights, so no tap needs a barrier;
+//   * the activations it multiplies them with (the lrelu'd input window in P1, c1's output T1 in P2)
+//     are shared through LDS, and only those hand-offs synchronise: 2 barriers per tile, not 2K + 2;
+//   * v_mfma_f32_16x16x32_bf16, 2 co tiles x 16 row tiles per wave: per MFMA 0.5 ds_read_b128 of B
+//     (128 B/clk per CU, half the LDS array) and 1/16 of a global load of A;
+//   * the next tile's window is fetched during P2 (the window is dead once P1 ends; T1 has its own
+//     buffer) and written, lrelu'd, two taps after its loads were issued;
+//   * LDS layout [plane][row][32 ch] with 16-byte chunk q of row r at q ^ ((r >> 1) & 3): the B-fragment
+//     reads (16 rows x 4 chunks at ANY row offset -- the taps shift rows by k*dil), the T1 stores and
+//     the window stores (plane stride of 321 rows: odd) are all bank-conflict free (checked exhaustively
+//     over the lane groups of ds_read_b128 / ds_write_b128, MI355X_MICROARCH.md section LDS);
+//   * output channels permuted in the A rows so that a lane's two accumulators of one row tile are the
+//     8 consecutive channels 32w + 8(l>>4) .. +7 of row (l & 15): one 16-byte T1 store / y store per row
+//     tile, in the layout the next conv's B fragments read.
+// Weights: the ordinary [K][C_out][C_in] bf16 pack (vo_pack_weight); bias fp32.
+
+#include <algorithm>
+#include <type_traits>
+
+#include "mrf_common.h"
+
+namespace vo {
+
+struct PrwArgs {
+  const bf16_t* x; const bf16_t* w1; const float* b1; const bf16_t* w2; const float* b2;
+  bf16_t* y; const bf16_t* acc;
+  int T, dil, tiles_per_b, ntiles;
+  float slope, out_scale;
+  unsigned long long* stamps;  // diagnostic builds only (-DVO_PRW_STAMPS, tools/probes/prw_stamps.py)
+};
+
+constexpr int RW_C = 128;
+constexpr int RW_R1 = 256;                // c1 rows per tile
+constexpr int RW_WP = RW_R1 + 64 + 1;     // window rows per plane: halo <= 64 (odd: conflict-free stores)
+constexpr int RW_TP = RW_R1 + 16;         // T1 rows per plane: P2 reads up to row R1 + K - 2
+constexpr int RW_NSTW = 16, RW_NSTT = 4, RW_NPT = 2 * 11 + 6;  // stamp geometry (diagnostic builds)
+constexpr size_t RW_LDS = (size_t)4 * (RW_WP + RW_TP) * 32 * sizeof(bf16_t) + 2 * RW_C * sizeof(float);
+
+__device__ __forceinline__ int rw_off(int r, int q) { return r * 32 + 8 * (q ^ ((r >> 1) & 3)); }
+
+template <int K, bool ACC, bool ST = false>
+__global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
+  constexpr int C = RW_C, R1 = RW_R1, NJ = R1 / 16;
+  constexpr int WP = RW_WP, TP = RW_TP;
+  constexpr int H2 = (K - 1) / 2, BT = R1 - 2 * H2;
+  constexpr int NWV = (R1 + 64) * 16 / 256;   // window vectors (16 B) per thread
+  constexpr int SPT = (NWV + K - 3) / (K - 2);  // window slots loaded per P2 tap (taps 0 .. K-3)
+  constexpr int RD = 48;                      // MRF-accumulator prefetch distance (steps)
+  constexpr int NST = NJ * 4;                 // (row tile, plane) steps per tap
+  constexpr int NB = 10, DB = 8;              // B-fragment ring / prefetch distance in steps
+  static_assert(SPT * (K - 2) >= NWV && SPT <= 4, "window staging");
+
+  const int T = a.T, dil = a.dil;
+  const int h1 = dil * H2;
+  const float slope = a.slope;
+
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);  // [4][WP][32]
+  bf16_t* t1 = win + 4 * WP * 32;                      // [4][TP][32]
+  float* sbias = reinterpret_cast<float*>(t1 + 4 * TP * 32);  // [b1 | b2]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output plane of this wave
+  const int lr = lane & 15, lg = lane >> 4;
+  // ST (diagnostic builds): s_memtime at fixed points of the first RW_NSTT tiles of workgroups
+  // 0 .. RW_NSTW-1, written by lane 0 of each wave to a buffer nothing else reads
+  int st_tile = 0;
+  auto stamp = [&](int idx) {
+    if constexpr (ST) {
+      if (blockIdx.x < RW_NSTW && st_tile < RW_NSTT && lane == 0)
+        a.stamps[((blockIdx.x * 4 + w) * RW_NSTT + st_tile) * RW_NPT + idx] = __builtin_amdgcn_s_memtime();
+    }
+  };
+
+  // contiguous tile run of this workgroup (uniform per workgroup: the early exit is safe)
+  const int G = gridDim.x;
+  int tile = (int)(((int64_t)blockIdx.x * a.ntiles) / G);
+  const int tile_end = (int)(((int64_t)(blockIdx.x + 1) * a.ntiles) / G);
+  if (tile >= tile_end) return;
+
+  for (int i = tid; i < 2 * C; i += 256) sbias[i] = i < C ? a.b1[i] : a.b2[i - C];
+
+  // ---- A fragments: lane l holds W[tap][co][ci] for co = 32w + 8(lr>>2) + 4t + (lr&3) (co tile t:
+  // accumulator register i of lane l is then channel 32w + 8lg + 4t + i) and ci = 32s + 8lg .. +7
+  // loads through buffer resources: 32-bit lane offsets (a 64-bit address per load kept 2 VGPRs live
+  // each and spilled), rows outside an utterance read as 0 (the convs' zero padding) with no clamp
+  const int aoff = ((32 * w + 8 * (lr >> 2) + (lr & 3)) * C + 8 * lg) * (int)sizeof(bf16_t);
+  const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, K * C * C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, K * C * C * 2, 0x00020000);
+  // 2-slot ring: tap u's fragments in slot u % 2; tap u + 1's are requested over the first 16 steps of
+  // tap u (2K is even, so a tile's last tap prefetches the next tile's first into slot 0)
+  bf16x8 A[2][4][2];
+  auto loadA_piece = [&](int u, int i) {  // u: tap in the tile's 2K-tap sequence (mod 2K); i = 2s + t
+    const int uu = u % (2 * K);
+    const int tap_off = (uu < K ? uu : uu - K) * (C * C * 2);
+    const int s = i >> 1, t = i & 1;
+    A[uu & 1][s][t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(uu < K ? rw1 : rw2,
+                                             aoff + t * 4 * C * 2 + s * 64, tap_off, 0));
+  };
+  auto utt = [&](const bf16_t* p, int b) {  // one utterance of a (B, T, C) tensor
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (int64_t)b * T * C), (short)0, T * C * 2, 0x00020000);
+  };
+
+  // ---- window staging: vector v = tid + 256 * slot = (row xr + 16 slot, 16-byte column xc)
+  const int xr = tid >> 4, xc = tid & 15;
+  const int xl = (xc >> 2) * WP * 32 + rw_off(xr, xc & 3);  // + slot * 16 rows (swizzle unchanged)
+  u32x4 xw[NWV];
+  auto load_win1 = [&](int tl, int sl) {
+    const int b = tl / a.tiles_per_b;
+    const int R0 = (tl - b * a.tiles_per_b) * BT - H2 - h1;
+    // rows before 0 / past T are out of the utterance's range and read 0 (the conv's zero padding)
+    xw[sl] = __builtin_amdgcn_raw_buffer_load_b128(utt(a.x, b), ((R0 + xr + 16 * sl) * C + xc * 8) * 2, 0, 0);
+  };
+  auto store_win1 = [&](int sl) { *reinterpret_cast<u32x4*>(win + xl + sl * 16 * 32) = lrelu8(xw[sl], slope); };
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) loadA_piece(0, i);
+#pragma unroll
+  for (int sl = 0; sl < NWV; ++sl) load_win1(tile, sl);
+#pragma unroll
+  for (int sl = 0; sl < NWV; ++sl) store_win1(sl);
+
+  f32x4 acc[2][NJ];
+  bf16x8 Bq[NB];
+
+  // One conv over the tile: K taps x 4 input planes x 16 row tiles, steps j-major inside a tap.  PH = 0:
+  // c1 over the window (row step dil, taps u = k); PH = 1: c2 over T1 (row step 1, taps u = K + k).
+  // Every step is one B-fragment read (DB steps ahead) and two MFMAs; the other work is spread one piece
+  // per step, so that it issues in the MFMAs' free issue cycles instead of stalling the matrix pipe:
+  // the next tap's A fragments (steps 0, 2, .., 14), hook(k, jj) (window staging, residual loads), and
+  // in the last tap the epilogue of row tile j in four parts during row tile j + 1's four steps (its
+  // accumulators are final after its own four steps).
+  auto conv = [&](auto ph, auto hook, auto post, auto cinit) {
+    constexpr int PH = decltype(ph)::value;
+    const bf16_t* src = PH ? t1 : win;
+    constexpr int PL = (PH ? TP : WP) * 32;  // plane stride (elements)
+    const int step = PH ? 1 : dil;
+    // the lane's row / chunk, opaque per tile: the per-tap B addresses are recomputed where they are
+    // used (hoisted out of the tile loop, 2 x 2K of them were live throughout and spilled)
+    int lro = lr, lgo = lg;
+    asm volatile("" : "+v"(lro), "+v"(lgo));
+    auto readB = [&](int q) {  // q: step index over the conv (tap q / NST, row tile, plane)
+      const int k = q / NST, j = (q % NST) / 4, s = q % 4;
+      // planes 0-1 and 2-3 from two bases: the ds_read offset field holds 16 bits
+      const bf16_t* base = src + (s >> 1) * 2 * PL + rw_off(k * step + lro, lgo);
+      Bq[q % NB] = *reinterpret_cast<const bf16x8*>(base + (s & 1) * PL + j * 512);
+    };
+#pragma unroll
+    for (int q = 0; q < DB; ++q) readB(q);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int u = PH * K + k;
+      stamp(2 + PH * (K + 2) + k);
+      const bf16x8(&Ak)[4][2] = A[u & 1];
+#pragma unroll
+      for (int jj = 0; jj < NST; ++jj) {
+        const int q = k * NST + jj;
+        const int j = jj / 4, s = jj % 4;
+        if (q + DB < K * NST) readB(q + DB);
+        if (jj < 16 && jj % 2 == 0) loadA_piece(u + 1, jj / 2);
+        hook(k, jj);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 b = Bq[q % NB];
+        if (k == 0 && s == 0) {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, cinit(j, 0), 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, cinit(j, 1), 0, 0, 0);
+        } else {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, acc[1][j], 0, 0, 0);
+        }
+        if (k == K - 1 && j > 0) post(j - 1, s);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) post(NJ - 1, p);
+  };
+
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / a.tiles_per_b;
+    const int t0 = (tile - b * a.tiles_per_b) * BT;
+    const int ntile = tile + 1 < tile_end ? tile + 1 : tile;  // next window (unconditional loads)
+
+    stamp(0);
+    lds_barrier();  // window staged; the previous P2's T1 reads are done
+    stamp(1);
+
+    // ---- P1: T1 = lrelu(c1(window) + b1), rows outside [0, T) = 0 (c2's zero padding).  During its last
+    // two taps this tile's residual rows x are requested in the accumulator layout: they enter P2 as the
+    // C operand of its first MFMAs (acc = b2 + x + c2), a whole tap and the B1 barrier after the request
+    const bool interior = t0 - H2 >= 0 && t0 - H2 + R1 <= T;
+    const int cofs = 32 * w + 8 * lg;
+    const __amdgpu_buffer_rsrc_t rsx = utt(a.x, b);
+    u32x4 xres[NJ];
+    auto p1_hook = [&](int k, int jj) {
+      const int g = (k - (K - 2)) * NST + jj;
+      if (g >= 0 && g % 8 == 0) {
+        const int j = g / 8;
+        xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((t0 + 16 * j + lr) * C + cofs) * 2, 0, 0);  // past T: 0
+      }
+    };
+    const f32x4* bias1 = reinterpret_cast<const f32x4*>(sbias + cofs);
+    const f32x4 b1z0 = bias1[0], b1z1 = bias1[1];
+    auto p1_cinit = [&](int, int t) { return t ? b1z1 : b1z0; };
+    uint32_t pv[4];
+    auto p1_post = [&](int j, int p) {  // part p: channels 2p, 2p + 1 of the lane's 8; part 3 stores
+      const int t = p >> 1, e = 2 * (p & 1);
+      pv[p] = lrelu_pk(acc[t][j][e], acc[t][j][e + 1], slope);
+      if (p == 3) {
+        const int r = 16 * j + lr;
+        const int pos = t0 - H2 + r;
+        u32x4 v = u32x4{pv[0], pv[1], pv[2], pv[3]};
+        if (!interior) v &= (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        *reinterpret_cast<u32x4*>(t1 + w * TP * 32 + rw_off(r, lg)) = v;
+      }
+    };
+    conv(std::integral_constant<int, 0>{}, p1_hook, p1_post, p1_cinit);
+    stamp(2 + K);
+    lds_barrier();  // T1 complete; every wave is past its window reads
+    stamp(3 + K);
+
+    // ---- P2: y = (b2 + x + c2(T1)) * out_scale (+ acc); the next window is staged meanwhile:
+    // SPT slots loaded per tap in taps 0 .. K-3 and written (lrelu'd) two taps later
+    const int valid = min(BT, T - t0);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
+    u32x4 ares[NJ];
+    const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
+    auto p2_hook = [&](int k, int jj) {
+      if (jj >= 20 && (jj - 20) % 8 == 0) {
+        const int i = (jj - 20) / 8, sl = k * SPT + i;
+        if (i < SPT && k <= K - 3 && sl < NWV) load_win1(ntile, sl);
+      }
+      if (jj >= 24 && (jj - 24) % 8 == 0) {
+        const int i = (jj - 24) / 8, sl = (k - 2) * SPT + i;
+        if (i < SPT && k >= 2 && sl < NWV) store_win1(sl);
+      }
+      if constexpr (ACC) {  // the MRF accumulator rows, RD steps before each row tile's epilogue
+        const int g = k * NST + jj, g0 = (K - 1) * NST + 4 - RD;
+        if (g >= g0 && g < g0 + NST && (g - g0) % 4 == 0) {
+          const int j = (g - g0) / 4;
+          ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((t0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
+        }
+      }
+    };
+    const f32x4* bias2 = reinterpret_cast<const f32x4*>(sbias + C + cofs);
+    const f32x4 b2z0 = bias2[0], b2z1 = bias2[1];
+    auto p2_cinit = [&](int j, int t) {  // b2 + x (the residual) for row tile j, channels of co tile t
+      const uint32_t lo = xres[j][2 * t], hi = xres[j][2 * t + 1];
+      const f32x4 xv = f32x4{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+      return (t ? b2z1 : b2z0) + xv;
+    };
+    const float osc = a.out_scale;
+    auto p2_post = [&](int j, int p) {  // part p: channels 2p, 2p + 1 of the lane's 8; part 3 stores
+      float q[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = 2 * p + u;
+        q[u] = acc[e >> 2][j][e & 3] * osc;
+        if constexpr (ACC) {
+          const uint32_t aw2 = ares[j][p];
+          q[u] += __uint_as_float(u ? (aw2 & 0xffff0000u) : (aw2 << 16));
+        }
+      }
+      pv[p] = pk_bf16(q[0], q[1]);
+      if (p == 3)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{pv[0], pv[1], pv[2], pv[3]}, yrs,
+                                               ((16 * j + lr) * C + cofs) * (int)sizeof(bf16_t), 0, 0);
+    };
+    conv(std::integral_constant<int, 1>{}, p2_hook, p2_post, p2_cinit);
+    stamp(4 + 2 * K);
+    ++st_tile;
+  }
+}
+
+template <int K, bool ACC>
+static int prw_launch(PrwArgs a, int B, hipStream_t st) {
+  constexpr int BT = RW_R1 - 2 * ((K - 1) / 2);
+  a.tiles_per_b = (a.T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  auto kern = mrf_prw_kernel<K, ACC>;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const int grid = (int)std::min<int64_t>((int64_t)cus, a.ntiles);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), RW_LDS, st, a);
+  VO_RETURN_LAUNCH();
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+// Entry from vo_resblock_pair (resblock.hip): *handled = 1 when this kernel covers the shape
+// (C = 128, K = 7 / 11, (K - 1) * dil <= 64).
+int vo_pair_rw_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                   const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
+                   hipStream_t st, int* handled) {
+  *handled = 0;
+  if (!(C == 128 && (K == 7 || K == 11) && dil >= 1 && dil * (K - 1) <= 64)) return VO_OK;
+  if (cfg == 93 || cfg == 99) return VO_OK;  // 93: the LDS-tile kernels (A/B)
+  PrwArgs a;
+  a.x = (const bf16_t*)x; a.w1 = (const bf16_t*)w1; a.b1 = b1; a.w2 = (const bf16_t*)w2; a.b2 = b2;
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
+  a.T = T; a.dil = dil; a.slope = slope; a.out_scale = out_scale;
+  a.tiles_per_b = a.ntiles = 0;
+  a.stamps = nullptr;
+  *handled = 1;
+  if (K == 7) return acc ? prw_launch<7, true>(a, B, st) : prw_launch<7, false>(a, B, st);
+  return acc ? prw_launch<11, true>(a, B, st) : prw_launch<11, false>(a, B, st);
+}
+
+#ifdef VO_PRW_STAMPS
+// Diagnostic entry (tools/probes/prw_stamps.py builds its own library with -DVO_PRW_STAMPS): one stamped
+// launch at the given shape; host_out receives RW_NSTW x 4 waves x RW_NSTT tiles x RW_NPT stamps.
+extern "C" int vo_prw_stamps(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
+                             const void* acc, int B, int T, int K, int dil, unsigned long long* host_out) {
+  const size_t n = (size_t)RW_NSTW * 4 * RW_NSTT * RW_NPT;
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, n * 8) != hipSuccess) return -1;
+  (void)hipMemset(d, 0, n * 8);
+  PrwArgs a;
+  a.x = (const bf16_t*)x; a.w1 = (const bf16_t*)w1; a.b1 = b1; a.w2 = (const bf16_t*)w2; a.b2 = b2;
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
+  a.T = T; a.dil = dil; a.slope = 0.1f; a.out_scale = 1.f / 3; a.stamps = d;
+  const int BT = RW_R1 - 2 * ((K - 1) / 2);
+  a.tiles_per_b = (T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  const int grid = std::min(256, a.ntiles);
+  if (K == 11)
+    hipLaunchKernelGGL((mrf_prw_kernel<11, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+  else
+    hipLaunchKernelGGL((mrf_prw_kernel<7, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(host_out, d, n * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return 0;
+}
+#endif

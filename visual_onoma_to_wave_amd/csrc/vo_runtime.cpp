@@ -18,7 +18,7 @@ extern "C" void vo_set_error(const char* fmt, ...) {
 
 extern "C" const char* vo_last_error(void) { return g_err; }
 
-extern "C" int vo_version(void) { return 1; }
+extern "C" int vo_version(void) { return VO_ABI_VERSION; }
 
 // experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0.
 // VO_TUNE="pair_cfg=1,conv_cfg=1" presets them for a whole process (bench A/B).

@@ -476,6 +476,9 @@ class RejoinFn(torch.autograd.Function):
     def forward(ctx, yj, N, S_out, T, pad, S_in):
         C = yj.shape[-1]
         ctx.dims = (yj.shape[1], N, S_out, T, pad, S_in)
+        # an output that carries no gradient (the D step's detached feature maps) arrives as None, and
+        # the backward then gathers the other one alone instead of adding a zero-filled tensor
+        ctx.set_materialize_grads(False)
         y, xj = ops.seq_remap2([dict(src=yj, dst_rows=N * T, Td=T, Ss=S_out, lo=0, hi=T, shift=0),
                                 dict(src=yj, dst_rows=N * S_in, Td=S_in, Ss=S_out, lo=pad, hi=pad + T, shift=-pad)])
         return y.view(N, T, C), xj.view(1, N * S_in, C)

@@ -12,8 +12,9 @@ Semantics: torch's single-tensor Adam / AdamW (amsgrad and maximize off).  One s
 param group (every ``state[p]["step"]`` is that group's tensor): parameters are updated together,
 as in the training steps here -- ``load_state_dict`` refuses a group whose per-parameter steps
 differ, and ``step`` warns when a parameter first gets a gradient after the group's first step.
-A capturable group's device-tensor learning rate survives ``load_state_dict`` (the loaded value is
-copied into it), and capturing a step with a float learning rate raises.  fp32 parameters,
+``load_state_dict`` copies the loaded values into the device tensors a captured step uses -- a capturable
+group's learning rate, the group's step tensor and the moments -- so a graph captured before the load
+continues from the loaded state; capturing a step with a float learning rate raises.  fp32 parameters,
 gradients and moments on the GPU.
 """
 
@@ -75,23 +76,40 @@ class FusedAdam(torch.optim.Optimizer):
             if len(steps) > 1:
                 raise ValueError(f"FusedAdam: param group {i} has unequal per-parameter steps {sorted(steps)[:4]}; "
                                  "one step count per group is supported")
-        # a device-tensor learning rate (capturable groups) is the tensor a captured graph reads: keep
-        # that tensor and copy the loaded value into it (torch's update_group puts a Python float there)
+        # a captured graph reads and writes the device tensors it was captured with -- a capturable group's
+        # learning rate, the group's step tensor and every parameter's moments: keep those tensors and
+        # copy the loaded values into them (torch's load_state_dict puts a float / the caller's tensors
+        # there), so a step captured before the load continues from the loaded state
         lr_tensors = [g["lr"] if torch.is_tensor(g["lr"]) else None for g in self.param_groups]
+        step_tensors = [g.get("_vo_step") for g in self.param_groups]
+        moments = {p: {k: self.state[p][k] for k in ("exp_avg", "exp_avg_sq") if k in self.state.get(p, {})}
+                   for g in self.param_groups for p in g["params"]}
         super().load_state_dict(state_dict)
         for group, lt in zip(self.param_groups, lr_tensors):
             if lt is not None:
                 lt.fill_(float(group["lr"]))
                 group["lr"] = lt
-        for group in self.param_groups:
+        for group, old_step in zip(self.param_groups, step_tensors):
             group.pop("_vo_step", None)
             group.pop("_vo_lr", None)
             for p in group["params"]:
                 st = self.state.get(p, {})
                 for k in ("exp_avg", "exp_avg_sq"):
-                    if k in st:  # own copies: torch's load_state_dict keeps the caller's tensors
+                    if k not in st:
+                        continue
+                    keep = moments[p].get(k)
+                    if keep is not None and keep.shape == st[k].shape:
+                        keep.copy_(st[k])
+                        st[k] = keep
+                    else:  # own copies: torch's load_state_dict keeps the caller's tensors
                         st[k] = st[k].to(device=p.device, dtype=torch.float32, copy=True).contiguous()
-            self._group_step(group)
+            t = self._group_step(group)
+            if old_step is not None:
+                old_step.copy_(t)
+                group["_vo_step"] = old_step
+                for p in group["params"]:
+                    if "step" in self.state.get(p, {}):
+                        self.state[p]["step"] = old_step
         self._tables.clear()
 
     def state_dict(self):
