@@ -509,6 +509,43 @@ def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, with_acc, cfg):
     assert rel_l2(out.float().cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("with_acc,scale", [(True, 1.0 / 3), (False, 1.0), (True, 0.3)])
+@pytest.mark.parametrize("T,k,d", [(32768, 11, 5), (20011, 7, 3), (777, 11, 1), (1, 7, 5), (250, 7, 1)])
+def test_pair_c128_frag_bit_identical(T, k, d, with_acc, scale):
+    """vo_resblock_pair_frag (weights in the fragment order of vo_pack_frag128, each load one contiguous
+    KiB) equals vo_resblock_pair on the [K][Co][Ci] packs bit for bit: same kernel, same summation order;
+    out_scale 0.3 takes the epilogue-add path for the MRF accumulator (1 / 0.3 is not a bf16 value)."""
+    from visual_onoma_to_wave_amd import ops
+    C, B = 128, 3
+    g = torch.Generator(device="cuda").manual_seed(T + 10 * k + d)
+    x = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
+    acc = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
+    p1 = ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
+    p2 = ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
+    b1 = torch.randn(C, device="cuda", generator=g) * 0.1
+    b2 = torch.randn(C, device="cuda", generator=g) * 0.1
+    outs = []
+    for frag in (False, True):
+        w1, w2 = (ops.pack_frag128(p1), ops.pack_frag128(p2)) if frag else (p1, p2)
+        o = acc.clone()
+        ops.resblock_pair(x, w1, b1, w2, b2, k, d, 0.1, out=o, out_scale=scale, acc=o if with_acc else None,
+                          frag=frag)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    # and against torch fp32 (the accumulator path with its epilogue add or identity MFMA)
+    import torch.nn.functional as F
+    if T <= 1000:
+        w1f = p1.float().permute(1, 2, 0)  # [K][Co][Ci] -> (Co, Ci, K)
+        w2f = p2.float().permute(1, 2, 0)
+        xf = x.float().transpose(1, 2)
+        t = F.leaky_relu(F.conv1d(F.leaky_relu(xf, 0.1), w1f, b1, padding=d * (k - 1) // 2, dilation=d), 0.1)
+        ref = ((F.conv1d(t, w2f, b2, padding=(k - 1) // 2) + xf) * scale).transpose(1, 2)
+        if with_acc:
+            ref = ref + acc.float()
+        assert rel_l2(outs[1].float().cpu(), ref.cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("cand,rs", [(71, 0), (72, 0), (72, 2)])
 @pytest.mark.parametrize("T,k,d", [(32768, 11, 5), (32768, 7, 3), (777, 11, 1), (1, 7, 5)])
 def test_pair_c128_candidates_vs_shipped(T, k, d, cand, rs):

@@ -4,7 +4,7 @@ Diagnostic library built here (never the product one):
     hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -DVO_PRW_STAMPS \
         visual_onoma_to_wave_amd/csrc/resblock_rw.hip visual_onoma_to_wave_amd/csrc/vo_runtime.cpp \
         -o tools/probes/build/libprw_stamps.so
-    python tools/probes/prw_stamps.py [k d]
+    python tools/probes/prw_stamps.py [k d [variant]]
 
 Prints, for tiles 1-3 of workgroups 0-15 (median over waves and workgroups), shader cycles spent in the
 B0 barrier, each P1 tap, the P1 tail (last row tile's epilogue), the B1 barrier, each P2 tap and the P2
@@ -27,6 +27,7 @@ NSTW, NSTT, NPT = 16, 4, 28
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 11
     d = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    v = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # kernel variant (pair_cfg 100 + v)
     L = ctypes.CDLL(os.path.join(ROOT, "tools/probes/build/libprw_stamps.so"))
     C, B, T = 128, 32, 32768
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -42,11 +43,11 @@ def main():
     buf = (ctypes.c_ulonglong * n)()
     P = ctypes.c_void_p
     fn = L.vo_prw_stamps
-    fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    fn.argtypes = [P, P, P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     fn.restype = ctypes.c_int
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     for _ in range(3):  # warm clocks; keep the last
-        assert fn(ptr(x), ptr(w[0]), ptr(b), ptr(w[1]), ptr(b), ptr(y), ptr(y), B, T, k, d,
+        assert fn(ptr(x), ptr(w[0]), ptr(b), ptr(w[1]), ptr(b), ptr(y), ptr(y), B, T, k, d, v,
                   ctypes.cast(buf, P)) == 0
     st = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(NSTW, 4, NSTT, NPT)
     st = st[:, :, 1:, :]  # tiles 1-3 (tile 0 carries the prologue)
@@ -61,7 +62,7 @@ def main():
     # (P1 tap K-1's interval ends at stamp 2+K = end of P1, including the last row tile's epilogue parts;
     #  the B1 interval is 2+K .. 3+K; P2 tap i is K+4+i .. K+5+i; the last one ends at 2K+4 = end of P2)
     tot = np.median((st[..., 2 * K + 4] - st[..., 0]).ravel())
-    print(f"k={k} d={d}: median tile {tot:.0f} cycles (ideal MFMA {2 * K * 2048})")
+    print(f"k={k} d={d} v={v}: median tile {tot:.0f} cycles (ideal MFMA {2 * K * 2048})")
     for nm, (i0, i1) in zip(names, idx):
         v = (st[..., i1] - st[..., i0]).ravel()
         print(f"  {nm:22s} median {np.median(v):8.0f}  p10 {np.percentile(v, 10):8.0f}  p90 {np.percentile(v, 90):8.0f}")

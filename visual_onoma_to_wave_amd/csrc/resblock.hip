@@ -622,7 +622,7 @@ int vo_pair_rr_try(const void* x, const void* w1, const float* b1, const void* w
                    hipStream_t st, int* handled);  // resblock_rr.hip
 int vo_pair_rw_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                    const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
-                   hipStream_t st, int* handled);  // resblock_rw.hip
+                   hipStream_t st, int* handled, int frag);  // resblock_rw.hip
 int vo_pair_wave_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                      const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
                      hipStream_t st, int* handled);  // resblock5.hip
@@ -650,7 +650,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   const int cfg = vo_tune_get("pair_cfg");
   {  // round 5: C = 128 k = 7 / 11 with wave-owned output planes (resblock_rw.hip); pair_cfg 93 = LDS tiles
     int handled = 0;
-    const int rc = vo_pair_rw_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled);
+    const int rc = vo_pair_rw_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled, 0);
     if (handled) return rc;
   }
   {  // round 4: register-resident frames (resblock_rr.hip) for C = 64 k = 7; pair_cfg 90-99 (A/B)

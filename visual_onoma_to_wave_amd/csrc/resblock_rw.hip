@@ -26,6 +26,7 @@
 // Weights: the ordinary [K][C_out][C_in] bf16 pack (vo_pack_weight); bias fp32.
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "mrf_common.h"
@@ -49,7 +50,7 @@ constexpr size_t RW_LDS = (size_t)4 * (RW_WP + RW_TP) * 32 * sizeof(bf16_t) + 2 
 
 __device__ __forceinline__ int rw_off(int r, int q) { return r * 32 + 8 * (q ^ ((r >> 1) & 3)); }
 
-template <int K, bool ACC, bool ST = false>
+template <int K, int ACC, bool FR = false, bool ST = false>
 __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
   constexpr int C = RW_C, R1 = RW_R1, NJ = R1 / 16;
   constexpr int WP = RW_WP, TP = RW_TP;
@@ -58,7 +59,9 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
   constexpr int SPT = (NWV + K - 3) / (K - 2);  // window slots loaded per P2 tap (taps 0 .. K-3)
   constexpr int RD = 48;                      // MRF-accumulator prefetch distance (steps)
   constexpr int NST = NJ * 4;                 // (row tile, plane) steps per tap
-  constexpr int NB = 10, DB = 8;              // B-fragment ring / prefetch distance in steps
+  constexpr int NB = 10, DB = 8;              // B-fragment ring / prefetch distance (steps); 12 / 14 measured no faster
+  // ACC: 0 = no MRF accumulator; 1 = y = acc_out * out_scale + acc_in (epilogue add); 2 = acc_in / out_scale
+  // enters the accumulators through an identity MFMA (1 / out_scale exact in bf16, e.g. 3)
   static_assert(SPT * (K - 2) >= NWV && SPT <= 4, "window staging");
 
   const int T = a.T, dil = a.dil;
@@ -96,6 +99,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
   // loads through buffer resources: 32-bit lane offsets (a 64-bit address per load kept 2 VGPRs live
   // each and spilled), rows outside an utterance read as 0 (the convs' zero padding) with no clamp
   const int aoff = ((32 * w + 8 * (lr >> 2) + (lr & 3)) * C + 8 * lg) * (int)sizeof(bf16_t);
+  const int afr = w * 8192 + lane * 16;  // FR: [tap][w][s][t][lane][8]
   const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, K * C * C * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, K * C * C * 2, 0x00020000);
   // 2-slot ring: tap u's fragments in slot u % 2; tap u + 1's are requested over the first 16 steps of
@@ -105,8 +109,11 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     const int uu = u % (2 * K);
     const int tap_off = (uu < K ? uu : uu - K) * (C * C * 2);
     const int s = i >> 1, t = i & 1;
+    // FR: fragment-ordered pack (vo_pack_frag128): each piece one contiguous KiB -- the [K][Co][Ci] pack's
+    // pieces touch 16 rows of 64 B each, and their occasional stalls held up whole waves (7 % per tile)
+    const int lo = FR ? afr + i * 1024 : aoff + t * 4 * C * 2 + s * 64;
     A[uu & 1][s][t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(uu < K ? rw1 : rw2,
-                                             aoff + t * 4 * C * 2 + s * 64, tap_off, 0));
+                                             lo, tap_off, 0));
   };
   auto utt = [&](const bf16_t* p, int b) {  // one utterance of a (B, T, C) tensor
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (int64_t)b * T * C), (short)0, T * C * 2, 0x00020000);
@@ -133,6 +140,16 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
 
   f32x4 acc[2][NJ];
   bf16x8 Bq[NB];
+  // identity A fragments (co tile t): lane (m = lr, lg) holds 1 at k = 4t + (m & 3) of its 8 when m / 4 == lg
+  bf16x8 aid[2], ais[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool one = (lr >> 2) == lg && e == 4 * t + (lr & 3);
+      aid[t][e] = (__bf16)(one ? 1.0f : 0.0f);
+      ais[t][e] = (__bf16)(one ? 1.0f / a.out_scale : 0.0f);  // ACC == 2: exact by the launcher's check
+    }
 
   // One conv over the tile: K taps x 4 input planes x 16 row tiles, steps j-major inside a tap.  PH = 0:
   // c1 over the window (row step dil, taps u = k); PH = 1: c2 over T1 (row step 1, taps u = K + k).
@@ -141,7 +158,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
   // the next tap's A fragments (steps 0, 2, .., 14), hook(k, jj) (window staging, residual loads), and
   // in the last tap the epilogue of row tile j in four parts during row tile j + 1's four steps (its
   // accumulators are final after its own four steps).
-  auto conv = [&](auto ph, auto hook, auto post, auto cinit) {
+  auto conv = [&](auto ph, auto hook, auto post, auto cinit, auto extra) {
     constexpr int PH = decltype(ph)::value;
     const bf16_t* src = PH ? t1 : win;
     constexpr int PL = (PH ? TP : WP) * 32;  // plane stride (elements)
@@ -150,8 +167,14 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     // used (hoisted out of the tile loop, 2 x 2K of them were live throughout and spilled)
     int lro = lr, lgo = lg;
     asm volatile("" : "+v"(lro), "+v"(lgo));
+    // step jj of tap k -> (row tile, plane): plane-major (16 row tiles, then the next plane: no two MFMAs
+    // of a row tile back to back -- j-major ran c1's taps 9 % slower, 2,480 vs 2,260 cycles), except in
+    // the last tap, which is j-major so that a row tile's accumulators are final after its four steps
+    // and its epilogue can run under the following row tiles' MFMAs
+    auto rt = [&](int k, int jj) { return k < K - 1 ? jj % NJ : jj / 4; };
+    auto pl = [&](int k, int jj) { return k < K - 1 ? jj / NJ : jj % 4; };
     auto readB = [&](int q) {  // q: step index over the conv (tap q / NST, row tile, plane)
-      const int k = q / NST, j = (q % NST) / 4, s = q % 4;
+      const int k = q / NST, j = rt(k, q % NST), s = pl(k, q % NST);
       // planes 0-1 and 2-3 from two bases: the ds_read offset field holds 16 bits
       const bf16_t* base = src + (s >> 1) * 2 * PL + rw_off(k * step + lro, lgo);
       Bq[q % NB] = *reinterpret_cast<const bf16x8*>(base + (s & 1) * PL + j * 512);
@@ -166,7 +189,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
 #pragma unroll
       for (int jj = 0; jj < NST; ++jj) {
         const int q = k * NST + jj;
-        const int j = jj / 4, s = jj % 4;
+        const int j = rt(k, jj), s = pl(k, jj);
         if (q + DB < K * NST) readB(q + DB);
         if (jj < 16 && jj % 2 == 0) loadA_piece(u + 1, jj / 2);
         hook(k, jj);
@@ -179,6 +202,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
           acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, acc[0][j], 0, 0, 0);
           acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, acc[1][j], 0, 0, 0);
         }
+        extra(k, j, s);
         if (k == K - 1 && j > 0) post(j - 1, s);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -202,12 +226,21 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     const bool interior = t0 - H2 >= 0 && t0 - H2 + R1 <= T;
     const int cofs = 32 * w + 8 * lg;
     const __amdgpu_buffer_rsrc_t rsx = utt(a.x, b);
-    u32x4 xres[NJ];
+    u32x4 xres[NJ], ares[NJ];
+    const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
+    // requested after each tap's A pieces (steps 16, 22, .., 58 of taps K-2 and K-1): vmcnt retires in
+    // issue order, so a residual load issued before an A piece would hold up the MFMAs that wait for it
+    // (spread over the last K-2 taps, a few row tiles each, they measured slower: 2.5 % per tile)
+    constexpr int RPT = 8, NRT = 2, RT0 = K - NRT, RSP = 6;
     auto p1_hook = [&](int k, int jj) {
-      const int g = (k - (K - 2)) * NST + jj;
-      if (g >= 0 && g % 8 == 0) {
-        const int j = g / 8;
-        xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((t0 + 16 * j + lr) * C + cofs) * 2, 0, 0);  // past T: 0
+      if (k < RT0 || jj < 16 || (jj - 16) % RSP != 0) return;  // after the tap's A pieces (steps 0-14)
+      const int i = (jj - 16) / RSP;
+      const int j = (k - RT0) * RPT + i;
+      if (i >= RPT || j >= NJ) return;
+      {
+        const int off = ((t0 + 16 * j + lr) * C + cofs) * 2;  // rows past T: read 0
+        xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+        if constexpr (ACC == 2) ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
       }
     };
     const f32x4* bias1 = reinterpret_cast<const f32x4*>(sbias + cofs);
@@ -225,7 +258,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
         *reinterpret_cast<u32x4*>(t1 + w * TP * 32 + rw_off(r, lg)) = v;
       }
     };
-    conv(std::integral_constant<int, 0>{}, p1_hook, p1_post, p1_cinit);
+    conv(std::integral_constant<int, 0>{}, p1_hook, p1_post, p1_cinit, [&](int, int, int) {});
     stamp(2 + K);
     lds_barrier();  // T1 complete; every wave is past its window reads
     stamp(3 + K);
@@ -235,8 +268,6 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     const int valid = min(BT, T - t0);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
-    u32x4 ares[NJ];
-    const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
     auto p2_hook = [&](int k, int jj) {
       if (jj >= 20 && (jj - 20) % 8 == 0) {
         const int i = (jj - 20) / 8, sl = k * SPT + i;
@@ -246,7 +277,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
         const int i = (jj - 24) / 8, sl = (k - 2) * SPT + i;
         if (i < SPT && k >= 2 && sl < NWV) store_win1(sl);
       }
-      if constexpr (ACC) {  // the MRF accumulator rows, RD steps before each row tile's epilogue
+      if constexpr (ACC == 1) {  // the MRF accumulator rows, RD steps before each row tile's epilogue
         const int g = k * NST + jj, g0 = (K - 1) * NST + 4 - RD;
         if (g >= g0 && g < g0 + NST && (g - g0) % 4 == 0) {
           const int j = (g - g0) / 4;
@@ -256,11 +287,18 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     };
     const f32x4* bias2 = reinterpret_cast<const f32x4*>(sbias + C + cofs);
     const f32x4 b2z0 = bias2[0], b2z1 = bias2[1];
-    auto p2_cinit = [&](int j, int t) {  // b2 + x (the residual) for row tile j, channels of co tile t
-      const uint32_t lo = xres[j][2 * t], hi = xres[j][2 * t + 1];
-      const f32x4 xv = f32x4{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-      return (t ? b2z1 : b2z0) + xv;
+    auto p2_cinit = [&](int, int t) { return t ? b2z1 : b2z0; };
+    // the residual x (and acc_in / out_scale) added by identity MFMAs in c2's first tap: the lane's x
+    // vector of row tile j IS the B fragment of input plane w, and A = I maps its 8 channels onto the
+    // accumulator rows that hold them (exact: products of 1 and bf16, fp32 accumulation)
+    auto p2_extra = [&](int k, int j, int s) {
+      if (k != 0 || s != 0) return;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
+        if constexpr (ACC == 2)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ais[t], __builtin_bit_cast(bf16x8, ares[j]), acc[t][j], 0, 0, 0);
+      }
     };
     const float osc = a.out_scale;
     auto p2_post = [&](int j, int p) {  // part p: channels 2p, 2p + 1 of the lane's 8; part 3 stores
@@ -269,7 +307,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
       for (int u = 0; u < 2; ++u) {
         const int e = 2 * p + u;
         q[u] = acc[e >> 2][j][e & 3] * osc;
-        if constexpr (ACC) {
+        if constexpr (ACC == 1) {
           const uint32_t aw2 = ares[j][p];
           q[u] += __uint_as_float(u ? (aw2 & 0xffff0000u) : (aw2 << 16));
         }
@@ -279,18 +317,18 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{pv[0], pv[1], pv[2], pv[3]}, yrs,
                                                ((16 * j + lr) * C + cofs) * (int)sizeof(bf16_t), 0, 0);
     };
-    conv(std::integral_constant<int, 1>{}, p2_hook, p2_post, p2_cinit);
+    conv(std::integral_constant<int, 1>{}, p2_hook, p2_post, p2_cinit, p2_extra);
     stamp(4 + 2 * K);
     ++st_tile;
   }
 }
 
-template <int K, bool ACC>
+template <int K, int ACC, bool FR>
 static int prw_launch(PrwArgs a, int B, hipStream_t st) {
   constexpr int BT = RW_R1 - 2 * ((K - 1) / 2);
   a.tiles_per_b = (a.T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
-  auto kern = mrf_prw_kernel<K, ACC>;
+  auto kern = mrf_prw_kernel<K, ACC, FR>;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -310,10 +348,10 @@ using namespace vo;
 // (C = 128, K = 7 / 11, (K - 1) * dil <= 64).
 int vo_pair_rw_try(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
                    const void* acc, int B, int T, int C, int K, int dil, float slope, float out_scale, int cfg,
-                   hipStream_t st, int* handled) {
+                   hipStream_t st, int* handled, int frag) {
   *handled = 0;
   if (!(C == 128 && (K == 7 || K == 11) && dil >= 1 && dil * (K - 1) <= 64)) return VO_OK;
-  if (cfg == 93 || cfg == 99) return VO_OK;  // 93: the LDS-tile kernels (A/B)
+  if (!frag && (cfg == 93 || cfg == 99)) return VO_OK;  // 93: the LDS-tile kernels (A/B)
   PrwArgs a;
   a.x = (const bf16_t*)x; a.w1 = (const bf16_t*)w1; a.b1 = b1; a.w2 = (const bf16_t*)w2; a.b2 = b2;
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
@@ -321,15 +359,66 @@ int vo_pair_rw_try(const void* x, const void* w1, const float* b1, const void* w
   a.tiles_per_b = a.ntiles = 0;
   a.stamps = nullptr;
   *handled = 1;
-  if (K == 7) return acc ? prw_launch<7, true>(a, B, st) : prw_launch<7, false>(a, B, st);
-  return acc ? prw_launch<11, true>(a, B, st) : prw_launch<11, false>(a, B, st);
+  // acc_in / out_scale through the identity MFMA when 1 / out_scale is a bf16 value (the MRF's 1/3 -> 3)
+  int accm = 0;
+  if (acc) {
+    const float inv = 1.0f / out_scale;
+    const float invb = __bfloat162float(__float2bfloat16(inv));
+    accm = (invb == inv && std::isfinite(inv) && inv * out_scale == 1.0f) ? 2 : 1;
+  }
+#define VO_PRW_DISPATCH(KK, FF) \
+  return accm == 2 ? prw_launch<KK, 2, FF>(a, B, st) : accm == 1 ? prw_launch<KK, 1, FF>(a, B, st) \
+                                                    : prw_launch<KK, 0, FF>(a, B, st)
+  if (frag) {
+    if (K == 7) VO_PRW_DISPATCH(7, true);
+    VO_PRW_DISPATCH(11, true);
+  }
+  if (K == 7) VO_PRW_DISPATCH(7, false);
+  VO_PRW_DISPATCH(11, false);
+#undef VO_PRW_DISPATCH
+}
+
+// [K][128][128] bf16 conv pack -> the fragment order the C = 128 pair kernel streams:
+// dst[k][w][s][t][lane][e] = src[k][32w + 8(l>>2 & 3) + 4t + (l & 3)][32s + 8(lane >> 4) + e], l = lane & 15
+__global__ void pack_frag128_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int K) {
+  const int v = blockIdx.x * 256 + threadIdx.x;  // one 16-byte vector per thread
+  if (v >= K * 2048) return;
+  const int lane = v & 63, t = (v >> 6) & 1, s = (v >> 7) & 3, w = (v >> 9) & 3, k = v >> 11;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int co = 32 * w + 8 * (lr >> 2) + 4 * t + (lr & 3), ci = 32 * s + 8 * lg;
+  *reinterpret_cast<uint4*>(dst + (int64_t)v * 8) =
+      *reinterpret_cast<const uint4*>(src + ((int64_t)k * 128 + co) * 128 + ci);
+}
+
+extern "C" int vo_pack_frag128(const void* src, void* dst, int K, void* stream) {
+  VO_CHECK_ARG(src && dst && src != dst, "pack_frag128: bad pointers");
+  VO_CHECK_ARG(K >= 1 && K <= 15, "pack_frag128: K=%d", K);
+  hipLaunchKernelGGL(pack_frag128_kernel, dim3((unsigned)((K * 2048 + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const bf16_t*)src, (bf16_t*)dst, K);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_resblock_pair_frag(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                                     void* y, const void* acc, int B, int T, int C, int K, int dil, float slope,
+                                     float out_scale, void* stream) {
+  VO_CHECK_ARG(x && w1 && b1 && w2 && b2 && y, "resblock_pair_frag: null pointer");
+  VO_CHECK_ARG(C == 128 && (K == 7 || K == 11) && dil >= 1 && dil * (K - 1) <= 64,
+               "resblock_pair_frag: C=%d K=%d dil=%d unsupported (C = 128, K = 7 / 11, (K-1)*dil <= 64)", C, K, dil);
+  VO_CHECK_ARG(slope >= 0.f && slope <= 1.f, "resblock_pair_frag: slope %g outside [0, 1]", slope);
+  VO_CHECK_ARG(B > 0 && T > 0, "resblock_pair_frag: empty");
+  VO_CHECK_ARG(y != x, "resblock_pair_frag: y must not alias x (neighbouring tiles re-read x)");
+  VO_CHECK_ARG(acc == nullptr || acc == y || acc != x, "resblock_pair_frag: acc must not alias x");
+  int handled = 0;
+  return vo_pair_rw_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, 0,
+                        reinterpret_cast<hipStream_t>(stream), &handled, 1);
 }
 
 #ifdef VO_PRW_STAMPS
 // Diagnostic entry (tools/probes/prw_stamps.py builds its own library with -DVO_PRW_STAMPS): one stamped
-// launch at the given shape; host_out receives RW_NSTW x 4 waves x RW_NSTT tiles x RW_NPT stamps.
+// launch at the given shape (MRF accumulator on, out_scale 1/3); host_out receives RW_NSTW x 4 waves x
+// RW_NSTT tiles x RW_NPT stamps.  v: 0 = [K][Co][Ci] weights, 4 = fragment-ordered weights.
 extern "C" int vo_prw_stamps(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
-                             const void* acc, int B, int T, int K, int dil, unsigned long long* host_out) {
+                             const void* acc, int B, int T, int K, int dil, int v, unsigned long long* host_out) {
   const size_t n = (size_t)RW_NSTW * 4 * RW_NSTT * RW_NPT;
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, n * 8) != hipSuccess) return -1;
@@ -342,10 +431,14 @@ extern "C" int vo_prw_stamps(const void* x, const void* w1, const float* b1, con
   a.tiles_per_b = (T + BT - 1) / BT;
   a.ntiles = a.tiles_per_b * B;
   const int grid = std::min(256, a.ntiles);
-  if (K == 11)
-    hipLaunchKernelGGL((mrf_prw_kernel<11, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+  if (K == 11 && v == 4)
+    hipLaunchKernelGGL((mrf_prw_kernel<11, 2, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+  else if (K == 11)
+    hipLaunchKernelGGL((mrf_prw_kernel<11, 2, false, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+  else if (v == 4)
+    hipLaunchKernelGGL((mrf_prw_kernel<7, 2, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
   else
-    hipLaunchKernelGGL((mrf_prw_kernel<7, true, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
+    hipLaunchKernelGGL((mrf_prw_kernel<7, 2, false, true>), dim3(grid), dim3(256), RW_LDS, 0, a);
   (void)hipDeviceSynchronize();
   (void)hipMemcpy(host_out, d, n * 8, hipMemcpyDeviceToHost);
   (void)hipFree(d);

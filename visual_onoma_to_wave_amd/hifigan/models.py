@@ -23,6 +23,8 @@ from .._base import HipModule
 LRELU_SLOPE = 0.1
 # K = 3 ResBlocks as one vo_resblock3 launch (VO_RB3=0: three vo_resblock_pair launches, for A/B)
 RB3_ENABLED = os.environ.get("VO_RB3", "1") != "0"
+# C = 128 k = 7 / 11 pairs on fragment-ordered weights (VO_FRAG=0: the [K][Co][Ci] packs, for A/B)
+FRAG_ENABLED = os.environ.get("VO_FRAG", "1") != "0"
 # Conv-path MRF stages (C = 256: two conv launches per ResBlock iteration) run their ResBlock
 # chains on concurrent streams (VO_MRF_STREAMS=0: one after another, for A/B)
 MRF_STREAMS = os.environ.get("VO_MRF_STREAMS", "1") != "0"
@@ -91,7 +93,11 @@ class ResBlock(HipModule):
         self.convs2.apply(init_weights)
 
     def _build(self, device, dtype):
-        return [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
+        packs = [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
+        if self.channels == 128 and self.kernel_size in (7, 11) and dtype == torch.bfloat16 and FRAG_ENABLED:
+            # the stage-1 pair kernel streams its weights in fragment order (vo_pack_frag128)
+            packs = [p + ((ops.pack_frag128(p[0][0]), ops.pack_frag128(p[1][0])),) for p in packs]
+        return packs
 
     def fused(self, x):
         """True when this ResBlock runs as fused pair / block launches (else two convs per pair)."""
@@ -116,13 +122,18 @@ class ResBlock(HipModule):
                                  out_scale=out_scale, acc=accumulate, tag=tag)
         if C in self.fused_pair_channels and x.dtype == self.compute_dtype == torch.bfloat16:
             # narrow stages: one fused launch per (c1, c2) pair, the intermediate stays in LDS
-            for n, (d, ((w1, b1), (w2, b2))) in enumerate(zip(self.dilation, packs)):
+            for n, (d, p) in enumerate(zip(self.dilation, packs)):
+                (w1, b1), (w2, b2) = p[0], p[1]
+                frag = len(p) > 2
+                if frag:
+                    w1, w2 = p[2]
                 last = n == len(self.dilation) - 1
                 cur = ops.resblock_pair(cur, w1, b1, w2, b2, k, d, LRELU_SLOPE, out=out if last else None,
                                         out_scale=out_scale if last else 1.0,
-                                        acc=accumulate if last else None, tag=tag)
+                                        acc=accumulate if last else None, tag=tag, frag=frag)
             return cur
-        for n, (d, ((w1, b1), (w2, b2))) in enumerate(zip(self.dilation, packs)):
+        for n, (d, p) in enumerate(zip(self.dilation, packs)):
+            (w1, b1), (w2, b2) = p[0], p[1]
             t = ops.conv1d(cur, w1, b1, Co=C, K=k, dil=d, pad=get_padding(k, d), pre_act=ops.ACT_LRELU,
                            pre_slope=LRELU_SLOPE, post_act=ops.ACT_LRELU, post_slope=LRELU_SLOPE,
                            compute_dtype=self.compute_dtype, out_dtype=x.dtype, variant=var, tag=tag)

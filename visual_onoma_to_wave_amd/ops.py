@@ -445,8 +445,20 @@ def transpose_bct(x, out_dtype, ldy=None):
 
 # ----------------------------------------------------------------------------- fused ResBlock pair
 
-def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None):
-    """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64, 128}."""
+def pack_frag128(w_packed):
+    """[K][128][128] bf16 conv pack -> the fragment order of the C = 128 pair kernel (vo_pack_frag128)."""
+    _contig(w_packed, "w_packed")
+    if w_packed.dtype != torch.bfloat16 or w_packed.dim() != 3 or tuple(w_packed.shape[1:]) != (128, 128):
+        raise ValueError("pack_frag128: a [K][128][128] bf16 pack")
+    out = torch.empty_like(w_packed)
+    _lib.check(_lib.lib().vo_pack_frag128(_ptr(w_packed), _ptr(out), w_packed.shape[0], _stream(w_packed)),
+               "vo_pack_frag128")
+    return out
+
+
+def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None, frag=False):
+    """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64, 128}.
+    frag: w1 / w2 are pack_frag128 packs (C = 128, K = 7 / 11; vo_resblock_pair_frag)."""
     _contig(x, "x")
     B, T, C = x.shape
     if x.dtype != torch.bfloat16 or w1.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16:
@@ -456,9 +468,10 @@ def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0,
         raise ValueError("resblock_pair: acc must match x")
     timer = profiling.active()
     ev = timer.start() if (tag is not None and timer is not None and timer.watching(tag)) else None
-    _lib.check(_lib.lib().vo_resblock_pair(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(out), _ptr(acc),
-                                           B, T, C, K, dil, float(slope), float(out_scale), _stream(x)),
-               "vo_resblock_pair")
+    fn = _lib.lib().vo_resblock_pair_frag if frag else _lib.lib().vo_resblock_pair
+    _lib.check(fn(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(out), _ptr(acc),
+                  B, T, C, K, dil, float(slope), float(out_scale), _stream(x)),
+               "vo_resblock_pair_frag" if frag else "vo_resblock_pair")
     if ev is not None:
         flops = 2.0 * 2.0 * B * T * C * C * K
         nbytes = 2.0 * x.numel() * 2 + (x.numel() * 2 if acc is not None else 0) + 2 * w1.numel() * 2
