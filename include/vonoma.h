@@ -175,6 +175,14 @@ int vo_attention(const void* qkv, int dtype, const int32_t* lens, int B, int L, 
 int64_t vo_attention_bwd_workspace_size(int B, int L, int H);
 int vo_attention_bwd(const void* qkv, const void* out, const void* dout, int dtype, const int32_t* lens, int B,
                      int L, int H, int dk, float scale, void* dqkv, void* workspace, void* stream);
+/* vo_attention that also writes the row log-sum-exp lse (B, H, L) fp32 (+inf for a row with no key),
+ * and the backward that consumes it (bf16: no pass over the keys to rebuild it; every product formed
+ * transposed so P / dS stay in registers; fp32: as vo_attention_bwd).  Same reference as above. */
+int vo_attention_lse(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
+                     float scale, void* out, float* lse, void* stream);
+int vo_attention_bwd_lse(const void* qkv, const void* out, const void* dout, int dtype, const int32_t* lens, int B,
+                         int L, int H, int dk, float scale, const float* lse, void* dqkv, void* workspace,
+                         void* stream);
 
 /* ------------------------------------------------------------------ length regulator
  * out[b, t, :] = x[b, j, :] for cs[j-1] <= t < cs[j] (cs = inclusive cumsum of

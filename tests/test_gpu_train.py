@@ -218,12 +218,14 @@ def _torch_attention(qkv, lens, n_head):
     return (p @ v).transpose(1, 2).reshape(B, L, D)
 
 
+@pytest.mark.parametrize("with_lse", [False, True])
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("B,L,H,ragged", [(2, 12, 2, True), (4, 512, 2, True), (3, 100, 2, False),
                                           (2, 1, 2, False), (1, 1000, 2, True), (2, 130, 1, True)])
-def test_attention_bwd_vs_torch(B, L, H, ragged, dt, tol):
+def test_attention_bwd_vs_torch(B, L, H, ragged, dt, tol, with_lse):
     """vo_attention_bwd (dQ | dK | dV) vs the fp32 autograd of the reference SDPA, ragged key
-    padding, L not a multiple of the 64-row tiles."""
+    padding, L not a multiple of the 64-row tiles; with_lse: the forward's row log-sum-exp handed to
+    vo_attention_bwd_lse (bf16: the version-2 kernels)."""
     from visual_onoma_to_wave_amd import ops
     gen = torch.Generator().manual_seed(B * L + H)
     D = 128 * H
@@ -234,8 +236,20 @@ def test_attention_bwd_vs_torch(B, L, H, ragged, dt, tol):
     ref_out = _torch_attention(qi, lens, H)
     (ref,) = torch.autograd.grad(ref_out, qi, gout.float())
     qc, lc = qkv.cuda(), lens.cuda()
-    out = ops.attention(qc, lc, H)
-    got = ops.attention_bwd(qc, out, gout.cuda(), lc, H)
+    if with_lse:
+        out, lse = ops.attention(qc, lc, H, with_lse=True)
+        assert torch.equal(out, ops.attention(qc, lc, H))  # the lse output changes nothing else
+        got = ops.attention_bwd(qc, out, gout.cuda(), lc, H, lse=lse)
+        # the row log-sum-exp itself vs the reference softmax's
+        dk = 128
+        qf = qkv.float().reshape(B, L, 3, H, dk)
+        sc = torch.einsum("bqhd,bkhd->bhqk", qf[:, :, 0], qf[:, :, 1]) / dk ** 0.5
+        sc = sc.masked_fill(torch.arange(L)[None, None, None, :] >= lens.long()[:, None, None, None], float("-inf"))
+        ref_lse = torch.logsumexp(sc, dim=-1)
+        assert torch.allclose(lse.cpu(), ref_lse, rtol=1e-4, atol=1e-3 if dt == torch.bfloat16 else 1e-4)
+    else:
+        out = ops.attention(qc, lc, H)
+        got = ops.attention_bwd(qc, out, gout.cuda(), lc, H)
     assert got.dtype == dt and got.shape == qkv.shape
     got = got.float().cpu()
     for part in range(3):  # dQ, dK, dV separately (padded keys: exactly zero)

@@ -124,6 +124,10 @@ _SIGNATURES = {
     "vo_attention_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),
     "vo_attention_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                  c_void_p, c_void_p, c_void_p]),
+    "vo_attention_lse": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                                 c_void_p]),
+    "vo_attention_bwd_lse": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                     c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_length_regulate": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                    c_int, c_void_p, c_void_p, c_void_p]),
     "vo_length_regulate_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,

@@ -81,15 +81,17 @@ def linear(x, weight, bias, relu=False, compute_dtype=torch.bfloat16, out_dtype=
 class AttentionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, lens, n_head):
-        out = ops.attention(qkv.contiguous(), lens, n_head)
-        ctx.save_for_backward(qkv, lens, out)
+        # the row log-sum-exp is kept for the backward (B x H x L fp32): it need not rebuild it
+        out, lse = ops.attention(qkv.contiguous(), lens, n_head, with_lse=True)
+        ctx.save_for_backward(qkv, lens, out, lse)
         ctx.n_head = n_head
         return out
 
     @staticmethod
     def backward(ctx, go):
-        qkv, lens, out = ctx.saved_tensors
-        return ops.attention_bwd(qkv.contiguous(), out, go.to(qkv.dtype).contiguous(), lens, ctx.n_head), None, None
+        qkv, lens, out, lse = ctx.saved_tensors
+        return ops.attention_bwd(qkv.contiguous(), out, go.to(qkv.dtype).contiguous(), lens, ctx.n_head,
+                                 lse=lse), None, None
 
 
 def attention(qkv, lens, n_head):

@@ -21,7 +21,8 @@ constexpr int KT = 64;  // keys per tile
 
 template <typename TC>
 __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ qkv, const int32_t* __restrict__ lens,
-                                                        int L, int H, float scale, TC* __restrict__ out, int xcd) {
+                                                        int L, int H, float scale, TC* __restrict__ out, int xcd,
+                                                        float* __restrict__ lse) {
   constexpr int KP = ATT_DK + 8;  // K tile pitch
   constexpr int VP = KT + 8;      // V^T tile pitch
   constexpr int PP = KT + 8;      // P tile pitch
@@ -159,6 +160,7 @@ __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ q
   for (int r = 0; r < 4; ++r) {
     const int q = q0 + 16 * wave + 4 * g + r;
     if (q >= L) continue;
+    if (lse && lr == 0) lse[(int64_t)bh * L + q] = l_run[r] > 0.f ? m_run[r] + __logf(l_run[r]) : INFINITY;
     const float inv = l_run[r] > 0.f ? 1.0f / l_run[r] : 0.f;
     TC* orow = out + ((int64_t)b * L + q) * D + h * ATT_DK;
 #pragma unroll
@@ -177,7 +179,7 @@ __global__ void __launch_bounds__(256) attention_kernel(const TC* __restrict__ q
 template <int NONE = 0>
 __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restrict__ qkv, const int32_t* __restrict__ lens,
                                                          int L, int H, float scale, bf16_t* __restrict__ out,
-                                                         int xcd) {
+                                                         int xcd, float* __restrict__ lse) {
   constexpr int P = ATT_DK + 16;  // row pitch (elements): 72 dwords = 8 mod 64 banks
   __shared__ __attribute__((aligned(16))) bf16_t kv_lds[2][2][KT * P];  // [buf][K | V][key][dk]
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -318,6 +320,8 @@ __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restric
   }
 
   if (qrow >= L) return;
+  // the row log-sum-exp for the backward (vo_attention_bwd_lse): +inf for a row with no key (P = 0)
+  if (lse && g == 0) lse[(int64_t)bh * L + qrow] = l_run > 0.f ? m_run + __logf(l_run) : INFINITY;
   const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
   bf16_t* orow = out + ((int64_t)b * L + qrow) * D + h * ATT_DK;
 #pragma unroll
@@ -332,8 +336,8 @@ __global__ void __launch_bounds__(256) attention2_kernel(const bf16_t* __restric
 
 using namespace vo;
 
-extern "C" int vo_attention(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
-                            float scale, void* out, void* stream) {
+static int attention_launch(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
+                            float scale, void* out, float* lse, void* stream) {
   VO_CHECK_ARG(qkv && out, "attention: null pointer");
   VO_CHECK_ARG(dk == ATT_DK, "attention: d_k=%d unsupported (128)", dk);
   VO_CHECK_ARG(B > 0 && L > 0 && H > 0, "attention: empty");
@@ -342,16 +346,27 @@ extern "C" int vo_attention(const void* qkv, int dtype, const int32_t* lens, int
   const int xcd = vo_tune_get("att_xcd") != 1;  // att_xcd 1: plain (tile, head) order (A/B)
   if (dtype == VO_BF16 && vo_tune_get("att_cfg") != 1)
     hipLaunchKernelGGL(attention2_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
-                       (bf16_t*)out, xcd);
+                       (bf16_t*)out, xcd, lse);
   else if (dtype == VO_BF16)
     hipLaunchKernelGGL(attention_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, lens, L, H, scale,
-                       (bf16_t*)out, xcd);
+                       (bf16_t*)out, xcd, lse);
   else if (dtype == VO_F32)
     hipLaunchKernelGGL(attention_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, lens, L, H, scale,
-                       (float*)out, xcd);
+                       (float*)out, xcd, lse);
   else {
     vo_set_error("attention: bad dtype");
     return VO_ERR_INVALID;
   }
   VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_attention(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
+                            float scale, void* out, void* stream) {
+  return attention_launch(qkv, dtype, lens, B, L, H, dk, scale, out, nullptr, stream);
+}
+
+extern "C" int vo_attention_lse(const void* qkv, int dtype, const int32_t* lens, int B, int L, int H, int dk,
+                                float scale, void* out, float* lse, void* stream) {
+  VO_CHECK_ARG(lse, "attention_lse: null lse");
+  return attention_launch(qkv, dtype, lens, B, L, H, dk, scale, out, lse, stream);
 }

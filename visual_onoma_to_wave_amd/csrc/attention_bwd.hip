@@ -344,6 +344,297 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const TC* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------- bf16 version 2
+// (round 5) The row log-sum-exp comes from the forward (vo_attention_lse: attention2_kernel writes it),
+// so the dQ kernel has no first pass over the keys; and every product is formed transposed, as in
+// attention2_kernel, so that no P / dS tile goes through LDS and no operand is staged transposed:
+//   dQ kernel (64 queries): S^T = K Q^T, dP^T = V dO^T   (lane: key 16 nt + 4 g + r, query lr)
+//                            dQ^T += K^T dS^T            (A = K^T by ds_read_tr16_b64 of row-major K;
+//                                                          B = dS^T from the lane's own accumulators)
+//   dK/dV kernel (64 keys):  S = Q K^T, dP = dO V^T     (lane: query 16 nt + 4 g + r, key lr)
+//                            dV^T += dO^T P, dK^T += Q^T dS
+// The 32-deep k-steps take the keys (queries) in the order a lane's two accumulator tiles hold them
+// (k index 8 g + j <-> 32 ks + 4 g + j, j < 4; 32 ks + 16 + 4 g + j - 4, j >= 4), and the transposed
+// reads use the same order -- exactly attention2_kernel's O^T += V^T P^T.  K / V (Q / dO) tiles are
+// double-buffered in LDS, the next tile fetched into registers during the current one (one barrier).
+constexpr int AB2_P = AB_DK + 16;  // LDS row pitch (elements): 72 dwords = 8 mod 64 banks
+
+typedef unsigned int ab_u4 __attribute__((ext_vector_type(4)));
+typedef short ab_v4s __attribute__((ext_vector_type(4)));
+typedef short ab_v8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) ab_v4s ab_lds_v4s;
+
+// A fragment of X^T (rows d = 16 dt + lane row, k = the 32 rows 32 ks .. of the row-major LDS tile X, in
+// the accumulator order above)
+__device__ __forceinline__ Frag<bf16_t> ab_tr_frag(const bf16_t* X, int ks, int dt, int g, int tq, int tp) {
+  const bf16_t* vb = X + (32 * ks + 4 * g + tq) * AB2_P + 16 * dt + 4 * tp;
+  const ab_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ab_lds_v4s*)vb);
+  const ab_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ab_lds_v4s*)(vb + 16 * AB2_P));
+  Frag<bf16_t> f;
+  f.v = __builtin_bit_cast(bf16x8, (ab_v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  return f;
+}
+
+// B fragment from two accumulator tiles (k-step ks: tiles 2 ks, 2 ks + 1)
+__device__ __forceinline__ Frag<bf16_t> ab_acc_frag(const f32x4& a, const f32x4& b) {
+  const ab_u4 w = ab_u4{pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3]), pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
+  Frag<bf16_t> f;
+  f.v = __builtin_bit_cast(bf16x8, w);
+  return f;
+}
+
+template <int NONE = 0>
+__global__ void __launch_bounds__(256) attn2_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                           const bf16_t* __restrict__ dout,
+                                                           const int32_t* __restrict__ lens, int L, int H, float scale,
+                                                           const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                           float* __restrict__ dd_ws, int xcd) {
+  constexpr int P = AB2_P, KT = AB_KT;
+  __shared__ __attribute__((aligned(16))) bf16_t kv_lds[2][2][KT * P];  // [buf][K | V][key][dk]
+  const int D = H * AB_DK;
+  const int nq = gridDim.x, wid = blockIdx.x + nq * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nq * gridDim.y) : wid;
+  const int bh = lid / nq;
+  const int b = bh / H, h = bh - b * H;
+  const int q0 = (lid - bh * nq) * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int len = min(lens ? lens[b] : L, L);
+  const int64_t rs = 3 * (int64_t)D;
+  const bf16_t* base = qkv + (int64_t)b * L * rs + h * AB_DK;
+
+  // Q^T / dO^T fragments (B operands): lane (g, lr) holds X[q = q0 + 16 wave + lr][32 ks + 8 g + j]
+  const int qrow = q0 + 16 * wave + lr;
+  const bool qok = qrow < L;
+  Frag<bf16_t> qf[4], df[4];
+  float dpart = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    if (qok) {
+      const int64_t off = ((int64_t)b * L + qrow) * D + h * AB_DK + 32 * ks + 8 * g;
+      qf[ks].load(base + (int64_t)qrow * rs + 32 * ks + 8 * g);
+      df[ks].load(dout + off);
+      float ov[8], dv[8];
+      load8(o + off, ov);
+      load8(dout + off, dv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dpart += ov[e] * dv[e];
+    } else {
+      qf[ks].zero();
+      df[ks].zero();
+    }
+  }
+  dpart += __shfl_xor(dpart, 16, 64);
+  dpart += __shfl_xor(dpart, 32, 64);  // D = rowsum(dO o O) of query lr, in all four lane groups
+  const float ddr = dpart;
+  const float lq = qok ? lse[(int64_t)bh * L + qrow] : INFINITY;
+  if (qok && g == 0) dd_ws[(int64_t)bh * L + qrow] = ddr;
+
+  ab_u4 kreg[4], vreg[4];
+  auto fetch = [&](int key0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int v = tid + 256 * s, kr = v >> 4, c8 = (v & 15) * 8;
+      const int key = min(key0 + kr, L - 1);  // rows past L are masked by len <= L
+      const bf16_t* rp = base + (int64_t)key * rs + c8;
+      kreg[s] = *reinterpret_cast<const ab_u4*>(rp + D);
+      vreg[s] = *reinterpret_cast<const ab_u4*>(rp + 2 * D);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int v = tid + 256 * s, kr = v >> 4, c8 = (v & 15) * 8;
+      *reinterpret_cast<ab_u4*>(&kv_lds[buf][0][kr * P + c8]) = kreg[s];
+      *reinterpret_cast<ab_u4*>(&kv_lds[buf][1][kr * P + c8]) = vreg[s];
+    }
+  };
+
+  f32x4 dq[8];  // dQ^T: lane (g, lr) holds dQ[q = lr][d = 16 dt + 4 g + r]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n_tiles = (len + KT - 1) / KT;
+  if (n_tiles > 0) {
+    fetch(0);
+    stash(0);
+  }
+  __syncthreads();
+  const int tq = lane >> 2 & 3, tp = lane & 3;
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int buf = kt & 1, key0 = kt * KT;
+    if (kt + 1 < n_tiles) fetch(key0 + KT);
+    const bf16_t* K = kv_lds[buf][0];
+    const bf16_t* V = kv_lds[buf][1];
+    f32x4 st[4], dpt[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      st[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dpt[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        Frag<bf16_t> kf, vf;
+        kf.load(K + (16 * nt + lr) * P + 32 * ks + 8 * g);
+        vf.load(V + (16 * nt + lr) * P + 32 * ks + 8 * g);
+        st[nt] = mfma(kf, qf[ks], st[nt]);
+        dpt[nt] = mfma(vf, df[ks], dpt[nt]);
+      }
+    }
+    // dS^T = P^T o (dP^T - D), P^T = exp(S^T * scale - lse): lane's key 16 nt + 4 g + r, query lr
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = key0 + 16 * nt + 4 * g + r < len;
+        const float p = valid ? __expf(st[nt][r] * scale - lq) : 0.f;
+        st[nt][r] = p * (dpt[nt][r] - ddr);
+      }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const Frag<bf16_t> sf = ab_acc_frag(st[2 * ks], st[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(ab_tr_frag(K, ks, dt, g, tq, tp), sf, dq[dt]);
+    }
+    if (kt + 1 < n_tiles) stash(buf ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+  }
+  if (!qok) return;
+  bf16_t* row = dqkv + ((int64_t)b * L + qrow) * rs + h * AB_DK;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+    *reinterpret_cast<uint2*>(row + 16 * dt + 4 * g) =
+        make_uint2(pk_bf16(dq[dt][0] * scale, dq[dt][1] * scale), pk_bf16(dq[dt][2] * scale, dq[dt][3] * scale));
+}
+
+template <int NONE = 0>
+__global__ void __launch_bounds__(256) attn2_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
+                                                             const bf16_t* __restrict__ dout,
+                                                             const int32_t* __restrict__ lens, int L, int H,
+                                                             float scale, const float* __restrict__ lse,
+                                                             const float* __restrict__ dd_ws, bf16_t* __restrict__ dqkv,
+                                                             int xcd) {
+  constexpr int P = AB2_P, QT = 64;
+  __shared__ __attribute__((aligned(16))) bf16_t qd_lds[2][2][QT * P];  // [buf][Q | dO][query][dk]
+  __shared__ float ld_s[2][2][QT];                                      // [buf][lse | D][query]
+  const int D = H * AB_DK;
+  const int nk = gridDim.x, wid = blockIdx.x + nk * blockIdx.y;
+  const int lid = xcd ? xcd_grouped_id(wid, nk * gridDim.y) : wid;
+  const int bh = lid / nk;
+  const int b = bh / H, h = bh - b * H;
+  const int k0 = (lid - bh * nk) * AB_KT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int len = min(lens ? lens[b] : L, L);
+  const int64_t rs = 3 * (int64_t)D;
+  const bf16_t* base = qkv + (int64_t)b * L * rs + h * AB_DK;
+  const bf16_t* dob = dout + (int64_t)b * L * D + h * AB_DK;
+  const int krow = k0 + 16 * wave + lr;
+
+  f32x4 dk[8], dv[8];  // dK^T / dV^T: lane (g, lr) holds [key = lr][d = 16 dt + 4 g + r]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (k0 < len) {  // workgroup-uniform: a tile of padded keys only gets zero gradients
+    Frag<bf16_t> kf[4], vf[4];  // K / V of key krow (B operands): [32 ks + 8 g + j]
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (krow < L) {
+        kf[ks].load(base + (int64_t)krow * rs + D + 32 * ks + 8 * g);
+        vf[ks].load(base + (int64_t)krow * rs + 2 * D + 32 * ks + 8 * g);
+      } else {
+        kf[ks].zero();
+        vf[ks].zero();
+      }
+    }
+    const bool kok = krow < len;
+    ab_u4 qreg[4], dreg[4];
+    float lreg = 0.f, dsreg = 0.f;
+    auto fetch = [&](int qb) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int v = tid + 256 * s, qr = v >> 4, c8 = (v & 15) * 8;
+        const int q = min(qb + qr, L - 1);  // rows past L: P = 0 through lse = +inf below
+        qreg[s] = *reinterpret_cast<const ab_u4*>(base + (int64_t)q * rs + c8);
+        dreg[s] = *reinterpret_cast<const ab_u4*>(dob + (int64_t)q * D + c8);
+      }
+      if (tid < QT) {
+        const int q = qb + tid;
+        lreg = q < L ? lse[(int64_t)bh * L + q] : INFINITY;
+        dsreg = q < L ? dd_ws[(int64_t)bh * L + q] : 0.f;
+      }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int v = tid + 256 * s, qr = v >> 4, c8 = (v & 15) * 8;
+        *reinterpret_cast<ab_u4*>(&qd_lds[buf][0][qr * P + c8]) = qreg[s];
+        *reinterpret_cast<ab_u4*>(&qd_lds[buf][1][qr * P + c8]) = dreg[s];
+      }
+      if (tid < QT) {
+        ld_s[buf][0][tid] = lreg;
+        ld_s[buf][1][tid] = dsreg;
+      }
+    };
+    const int n_qt = (L + QT - 1) / QT;
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    const int tq = lane >> 2 & 3, tp = lane & 3;
+    for (int qt = 0; qt < n_qt; ++qt) {
+      const int buf = qt & 1;
+      if (qt + 1 < n_qt) fetch((qt + 1) * QT);
+      const bf16_t* Q = qd_lds[buf][0];
+      const bf16_t* dO = qd_lds[buf][1];
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          Frag<bf16_t> qf, df;
+          qf.load(Q + (16 * nt + lr) * P + 32 * ks + 8 * g);
+          df.load(dO + (16 * nt + lr) * P + 32 * ks + 8 * g);
+          sc[nt] = mfma(qf, kf[ks], sc[nt]);
+          dp[nt] = mfma(df, vf[ks], dp[nt]);
+        }
+      }
+      // P = exp(S * scale - lse[q]), dS = P o (dP - D[q]): lane's query 16 nt + 4 g + r, key lr
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = 16 * nt + 4 * g + r;
+          const float p = kok ? __expf(sc[nt][r] * scale - ld_s[buf][0][qq]) : 0.f;
+          sc[nt][r] = p;
+          dp[nt][r] = p * (dp[nt][r] - ld_s[buf][1][qq]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const Frag<bf16_t> pf = ab_acc_frag(sc[2 * ks], sc[2 * ks + 1]);
+        const Frag<bf16_t> sf = ab_acc_frag(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          dv[dt] = mfma(ab_tr_frag(dO, ks, dt, g, tq, tp), pf, dv[dt]);
+          dk[dt] = mfma(ab_tr_frag(Q, ks, dt, g, tq, tp), sf, dk[dt]);
+        }
+      }
+      if (qt + 1 < n_qt) stash(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  if (krow >= L) return;
+  bf16_t* row = dqkv + ((int64_t)b * L + krow) * rs + h * AB_DK;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    *reinterpret_cast<uint2*>(row + D + 16 * dt + 4 * g) =
+        make_uint2(pk_bf16(dk[dt][0] * scale, dk[dt][1] * scale), pk_bf16(dk[dt][2] * scale, dk[dt][3] * scale));
+    *reinterpret_cast<uint2*>(row + 2 * D + 16 * dt + 4 * g) =
+        make_uint2(pk_bf16(dv[dt][0], dv[dt][1]), pk_bf16(dv[dt][2], dv[dt][3]));
+  }
+}
+
 }  // namespace vo
 
 using namespace vo;
@@ -377,5 +668,27 @@ extern "C" int vo_attention_bwd(const void* qkv, const void* out, const void* do
     vo_set_error("attention_bwd: bad dtype");
     return VO_ERR_INVALID;
   }
+  VO_RETURN_LAUNCH();
+}
+
+// Backward with the forward's row log-sum-exp (vo_attention_lse): bf16 -> the version-2 kernels (no key
+// pass to rebuild it); fp32 -> the version-1 kernels (which rebuild it; lse unused).  workspace:
+// vo_attention_bwd_workspace_size(B, L, H) bytes.
+extern "C" int vo_attention_bwd_lse(const void* qkv, const void* out, const void* dout, int dtype, const int32_t* lens,
+                                    int B, int L, int H, int dk, float scale, const float* lse, void* dqkv,
+                                    void* workspace, void* stream) {
+  VO_CHECK_ARG(qkv && out && dout && dqkv && workspace && lse, "attention_bwd_lse: null pointer");
+  VO_CHECK_ARG(dk == AB_DK, "attention_bwd_lse: d_k=%d unsupported (128)", dk);
+  VO_CHECK_ARG(B > 0 && L > 0 && H > 0, "attention_bwd_lse: empty");
+  if (dtype != VO_BF16 || vo_tune_get("att_cfg") == 1)  // att_cfg 1: the version-1 kernels (A/B)
+    return vo_attention_bwd(qkv, out, dout, dtype, lens, B, L, H, dk, scale, dqkv, workspace, stream);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* dd = (float*)workspace;
+  dim3 grid((unsigned)((L + 63) / 64), (unsigned)(B * H));
+  const int xcd = vo_tune_get("att_xcd") != 1;
+  hipLaunchKernelGGL(attn2_bwd_dq_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)out,
+                     (const bf16_t*)dout, lens, L, H, scale, lse, (bf16_t*)dqkv, dd, xcd);
+  hipLaunchKernelGGL(attn2_bwd_dkdv_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lens,
+                     L, H, scale, lse, (const float*)dd, (bf16_t*)dqkv, xcd);
   VO_RETURN_LAUNCH();
 }

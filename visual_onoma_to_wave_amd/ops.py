@@ -226,22 +226,29 @@ def layernorm_bwd(x, gy, gamma, res=None, lens=None, eps=1e-5):
 
 # ----------------------------------------------------------------------------- attention
 
-def attention(qkv, lens, n_head, out=None):
-    """qkv (B, L, 3D) -> (B, L, D); keys t >= lens[b] masked."""
+def attention(qkv, lens, n_head, out=None, with_lse=False):
+    """qkv (B, L, 3D) -> (B, L, D); keys t >= lens[b] masked.  with_lse: also the row log-sum-exp
+    (B, H, L) fp32 that attention_bwd(..., lse=) consumes (vo_attention_lse)."""
     _contig(qkv, "qkv")
     B, L, D3 = qkv.shape
     D = D3 // 3
     dk = D // n_head
     out = out if out is not None else torch.empty((B, L, D), dtype=qkv.dtype, device=qkv.device)
     scale = 1.0 / float(dk) ** 0.5
+    if with_lse:
+        lse = torch.empty((B, n_head, L), dtype=torch.float32, device=qkv.device)
+        _lib.check(_lib.lib().vo_attention_lse(_ptr(qkv), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
+                                               scale, _ptr(out), _ptr(lse), _stream(qkv)), "vo_attention_lse")
+        return out, lse
     _lib.check(_lib.lib().vo_attention(_ptr(qkv), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
                                        scale, _ptr(out), _stream(qkv)), "vo_attention")
     return out
 
 
-def attention_bwd(qkv, out, dout, lens, n_head):
+def attention_bwd(qkv, out, dout, lens, n_head, lse=None):
     """Backward of ``attention``: dqkv (B, L, 3D) in qkv's dtype from the forward output and its
-    gradient (flash-style recomputation, vo_attention_bwd)."""
+    gradient (flash-style recomputation, vo_attention_bwd); with the forward's row log-sum-exp (lse,
+    attention(..., with_lse=True)) the bf16 path skips rebuilding it (vo_attention_bwd_lse)."""
     for t, n in ((qkv, "qkv"), (out, "out"), (dout, "dout")):
         _contig(t, n)
     B, L, D3 = qkv.shape
@@ -255,6 +262,13 @@ def attention_bwd(qkv, out, dout, lens, n_head):
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(int(L_.vo_attention_bwd_workspace_size(B, L, n_head)) // 4, dtype=torch.float32,
                      device=qkv.device)
+    if lse is not None:
+        if lse.shape != (B, n_head, L) or lse.dtype != torch.float32 or not lse.is_contiguous():
+            raise ValueError("attention_bwd: lse must be the forward's (B, H, L) fp32 row log-sum-exp")
+        _lib.check(L_.vo_attention_bwd_lse(_ptr(qkv), _ptr(out), _ptr(dout), vo_dtype(qkv), _ptr(lens), B, L, n_head,
+                                           dk, 1.0 / float(dk) ** 0.5, _ptr(lse), _ptr(dqkv), _ptr(ws),
+                                           _stream(qkv)), "vo_attention_bwd_lse")
+        return dqkv
     _lib.check(L_.vo_attention_bwd(_ptr(qkv), _ptr(out), _ptr(dout), vo_dtype(qkv), _ptr(lens), B, L, n_head, dk,
                                    1.0 / float(dk) ** 0.5, _ptr(dqkv), _ptr(ws), _stream(qkv)),
                "vo_attention_bwd")
