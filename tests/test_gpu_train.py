@@ -98,6 +98,45 @@ def test_training_reduces_loss(device):
     assert float(losses[0]) < 0.8 * first
 
 
+def test_step_batched_packs_bit_identical(device):
+    """autograd's step-batched weight packs (every conv's forward and input-gradient layouts of a step in
+    one vo_pack_batch call per dtype, the fused q/k/v weights written by three jobs) against per-call
+    packs (VO_C4_PREPACK=0 behaviour): four mixed-precision training steps with the optimizer moving the
+    weights, losses and every parameter bit for bit; at most two pack calls (fp32 encoder, bf16
+    decoder) per step."""
+    from visual_onoma_to_wave_amd import autograd as AG
+    from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
+    from visual_onoma_to_wave_amd.train import train_step
+    pc, mc, tc = configs()
+    tc = dict(tc)
+    tc["optimizer"] = dict(tc["optimizer"], warm_up_step=10, init_lr=1e-3)
+    batch = _batch(golden("vtts_tf"), device)
+    runs = []
+    saved = AG.PREPACK
+    try:
+        for prepack in (False, True):
+            AG.PREPACK = prepack
+            AG.reset_packs()
+            m = vTTS(pc, mc, tc)
+            load_into(m, vtts_arrays())
+            m = m.to(device).train().set_precision("mixed")
+            _no_dropout(m)
+            opt = ScheduledOptim(m, tc, mc, 0)
+            losses = []
+            for i in range(4):
+                b0 = AG.STATS["batches"]
+                losses.append([float(x) for x in train_step(m, opt, FastSpeech2Loss(), batch)])
+                if prepack and i > 0:
+                    assert AG.STATS["batches"] - b0 <= 2
+            runs.append((losses, [p.detach().clone() for p in m.parameters()]))
+    finally:
+        AG.PREPACK = saved
+        AG.reset_packs()
+    (l0, p0), (l1, p1) = runs
+    assert l0 == l1
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
 def test_graphed_train_step_matches_eager(device):
     """train.GraphedTrainStep (HIP-graph replay with the capturable Adam and a device-tensor
     learning rate, replays launched back to back with no host wait) against the same number of

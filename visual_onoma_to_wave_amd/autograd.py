@@ -18,10 +18,125 @@ The forward of every op is the same HIP kernel the inference path runs.  Backwar
 All functions take and return channels-last (B, T, C) activations.
 """
 
+import os
+import weakref
+
 import torch
 import torch.nn.functional as F
 
 from . import ops
+
+# ---------------------------------------------------------------------------- step-batched weight packs
+# Every conv of the training forward packs its weight ([K][Co][Ci], compute dtype) and its backward the
+# taps-reversed input-gradient layout ([K][Ci][Co]); packed one launch per layer and layout that was
+# ~100 launches of 4-7 us per C4 step.  Instead each (weights, compute dtype) the step uses keeps
+# persistent pack buffers here, and the first look-up at new parameter versions (after an optimizer
+# step, or in each HIP-graph replay) re-packs EVERY stale layout of the store in one vo_pack_batch call
+# per dtype (its job table: 32 packs per launch).  The fused q/k/v projection's weights are written by
+# three jobs into one [768][256] buffer (no torch.cat per step).  VO_C4_PREPACK=0: per-call packs (A/B).
+PREPACK = os.environ.get("VO_C4_PREPACK", "1") != "0"
+STATS = {"batches": 0, "packs": 0}
+
+
+class _PackEntry:
+    __slots__ = ("refs", "cdt", "Co", "Ci", "K", "buf", "ver", "need_dgrad")
+
+    def __init__(self, params, cdt):
+        self.refs, self.cdt = tuple(weakref.ref(p) for p in params), cdt  # the store keeps no model alive
+        self.Co = sum(p.shape[0] for p in params)
+        self.Ci = params[0].shape[1]
+        self.K = params[0].shape[2] if params[0].dim() == 3 else 1
+        self.buf, self.ver, self.need_dgrad = {}, {}, False
+
+    @property
+    def params(self):
+        return tuple(r() for r in self.refs)
+
+    def alive(self):
+        return all(r() is not None for r in self.refs)
+
+    def version(self):
+        return tuple(p._version for p in self.params)
+
+    def jobs(self, kind):
+        """vo_pack_batch jobs (src, dst, fields, offset) writing this layout from every source."""
+        K, Ci, Co = self.K, self.Ci, self.Co
+        dst = self.buf[kind]
+        out, row0 = [], 0
+        for p in self.params:
+            co = p.shape[0]
+            src = p.detach()
+            if kind == "fwd":  # dst[k][r0 + co][ci] = src[co][ci][k]
+                f = dict(mode=ops.PJ_GATHER, swap=0, T=K, rows=co, width=Ci, dst_rows=Co, ld=Ci, rpg=co, cpg=0,
+                         cig=Ci, K=K, tap0=0, tstep=1, src_rows=co)
+                out.append((src, dst, f, row0 * Ci))
+            else:  # dgrad: dst[K-1-k][ci][r0 + co] = src[co][ci][k]
+                f = dict(mode=ops.PJ_GATHER, swap=1, T=K, rows=Ci, width=co, dst_rows=Ci, ld=Co, rpg=Ci, cpg=0,
+                         cig=Ci, K=K, tap0=K - 1, tstep=-1, src_rows=co)
+                out.append((src, dst, f, row0))
+            row0 += co
+        return out
+
+
+_STORES = ({}, {})  # [capturing]: packs made inside a graph capture live in the graph's own store
+
+
+def _store():
+    return _STORES[1 if torch.cuda.is_current_stream_capturing() else 0]
+
+
+def reset_packs():
+    """Forget every step-batched pack: before and after a graph capture (the capture re-packs inside the
+    graph, so every replay packs the weights it is about to read), and after each replay (replays move the
+    parameters without bumping their version counters: an eager step afterwards must re-pack)."""
+    for st in _STORES:
+        st.clear()
+
+
+def _packed_weight(params, cdt, kind):
+    """The ``kind`` ("fwd" | "dgrad") layout of the conv whose weight is ``params`` concatenated along
+    C_out (fp32 (Co_i, Ci, K) or (Co_i, Ci) parameters), packed for compute dtype ``cdt``."""
+    store = _store()
+    key = (tuple(id(p) for p in params), cdt)
+    e = store.get(key)
+    if e is None or any(a is not b for a, b in zip(e.params, params)):  # new, or ids of dead parameters reused
+        e = store[key] = _PackEntry(params, cdt)
+    if kind == "dgrad":
+        e.need_dgrad = True
+    if e.ver.get(kind) != e.version():
+        _refresh(store)
+    return e.buf[kind]
+
+
+def _refresh(store):
+    """Re-pack every stale layout of the store: one vo_pack_batch call per dtype."""
+    per_dtype = {}
+    for k in [k for k, e in store.items() if not e.alive()]:
+        del store[k]
+    for e in store.values():
+        ver = e.version()
+        for kind in ("fwd", "dgrad") if e.need_dgrad else ("fwd",):
+            if e.ver.get(kind) == ver:
+                continue
+            if kind not in e.buf:
+                dev = e.params[0].device
+                shape = (e.K, e.Co, e.Ci) if kind == "fwd" else (e.K, e.Ci, e.Co)
+                e.buf[kind] = torch.empty(shape, dtype=e.cdt, device=dev)
+            per_dtype.setdefault(e.cdt, []).extend(e.jobs(kind))
+            e.ver[kind] = ver
+            STATS["packs"] += 1
+    for cdt, jobs in per_dtype.items():
+        ops.pack_batch(jobs, cdt)
+        STATS["batches"] += 1
+
+
+def _params_of(w):
+    """The fp32 parameter(s) behind a conv weight argument (a Linear's weight[:, :, None] view -> the
+    Linear's weight), or None when it is not a plain contiguous fp32 tensor."""
+    base = w._base if (w._base is not None and w.dim() == 3 and w.shape[2] == 1) else w
+    if base.dtype != torch.float32 or not base.is_contiguous() or base.shape[0] != w.shape[0]:
+        return None
+    return (base,)
 
 
 class Conv1dFn(torch.autograd.Function):
@@ -30,7 +145,8 @@ class Conv1dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, K, dil, pad, relu, compute_dtype, out_dtype):
         Co = w.shape[0]
-        wp = ops.pack_conv_weight(w, compute_dtype)
+        src = _params_of(w) if PREPACK else None
+        wp = _packed_weight(src, compute_dtype, "fwd") if src else ops.pack_conv_weight(w, compute_dtype)
         y = ops.conv1d(x.contiguous(), wp, b.detach().float().contiguous() if b is not None else None, Co=Co,
                        K=K, dil=dil, pad=pad, post_act=ops.ACT_RELU if relu else ops.ACT_NONE,
                        out_dtype=out_dtype, compute_dtype=compute_dtype)
@@ -48,7 +164,8 @@ class Conv1dFn(torch.autograd.Function):
         gx = gw = gb = None
         want_b = has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[0]:
-            wd = ops.pack_dgrad_weight(w, cdt)
+            src = _params_of(w) if PREPACK else None
+            wd = _packed_weight(src, cdt, "dgrad") if src else ops.pack_dgrad_weight(w, cdt)
             gx = ops.conv1d(gz.to(cdt) if gz.dtype != cdt else gz, wd, None, Co=w.shape[1], K=K, dil=dil,
                             pad=(K - 1) * dil - pad, T_out=x.shape[1], out_dtype=x.dtype, compute_dtype=cdt)
         if ctx.needs_input_grad[1]:
@@ -76,6 +193,49 @@ def conv1d(x, w, b, K=1, dil=1, pad=0, relu=False, compute_dtype=torch.bfloat16,
 
 def linear(x, weight, bias, relu=False, compute_dtype=torch.bfloat16, out_dtype=None):
     return conv1d(x, weight[:, :, None], bias, 1, 1, 0, relu, compute_dtype, out_dtype)
+
+
+class QKVLinearFn(torch.autograd.Function):
+    """The fused q / k / v projection (SubLayers.py:39-41 as one GEMM): x (B, L, D) -> (B, L, 3D) with
+    the three Linears' weights packed side by side by the step's pack batch (no per-step torch.cat of
+    the weights); the backward splits dW and db back onto the three Linears."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, compute_dtype):
+        params = (wq, wk, wv)
+        wp = _packed_weight(params, compute_dtype, "fwd")
+        b = torch.cat([bq.detach(), bk.detach(), bv.detach()]).float()
+        y = ops.conv1d(x.contiguous(), wp, b, Co=wp.shape[1], K=1, compute_dtype=compute_dtype,
+                       out_dtype=x.dtype)
+        ctx.save_for_backward(x, wq, wk, wv)
+        ctx.cdt = compute_dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wq, wk, wv = ctx.saved_tensors
+        cdt = ctx.cdt
+        gz = gy.contiguous()
+        gz = gz.to(cdt) if gz.dtype != cdt else gz
+        gx = None
+        if ctx.needs_input_grad[0]:
+            wd = _packed_weight((wq, wk, wv), cdt, "dgrad")
+            gx = ops.conv1d(gz, wd, None, Co=wq.shape[1], K=1, T_out=x.shape[1], out_dtype=x.dtype,
+                            compute_dtype=cdt)
+        fuse_b = gy.dtype == cdt  # bias = column sums of the same dY (no cast), as Conv1dFn
+        r = ops.conv1d_wgrad(gz, x.to(cdt).contiguous(), 1, with_bias=fuse_b)
+        gw, gb = r if fuse_b else (r, ops.colsum(gy.contiguous()))
+        gw = gw.to(wq.dtype).reshape(gw.shape[0], gw.shape[1])
+        n = wq.shape[0]
+        return (gx, gw[:n], gw[n:2 * n], gw[2 * n:], gb[:n], gb[n:2 * n], gb[2 * n:], None)
+
+
+def qkv_linear(x, wq, wk, wv, bq, bk, bv, compute_dtype):
+    if not PREPACK:
+        w = torch.cat([wq, wk, wv], 0)
+        b = torch.cat([bq, bk, bv], 0)
+        return linear(x, w, b, compute_dtype=compute_dtype)
+    return QKVLinearFn.apply(x, wq, wk, wv, bq, bk, bv, compute_dtype)
 
 
 class AttentionFn(torch.autograd.Function):

@@ -725,20 +725,27 @@ _PJ_FIELDS = ("mode", "swap", "T", "rows", "width", "dst_rows", "ld", "rpg", "cp
 
 def pack_batch(jobs, dtype):
     """Many weight packs in one launch (vo_pack_batch; layouts in include/vonoma.h): jobs is a list of
-    (src fp32 contiguous, dst contiguous tensor of ``dtype``, {field: int}).  Entries of dst a job
-    does not name are left as they are."""
+    (src fp32 contiguous, dst contiguous tensor of ``dtype``, {field: int}[, element offset of the job's
+    block in dst]).  Entries of dst a job does not name are left as they are."""
     if not jobs:
         return
     arr = (_lib.PackJob * len(jobs))()
-    for e, (src, dst, f) in zip(arr, jobs):
+    for e, job in zip(arr, jobs):
+        src, dst, f = job[:3]
+        off = job[3] if len(job) > 3 else None  # element offset of the job's (0, 0) in dst (a block of it)
         _contig(src, "src")
         _contig(dst, "dst")
         if src.dtype != torch.float32 or dst.dtype != dtype:
             raise ValueError("pack_batch: src must be fp32 and dst the batch dtype")
         rows_total = f["T"] * f["dst_rows"] * f["ld"]
-        if dst.numel() != rows_total:
+        if off is None and dst.numel() != rows_total:
             raise ValueError(f"pack_batch: dst has {dst.numel()} elements, the job's layout {rows_total}")
-        e.src, e.dst = src.data_ptr(), dst.data_ptr()
+        if off is not None:  # the last element the job writes must lie in dst
+            last = (off + (f["T"] - 1) * f["dst_rows"] * f["ld"] + (f["rows"] - 1) * f["ld"] +
+                    ((f["rows"] - 1) // f["rpg"]) * f["cpg"] + f["width"])
+            if off < 0 or last > dst.numel():
+                raise ValueError(f"pack_batch: a block at {off} of {dst.numel()} elements ends at {last}")
+        e.src, e.dst = src.data_ptr(), dst.data_ptr() + (off or 0) * dst.element_size()
         for k in _PJ_FIELDS:
             setattr(e, k, int(f[k]))
     _lib.check(_lib.lib().vo_pack_batch(len(jobs), ctypes.cast(arr, ctypes.c_void_p), vo_dtype(dtype),

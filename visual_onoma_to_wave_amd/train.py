@@ -36,6 +36,7 @@ import torch
 import torch.distributed as dist
 
 from . import _base
+from . import autograd as AG
 
 
 def packet_capture_disabled():
@@ -352,8 +353,10 @@ class GraphedTrainStep:
                 self._body(self.static)
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
+        AG.reset_packs()  # the capture packs the weights inside the graph (autograd's step-batched packs)
         with _capture_ctx([self.bucketer]), torch.cuda.graph(self.graph):
             self.out = self._body(self.static)
+        AG.reset_packs()
         snap.restore()  # the warm-up updates are undone: the first replay is the first update
         self.opt.current_step = step0
         _base.invalidate_packs(self.model)
@@ -369,6 +372,7 @@ class GraphedTrainStep:
         self.opt._update_learning_rate()
         self.graph.replay()
         _base.invalidate_packs(self.model)  # replays move the parameters without bumping their versions
+        AG.reset_packs()
         return self.out
 
 

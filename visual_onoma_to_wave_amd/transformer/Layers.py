@@ -37,9 +37,8 @@ class FFTBlock(HipModule):
     def train_run(self, x, lens):
         """Training forward (autograd; dropout active), scripts/transformer/Layers.py:21-30."""
         mha, ffn, cd = self.slf_attn, self.pos_ffn, self.compute_dtype
-        wqkv = torch.cat([mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight], 0)
-        bqkv = torch.cat([mha.w_qs.bias, mha.w_ks.bias, mha.w_vs.bias], 0)
-        qkv = AG.linear(x, wqkv, bqkv, compute_dtype=cd)
+        qkv = AG.qkv_linear(x, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
+                            mha.w_vs.bias, cd)
         att = AG.attention(qkv, lens, mha.n_head)
         y = F.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p, True)
         x1 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
