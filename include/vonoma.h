@@ -281,16 +281,16 @@ int vo_conv_post(const void* x, int x_dtype, const float* w, float bias, int B, 
 int vo_resblock_pair(const void* x, const void* w1, const float* b1, const void* w2,
                      const float* b2, void* y, const void* acc, int B, int T, int C, int K,
                      int dil, float slope, float out_scale, void* stream);
-/* vo_resblock_pair for C = 128, K = 7 / 11 with w1 / w2 in the fragment order that the stage-1 kernel
- * streams into registers (vo_pack_frag128 of the [K][128][128] pack): every weight load is one
- * contiguous KiB.  Results equal vo_resblock_pair's on the same weights bit for bit.  Same reference
- * (scripts/hifigan/models.py:96-103, 155-160). */
+/* vo_resblock_pair for C = 64 / 128, K = 7 / 11 with w1 / w2 in the fragment order that the pair
+ * kernel streams into registers (vo_pack_frag of the [K][C][C] pack): every weight load is one
+ * contiguous KiB.  C = 128: results equal vo_resblock_pair's on the same weights bit for bit.  Same
+ * reference (scripts/hifigan/models.py:96-103, 155-160). */
 int vo_resblock_pair_frag(const void* x, const void* w1, const float* b1, const void* w2,
                           const float* b2, void* y, const void* acc, int B, int T, int C, int K,
                           int dil, float slope, float out_scale, void* stream);
-/* [K][128][128] bf16 (vo_pack_weight VO_PACK_CONV) -> [K][4][4][2][64][8] fragment order:
- * dst[k][w][s][t][l][e] = src[k][32w + 8((l & 15) >> 2) + 4t + (l & 3)][32s + 8(l >> 4) + e]. */
-int vo_pack_frag128(const void* src, void* dst, int K, void* stream);
+/* [K][C][C] bf16 (vo_pack_weight VO_PACK_CONV), C = 64 / 128 -> [K][C/32][C/32][2][64][8] fragment order:
+ * dst[k][p][s][t][l][e] = src[k][32p + 8((l & 15) >> 2) + 4t + (l & 3)][32s + 8(l >> 4) + e]. */
+int vo_pack_frag(const void* src, void* dst, int C, int K, void* stream);
 
 /* Fused ResBlock1 with K = 3 (bf16, channels-last (B, T, C), C = 32 / 64 / 128): all three
  * (c1_dil[s], c2) iterations in one launch,

@@ -459,9 +459,10 @@ def test_fused_resblock3_vs_torch_fp32(C, T, with_acc, cfg):
     assert rel_l2(out.float().cpu(), chain.float().cpu()) < 3e-3
 
 
-# cfg 0: the shipped dispatch (register-resident frames for C = 64 k = 7); 93: the LDS-tile kernels;
+# cfg 0: the shipped dispatch (wave-owned planes for C = 64 / 128 k = 7 / 11); 93: the LDS-tile kernels;
+# 111: the round-4 C = 64 dispatch (register-resident frames for k = 7);
 # VO_PARITY_PAIR_CFGS=94,95 adds A/B candidates of the ablation build
-_PAIR_CFGS = [0, 93] + [int(c) for c in os.environ.get("VO_PARITY_PAIR_CFGS", "").split(",") if c]
+_PAIR_CFGS = [0, 93, 111] + [int(c) for c in os.environ.get("VO_PARITY_PAIR_CFGS", "").split(",") if c]
 
 
 @pytest.mark.parametrize("cfg", _PAIR_CFGS)
@@ -471,6 +472,8 @@ _PAIR_CFGS = [0, 93] + [int(c) for c in os.environ.get("VO_PARITY_PAIR_CFGS", ""
                                      # several tiles per persistent workgroup (pipelined window/weights)
                                      (32, 131072, 11, 5), (32, 65536, 3, 1), (64, 65536, 7, 3),
                                      (64, 65536, 3, 1), (64, 40000, 11, 5),
+                                     # C = 64 k = 7 / 11 plane kernel: one tile (502 / 506 valid rows), +1, two
+                                     (64, 503, 11, 5), (64, 13, 7, 1), (64, 1013, 7, 5), (64, 506, 7, 3),
                                      (128, 300, 3, 1), (128, 20000, 3, 5),
                                      # C = 128 k = 7 / 11: T = 1, one tile, tile edges (246 / 250 valid
                                      # rows), utterances crossing inside a workgroup's run, every dilation
@@ -511,12 +514,14 @@ def test_fused_resblock_pair_vs_torch_fp32(C, T, k, d, with_acc, cfg):
 
 @pytest.mark.parametrize("with_acc,scale", [(True, 1.0 / 3), (False, 1.0), (True, 0.3)])
 @pytest.mark.parametrize("T,k,d", [(32768, 11, 5), (20011, 7, 3), (777, 11, 1), (1, 7, 5), (250, 7, 1)])
-def test_pair_c128_frag_bit_identical(T, k, d, with_acc, scale):
-    """vo_resblock_pair_frag (weights in the fragment order of vo_pack_frag128, each load one contiguous
-    KiB) equals vo_resblock_pair on the [K][Co][Ci] packs bit for bit: same kernel, same summation order;
-    out_scale 0.3 takes the epilogue-add path for the MRF accumulator (1 / 0.3 is not a bf16 value)."""
+@pytest.mark.parametrize("C", [128, 64])
+def test_pair_plane_frag_bit_identical(C, T, k, d, with_acc, scale):
+    """vo_resblock_pair_frag (weights in the fragment order of vo_pack_frag, each load one contiguous
+    KiB) equals the plane kernel on the [K][Co][Ci] packs bit for bit (vo_resblock_pair): same kernel,
+    same summation order; out_scale 0.3 takes the epilogue-add path for the MRF accumulator (1 / 0.3 is
+    not a bf16 value)."""
     from visual_onoma_to_wave_amd import ops
-    C, B = 128, 3
+    B = 3
     g = torch.Generator(device="cuda").manual_seed(T + 10 * k + d)
     x = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
     acc = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
@@ -526,7 +531,7 @@ def test_pair_c128_frag_bit_identical(T, k, d, with_acc, scale):
     b2 = torch.randn(C, device="cuda", generator=g) * 0.1
     outs = []
     for frag in (False, True):
-        w1, w2 = (ops.pack_frag128(p1), ops.pack_frag128(p2)) if frag else (p1, p2)
+        w1, w2 = (ops.pack_frag(p1), ops.pack_frag(p2)) if frag else (p1, p2)
         o = acc.clone()
         ops.resblock_pair(x, w1, b1, w2, b2, k, d, 0.1, out=o, out_scale=scale, acc=o if with_acc else None,
                           frag=frag)

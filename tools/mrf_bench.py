@@ -18,7 +18,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from visual_onoma_to_wave_amd import _lib, ops  # noqa: E402
 
 PEAK = 2500.0
-FRAG = os.environ.get("VO_FRAG", "1") != "0"  # C = 128 pairs on fragment-ordered weights, as the Generator
+FRAG = os.environ.get("VO_FRAG", "1") != "0"  # C = 64 / 128 pairs on fragment-ordered weights, as the Generator
+# channel widths run on fragment-ordered packs (VO_FRAG_C="128": C = 64 on [K][Co][Ci] packs, for A/B)
+FRAG_C = tuple(int(c) for c in os.environ.get("VO_FRAG_C", "64,128").split(","))
 ACC = os.environ.get("MRF_BENCH_ACC", "1") != "0"  # pairs with the MRF accumulator (0: plain y)
 STAGES = {0: (256, 4096), 1: (128, 32768), 2: (64, 65536), 3: (32, 131072)}
 DILS = (1, 3, 5)
@@ -68,12 +70,12 @@ def workloads(C, T, B):
             out.append(("k3 block (3 pairs)", rb3, 3 * fl1))
         else:
             for d, q in zip(DILS, p):
-                if FRAG and C == 128:  # the Generator's stage-1 packs (vo_pack_frag128)
-                    q = (ops.pack_frag128(q[0]), q[1], ops.pack_frag128(q[2]), q[3])
+                if FRAG and C in FRAG_C:  # the Generator's fragment-ordered packs (vo_pack_frag)
+                    q = (ops.pack_frag(q[0]), q[1], ops.pack_frag(q[2]), q[3])
 
                 def pair(d=d, q=q, k=k):
                     ops.resblock_pair(x, q[0], q[1], q[2], q[3], k, d, 0.1, out=y, out_scale=1.0 / 3,
-                                      acc=acc if ACC else None, frag=FRAG and C == 128)
+                                      acc=acc if ACC else None, frag=FRAG and C in FRAG_C and k in (7, 11))
                 out.append((f"k{k} d{d} pair", pair, fl1))
     return y, out
 

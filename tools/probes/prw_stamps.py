@@ -1,4 +1,4 @@
-"""Per-phase timeline of the C = 128 wave-owned-plane pair (csrc/resblock_rw.hip) from s_memtime stamps.
+"""Per-phase timeline of the C = 128 / 64 wave-owned-plane pair (csrc/resblock_rw.hip) from s_memtime stamps.
 Diagnostic library built here (never the product one):
 
     hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -DVO_PRW_STAMPS \
@@ -27,17 +27,19 @@ NSTW, NSTT, NPT = 16, 4, 28
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 11
     d = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    v = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # kernel variant (pair_cfg 100 + v)
-    L = ctypes.CDLL(os.path.join(ROOT, "tools/probes/build/libprw_stamps.so"))
-    C, B, T = 128, 32, 32768
+    v = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # bit 2: fragment-ordered weights, bit 3: C = 64, bit 4: no acc
+    L = ctypes.CDLL(os.environ.get("PRW_LIB", os.path.join(ROOT, "tools/probes/build/libprw_stamps.so")))
+    C, B, T = (64, 32, 65536) if v & 8 else (128, 32, 32768)
     g = torch.Generator(device="cuda").manual_seed(1)
     x = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
     y = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
     b = torch.randn(C, device="cuda", generator=g) * 0.1
     w = [ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
          for _ in range(2)]
+    if v & 4:
+        w = [ops.pack_frag(q) for q in w]
     for _ in range(5):
-        ops.resblock_pair(x, w[0], b, w[1], b, k, d, 0.1, out=y, out_scale=1 / 3, acc=y)
+        ops.resblock_pair(x, w[0], b, w[1], b, k, d, 0.1, out=y, out_scale=1 / 3, acc=y, frag=bool(v & 4))
     torch.cuda.synchronize()
     n = NSTW * 4 * NSTT * NPT
     buf = (ctypes.c_ulonglong * n)()
@@ -62,7 +64,7 @@ def main():
     # (P1 tap K-1's interval ends at stamp 2+K = end of P1, including the last row tile's epilogue parts;
     #  the B1 interval is 2+K .. 3+K; P2 tap i is K+4+i .. K+5+i; the last one ends at 2K+4 = end of P2)
     tot = np.median((st[..., 2 * K + 4] - st[..., 0]).ravel())
-    print(f"k={k} d={d} v={v}: median tile {tot:.0f} cycles (ideal MFMA {2 * K * 2048})")
+    print(f"C={C} k={k} d={d} v={v}: median tile {tot:.0f} cycles (ideal MFMA {2 * K * 2048 * C // 128})")
     for nm, (i0, i1) in zip(names, idx):
         v = (st[..., i1] - st[..., i0]).ravel()
         print(f"  {nm:22s} median {np.median(v):8.0f}  p10 {np.percentile(v, 10):8.0f}  p90 {np.percentile(v, 90):8.0f}")

@@ -105,7 +105,7 @@ _SIGNATURES = {
                                  c_int, c_int, c_int, c_int, c_float, c_float, c_void_p]),
     "vo_resblock_pair_frag": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                       c_int, c_int, c_int, c_int, c_float, c_float, c_void_p]),
-    "vo_pack_frag128": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "vo_pack_frag": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vo_resblock3": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                              c_int, c_int, c_float, c_float, c_void_p]),
     "vo_conv1d": (c_int, [ctypes.POINTER(Conv1dDesc), c_void_p]),

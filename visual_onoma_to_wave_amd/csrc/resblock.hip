@@ -648,7 +648,7 @@ extern "C" int vo_resblock_pair(const void* x, const void* w1, const float* b1, 
   // 256-row tiles (3 workgroups/CU), K=11 -> 512-row tiles.  pair_cfg selects the
   // alternatives for A/B runs.
   const int cfg = vo_tune_get("pair_cfg");
-  {  // round 5: C = 128 k = 7 / 11 with wave-owned output planes (resblock_rw.hip); pair_cfg 93 = LDS tiles
+  {  // round 5: C = 64 / 128 k = 7 / 11 with wave-owned output planes (resblock_rw.hip); pair_cfg 93 = LDS tiles
     int handled = 0;
     const int rc = vo_pair_rw_try(x, w1, b1, w2, b2, y, acc, B, T, C, K, dil, slope, out_scale, cfg, st, &handled, 0);
     if (handled) return rc;

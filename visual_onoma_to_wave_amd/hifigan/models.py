@@ -94,9 +94,9 @@ class ResBlock(HipModule):
 
     def _build(self, device, dtype):
         packs = [(_pack(c1, device, dtype), _pack(c2, device, dtype)) for c1, c2 in zip(self.convs1, self.convs2)]
-        if self.channels == 128 and self.kernel_size in (7, 11) and dtype == torch.bfloat16 and FRAG_ENABLED:
-            # the stage-1 pair kernel streams its weights in fragment order (vo_pack_frag128)
-            packs = [p + ((ops.pack_frag128(p[0][0]), ops.pack_frag128(p[1][0])),) for p in packs]
+        if self.channels in (64, 128) and self.kernel_size in (7, 11) and dtype == torch.bfloat16 and FRAG_ENABLED:
+            # the C = 64 / 128 pair kernel streams its weights in fragment order (vo_pack_frag)
+            packs = [p + ((ops.pack_frag(p[0][0]), ops.pack_frag(p[1][0])),) for p in packs]
         return packs
 
     def fused(self, x):

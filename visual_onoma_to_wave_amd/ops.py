@@ -459,20 +459,21 @@ def transpose_bct(x, out_dtype, ldy=None):
 
 # ----------------------------------------------------------------------------- fused ResBlock pair
 
-def pack_frag128(w_packed):
-    """[K][128][128] bf16 conv pack -> the fragment order of the C = 128 pair kernel (vo_pack_frag128)."""
+def pack_frag(w_packed):
+    """[K][C][C] bf16 conv pack (C = 64 / 128) -> the fragment order of the pair kernel (vo_pack_frag)."""
     _contig(w_packed, "w_packed")
-    if w_packed.dtype != torch.bfloat16 or w_packed.dim() != 3 or tuple(w_packed.shape[1:]) != (128, 128):
-        raise ValueError("pack_frag128: a [K][128][128] bf16 pack")
+    if (w_packed.dtype != torch.bfloat16 or w_packed.dim() != 3 or w_packed.shape[1] != w_packed.shape[2]
+            or w_packed.shape[1] not in (64, 128)):
+        raise ValueError("pack_frag: a [K][C][C] bf16 pack, C = 64 / 128")
     out = torch.empty_like(w_packed)
-    _lib.check(_lib.lib().vo_pack_frag128(_ptr(w_packed), _ptr(out), w_packed.shape[0], _stream(w_packed)),
-               "vo_pack_frag128")
+    _lib.check(_lib.lib().vo_pack_frag(_ptr(w_packed), _ptr(out), w_packed.shape[1], w_packed.shape[0],
+                                       _stream(w_packed)), "vo_pack_frag")
     return out
 
 
 def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0, acc=None, tag=None, frag=False):
     """y = (x + c2(lrelu(c1_dil(lrelu(x))))) * out_scale (+ acc); x (B, T, C) bf16, C in {32, 64, 128}.
-    frag: w1 / w2 are pack_frag128 packs (C = 128, K = 7 / 11; vo_resblock_pair_frag)."""
+    frag: w1 / w2 are pack_frag packs (C = 64 / 128, K = 7 / 11; vo_resblock_pair_frag)."""
     _contig(x, "x")
     B, T, C = x.shape
     if x.dtype != torch.bfloat16 or w1.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16:
