@@ -103,7 +103,8 @@ def test_step_batched_packs_bit_identical(device):
     one vo_pack_batch call per dtype, the fused q/k/v weights written by three jobs) against per-call
     packs (VO_C4_PREPACK=0 behaviour): four mixed-precision training steps with the optimizer moving the
     weights, losses and every parameter bit for bit; at most two pack calls (fp32 encoder, bf16
-    decoder) per step."""
+    decoder) per step, also in the first step after reset_packs() (the stores seeded from the layouts
+    earlier steps used, as inside a graph capture)."""
     from visual_onoma_to_wave_amd import autograd as AG
     from visual_onoma_to_wave_amd.model import FastSpeech2Loss, ScheduledOptim, vTTS
     from visual_onoma_to_wave_amd.train import train_step
@@ -124,6 +125,8 @@ def test_step_batched_packs_bit_identical(device):
             opt = ScheduledOptim(m, tc, mc, 0)
             losses = []
             for i in range(4):
+                if i == 3:  # a store emptied (as around a graph capture) is re-seeded: still one batch per dtype
+                    AG.reset_packs()
                 b0 = AG.STATS["batches"]
                 losses.append([float(x) for x in train_step(m, opt, FastSpeech2Loss(), batch)])
                 if prepack and i > 0:

@@ -40,7 +40,11 @@ def _bn_case(shape, dtype, seed):
 
 @pytest.mark.parametrize("shape,dtype", [((4, 300, 512), torch.float32), ((3, 77, 80), torch.float32),
                                          ((8, 512, 512), torch.bfloat16), ((384, 1, 24, 102), torch.float32),
-                                         ((5, 1, 24, 7), torch.float32)])
+                                         ((5, 1, 24, 7), torch.float32), ((3, 77, 80), torch.bfloat16),
+                                         # vectorised kernels (C % V == 0, C = 1 with M % V == 0) and the
+                                         # scalar ones (C = 1, M = 45; C = 12: not a whole bf16 vector)
+                                         ((3, 1, 5, 3), torch.float32), ((2, 33, 12), torch.bfloat16),
+                                         ((32, 512, 512), torch.bfloat16)])
 def test_batch_norm_train_fwd_bwd(shape, dtype):
     """y, running mean / var, num_batches_tracked, dx, dgamma, dbeta vs nn.BatchNorm in train mode."""
     from visual_onoma_to_wave_amd import autograd as AG

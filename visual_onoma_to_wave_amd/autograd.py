@@ -79,6 +79,11 @@ class _PackEntry:
 
 
 _STORES = ({}, {})  # [capturing]: packs made inside a graph capture live in the graph's own store
+# every (weights, dtype) a step has packed, and whether its backward wanted the dgrad layout: a store that
+# is empty after reset_packs() is seeded with all of them at its first look-up, so that the step's first
+# conv re-packs every layout of the step in one batch (inside a graph capture too: entries discovered one
+# conv at a time each packed alone, ~100 launches per captured C4 step)
+_KNOWN = {}
 
 
 def _store():
@@ -93,16 +98,30 @@ def reset_packs():
         st.clear()
 
 
+def _seed(store):
+    for key, (refs, cdt, dgrad) in list(_KNOWN.items()):
+        params = tuple(r() for r in refs)
+        if any(p is None for p in params):
+            del _KNOWN[key]
+            continue
+        e = store[key] = _PackEntry(params, cdt)
+        e.need_dgrad = dgrad
+
+
 def _packed_weight(params, cdt, kind):
     """The ``kind`` ("fwd" | "dgrad") layout of the conv whose weight is ``params`` concatenated along
     C_out (fp32 (Co_i, Ci, K) or (Co_i, Ci) parameters), packed for compute dtype ``cdt``."""
     store = _store()
     key = (tuple(id(p) for p in params), cdt)
+    if not store:
+        _seed(store)
     e = store.get(key)
     if e is None or any(a is not b for a, b in zip(e.params, params)):  # new, or ids of dead parameters reused
         e = store[key] = _PackEntry(params, cdt)
-    if kind == "dgrad":
+        _KNOWN[key] = (e.refs, cdt, False)
+    if kind == "dgrad" and not e.need_dgrad:
         e.need_dgrad = True
+        _KNOWN[key] = (e.refs, cdt, True)
     if e.ver.get(kind) != e.version():
         _refresh(store)
     return e.buf[kind]
