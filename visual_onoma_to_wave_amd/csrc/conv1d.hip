@@ -895,6 +895,10 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       const int64_t t256 = (int64_t)d->B * ((d->T_out + 255) / 256) * (d->Co / 256);
       if (d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
+      // Co <= 256 k > 1 with fewer than 512 128 x 128 tiles (the C4 decoder's FFN w_1 input gradient, 1024 ->
+      // 256 k9 at 16384 rows: 125 -> 106 us, tools/probes/dgrad_tiles.py): 64 x 128, twice the workgroups
+      const int64_t t128 = (int64_t)d->B * ((d->T_out + 127) / 128) * ((d->Co + 127) / 128);
+      if (d->Co <= 256 && d->Co % 64 == 0 && t128 < 512) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);
     }
     // mid-width convs (PostNet 512 -> 512 k5, conv_pre 80 -> 512 k7 at 16384 rows): 128 x 256
     // tiles (twice the rows per staged weight tap): 512 k5 67.9 -> 63.4 us, 80 k7 27.6 -> 27.0,
@@ -904,6 +908,8 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     if (gc == 9 || (gc != 1 && gc != 10 && d->Co >= 512 && d->Co < 768 && d->Co % 128 == 0 && !d->transposed))
       return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 4, 2>(d, st);  // 128 x 256
     if (gc == 10) return launch_cfg<TIN, TC, TOUT, 4, 4, 4, 2, 2>(d, st);  // 256 x 128
+    if (gc == 11) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);  // 64 x 128 (A/B)
+    if (gc == 12 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256 (A/B)
   }
   return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }

@@ -274,27 +274,37 @@ __global__ void __launch_bounds__(256) bn_stats_v_kernel(const TX* __restrict__ 
   }
 }
 
-// bn_finalize_kernel with the partial loads issued 8 ahead (the serial chain of dependent-looking
-// loads took 17 us for 32 partials)
-__global__ void bn_finalize_v_kernel(const float* __restrict__ part, int nb, int C, float eps, float momentum,
-                                     float* __restrict__ mean_rstd, float* __restrict__ run_mean,
-                                     float* __restrict__ run_var, int64_t* __restrict__ nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) nbt[0] += 1;
-  if (c >= C) return;
+// finalize: 8 lanes per channel, lane s merging partials s, s + 8, .. (loads issued ahead), then the 8
+// lane results merged in lane order -- a fixed order (deterministic).  One lane walking all 128
+// partials took 17 us (serial merges with a division each, behind one load latency per step).
+constexpr int BN_FL = 8;
+__global__ void __launch_bounds__(256) bn_finalize_v_kernel(const float* __restrict__ part, int nb, int C, float eps,
+                                                            float momentum, float* __restrict__ mean_rstd,
+                                                            float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                            int64_t* __restrict__ nbt) {
+  __shared__ float sn[256], sm[256], s2[256];
+  const int tid = threadIdx.x, sl = tid % BN_FL;
+  const int c = blockIdx.x * (256 / BN_FL) + tid / BN_FL;
+  if (blockIdx.x == 0 && tid == 0 && nbt) nbt[0] += 1;
   Welford w{0.f, 0.f, 0.f};
-  for (int b0 = 0; b0 < nb; b0 += 8) {
-    float q[8][3];
+  if (c < C) {
+    for (int b0 = sl; b0 < nb; b0 += 4 * BN_FL) {
+      float q[4][3];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int b = min(b0 + i, nb - 1);
-      const float* p = part + ((int64_t)b * C + c) * 3;
-      q[i][0] = p[0]; q[i][1] = p[1]; q[i][2] = p[2];
+      for (int i = 0; i < 4; ++i) {
+        const int b = min(b0 + i * BN_FL, nb - 1);
+        const float* p = part + ((int64_t)b * C + c) * 3;
+        q[i][0] = p[0]; q[i][1] = p[1]; q[i][2] = p[2];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (b0 + i * BN_FL < nb) w = wf_merge(w, Welford{q[i][0], q[i][1], q[i][2]});
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (b0 + i < nb) w = wf_merge(w, Welford{q[i][0], q[i][1], q[i][2]});
   }
+  sn[tid] = w.n; sm[tid] = w.mean; s2[tid] = w.m2;
+  __syncthreads();
+  if (sl != 0 || c >= C) return;
+  for (int k = 1; k < BN_FL; ++k) w = wf_merge(w, Welford{sn[tid + k], sm[tid + k], s2[tid + k]});
   const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
   mean_rstd[c] = w.mean;
   mean_rstd[C + c] = rsqrtf(var + eps);
@@ -305,6 +315,9 @@ __global__ void bn_finalize_v_kernel(const float* __restrict__ part, int nb, int
   }
 }
 
+// apply: the grid's thread count is a multiple of CV (the launcher rounds it), so a thread's vector
+// column -- and its channels' parameters, loaded once -- stays the same over the grid-stride loop
+// (per-element parameter loads, 8 channels 32 bytes apart per lane, ran the kernel at 59 us)
 template <typename TX, bool FLAT>
 __global__ void __launch_bounds__(256) bn_apply_v_kernel(const TX* __restrict__ x, int nvec, int C,
                                                          const float* __restrict__ mean_rstd,
@@ -313,16 +326,22 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const TX* __restrict__ 
   using VT = BnVec<TX>;
   constexpr int V = VT::V;
   const int CV = FLAT ? 1 : C / V;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
-    const int c0 = FLAT ? 0 : (i % CV) * V;
+  const int i0 = blockIdx.x * 256 + threadIdx.x;
+  const int c0 = FLAT ? 0 : (i0 % CV) * V;
+  float mu[V], rs[V], ga[V], be[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = FLAT ? 0 : c0 + e;
+    mu[e] = mean_rstd[c]; rs[e] = mean_rstd[C + c];
+    ga[e] = gamma ? gamma[c] : 1.f; be[e] = gamma ? beta[c] : 0.f;
+  }
+  for (int i = i0; i < nvec; i += gridDim.x * 256) {
     float v[V];
     VT::load(x + (int64_t)i * V, v);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int c = FLAT ? 0 : c0 + e;
-      float t = (v[e] - mean_rstd[c]) * mean_rstd[C + c];
-      if (gamma) t = t * gamma[c] + beta[c];
-      v[e] = t;
+      const float t = (v[e] - mu[e]) * rs[e];
+      v[e] = gamma ? t * ga[e] + be[e] : t;
     }
     VT::store(y + (int64_t)i * V, v);
   }
@@ -396,23 +415,30 @@ __global__ void __launch_bounds__(256) bn_bwd_stats_v_kernel(const TX* __restric
   }
 }
 
-__global__ void bn_bwd_finalize_v_kernel(const float* __restrict__ part, int nb, int C, float* __restrict__ dgamma,
-                                         float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ void __launch_bounds__(256) bn_bwd_finalize_v_kernel(const float* __restrict__ part, int nb, int C,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float sa[256], sb[256];
+  const int tid = threadIdx.x, sl = tid % BN_FL;
+  const int c = blockIdx.x * (256 / BN_FL) + tid / BN_FL;
   float a = 0.f, b = 0.f;
-  for (int k0 = 0; k0 < nb; k0 += 8) {
-    float q[8][2];
+  if (c < C) {
+    for (int k0 = sl; k0 < nb; k0 += 4 * BN_FL) {
+      float q[4][2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k = min(k0 + i, nb - 1);
-      q[i][0] = part[((int64_t)k * C + c) * 2];
-      q[i][1] = part[((int64_t)k * C + c) * 2 + 1];
+      for (int i = 0; i < 4; ++i) {
+        const int k = min(k0 + i * BN_FL, nb - 1);
+        q[i][0] = part[((int64_t)k * C + c) * 2];
+        q[i][1] = part[((int64_t)k * C + c) * 2 + 1];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (k0 + i * BN_FL < nb) { a += q[i][0]; b += q[i][1]; }
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (k0 + i < nb) { a += q[i][0]; b += q[i][1]; }
   }
+  sa[tid] = a; sb[tid] = b;
+  __syncthreads();
+  if (sl != 0 || c >= C) return;
+  for (int k = 1; k < BN_FL; ++k) { a += sa[tid + k]; b += sb[tid + k]; }
   dbeta[c] = a;
   dgamma[c] = b;
 }
@@ -426,8 +452,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const TX* __restric
                                                              const float* __restrict__ dbeta, TX* __restrict__ dx) {
   constexpr int V = BnVec<TX>::V;
   const int CV = FLAT ? 1 : C / V;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
-    const int c0 = FLAT ? 0 : (i % CV) * V;
+  const int i0 = blockIdx.x * 256 + threadIdx.x;
+  const int c0 = FLAT ? 0 : (i0 % CV) * V;
+  float mu[V], rs[V], gr[V], db[V], dg[V];  // gr = gamma rstd, db / dg = dbeta / M, dgamma / M
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = FLAT ? 0 : c0 + e;
+    mu[e] = mean_rstd[c]; rs[e] = mean_rstd[C + c];
+    gr[e] = (gamma ? gamma[c] : 1.f) * rs[e];
+    db[e] = dbeta[c] * inv_m; dg[e] = dgamma[c] * inv_m;
+  }
+  for (int i = i0; i < nvec; i += gridDim.x * 256) {
     const int64_t o = (int64_t)i * V;
     float xv[V], gv[V];
     BnVec<TX>::load(x + o, xv);
@@ -440,11 +475,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const TX* __restric
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int c = FLAT ? 0 : c0 + e;
-      const float rs = mean_rstd[C + c];
-      const float xh = (xv[e] - mean_rstd[c]) * rs;
-      const float g = gamma ? gamma[c] : 1.f;
-      xv[e] = g * rs * (gv[e] - dbeta[c] * inv_m - xh * dgamma[c] * inv_m);
+      const float xh = (xv[e] - mu[e]) * rs[e];
+      xv[e] = gr[e] * (gv[e] - db[e] - xh * dg[e]);
     }
     BnVec<TX>::store(dx + o, xv);
   }
@@ -767,6 +799,17 @@ static bool bn_vec_ok(int M, int C, int dtype, bool* flat) {
   return C % V == 0 && C / V <= 256;
 }
 
+// apply grid: at most 2048 blocks, the thread count a multiple of the CV vector columns (so that every
+// thread keeps one column: bn_apply_v_kernel)
+static unsigned bn_apply_blocks(int nvec, int CV) {
+  int g = 256, c = CV;
+  while (c) { const int t = g % c; g = c; c = t; }  // gcd(256, CV)
+  const int step = CV / g;
+  int64_t blk = std::min<int64_t>((nvec + 255) / 256, 2048);
+  blk = (blk + step - 1) / step * step;
+  return (unsigned)std::max<int64_t>(blk, step);
+}
+
 static void bn_vec_geometry(int M, int C, int dtype, bool flat, int* rows, int* RB, int* nb) {
   const int V = dtype == VO_BF16 ? 8 : 4;
   *rows = flat ? M / V : M;
@@ -806,12 +849,12 @@ extern "C" int vo_bn_train_fwd(const void* x, int dtype, int M, int C, const flo
     bn_vec_geometry(M, C, dtype, flat, &rows, &RBv, &nbv);
     const int V = dtype == VO_BF16 ? 8 : 4;
     const int nvec = (int)((int64_t)M * C / V);
-    const unsigned ablk = (unsigned)std::min<int64_t>((nvec + 255) / 256, 2048);
+    const unsigned ablk = bn_apply_blocks(nvec, flat ? 1 : C / V);
 #define VO_BN_FWD(TX, FL)                                                                                          \
   do {                                                                                                             \
     hipLaunchKernelGGL((bn_stats_v_kernel<TX, FL>), dim3((unsigned)nbv), dim3(256), 0, st, (const TX*)x, rows, C, RBv, \
                        workspace);                                                                                 \
-    hipLaunchKernelGGL(bn_finalize_v_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, workspace, nbv, C,  \
+    hipLaunchKernelGGL(bn_finalize_v_kernel, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, st, workspace, nbv, C,    \
                        eps, momentum, mean_rstd, run_mean, run_var, nbt);                                          \
     hipLaunchKernelGGL((bn_apply_v_kernel<TX, FL>), dim3(ablk), dim3(256), 0, st, (const TX*)x, nvec, C, mean_rstd,  \
                        gamma, beta, (TX*)y);                                                                       \
@@ -860,13 +903,13 @@ extern "C" int vo_bn_bwd(const void* x, int x_dtype, const void* dy, int dy_dtyp
     bn_vec_geometry(M, C, x_dtype, flat, &rows, &RBv, &nbv);
     const int V = x_dtype == VO_BF16 ? 8 : 4;
     const int nvec = (int)((int64_t)M * C / V);
-    const unsigned ablk = (unsigned)std::min<int64_t>((nvec + 255) / 256, 2048);
+    const unsigned ablk = bn_apply_blocks(nvec, flat ? 1 : C / V);
     const float inv_m = 1.f / (float)M;
 #define VO_BNB_V(TX, TG, FL)                                                                                        \
   do {                                                                                                              \
     hipLaunchKernelGGL((bn_bwd_stats_v_kernel<TX, TG, FL>), dim3((unsigned)nbv), dim3(256), 0, st, (const TX*)x,     \
                        (const TG*)dy, rows, C, RBv, mean_rstd, workspace);                                          \
-    hipLaunchKernelGGL(bn_bwd_finalize_v_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, workspace, nbv, \
+    hipLaunchKernelGGL(bn_bwd_finalize_v_kernel, dim3((unsigned)((C + 31) / 32)), dim3(256), 0, st, workspace, nbv,   \
                        C, dgamma, dbeta);                                                                           \
     hipLaunchKernelGGL((bn_bwd_apply_v_kernel<TX, TG, FL>), dim3(ablk), dim3(256), 0, st, (const TX*)x,             \
                        (const TG*)dy, nvec, C, inv_m, mean_rstd, gamma, dgamma, dbeta, (TX*)dx);                    \
