@@ -515,6 +515,14 @@ int vo_bn_train_fwd(const void* x, int dtype, int M, int C, const float* gamma, 
 int vo_bn_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, int M, int C, const float* gamma,
               const float* mean_rstd, float* workspace, float* dgamma, float* dbeta, void* dx, void* stream);
 
+/* Dropout in training (nn.Dropout / F.dropout: scripts/transformer/SubLayers.py:38,87,
+ * scripts/transformer/Layers.py:129-131, scripts/model/modules.py:52-56): y[i] = x[i] / (1 - p) when
+ * hash(*seed, salt, i) >= p 2^32, else 0 (x, y fp32 / bf16, 16-byte aligned, n < 2^32; y may alias x).
+ * The mask depends only on (*seed, salt, i): the backward is the same call on dy.  One device seed per
+ * training step, a distinct salt per dropout site of the step. */
+int vo_dropout(const void* x, int dtype, int64_t n, float p, const int64_t* seed, unsigned salt, void* y,
+               void* stream);
+
 /* Glyph-encoder Conv2d(1, 1, 3, padding=1) on N single-channel H x W maps (fp32), w[0..9) the
  * row-major kernel, w[9] the bias (scripts/model/visual_feature_extractor.py:40-47,60-72):
  * forward, and the backward -> dx and dw[10] (weight + bias gradient; per-block partials summed in

@@ -262,3 +262,48 @@ def test_bucket_embed_vs_torch(dt):
     from visual_onoma_to_wave_amd import ops
     with pytest.raises(Exception, match="table has 200 rows"):
         ops.bucket_embed(x.cuda().contiguous(), tgt.cuda(), bins.cuda(), torch.zeros(200, D, device="cuda"))
+
+
+@pytest.mark.parametrize("dtype,shape", [(torch.bfloat16, (32, 512, 256)), (torch.float32, (32, 12, 256)),
+                                         (torch.float32, (3, 7, 5)), (torch.bfloat16, (2, 3, 3))])
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_dropout_counter_mask(dtype, shape, p):
+    """autograd.dropout (vo_dropout): kept elements are x / (1 - p) exactly as F.dropout scales them, the
+    keep rate is 1 - p, the backward applies the forward's mask (no mask tensor), a new call draws a new
+    mask, and n % 8 tails are covered."""
+    from visual_onoma_to_wave_amd import autograd as AG
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    x = (torch.rand(shape, device="cuda", generator=g) + 0.5).to(dtype).requires_grad_(True)
+    y = AG.dropout(x, p)
+    keep = y.detach() != 0
+    scaled = (x.detach().float() * (1.0 / (1.0 - p))).to(dtype)
+    assert torch.equal(y.detach()[keep], scaled[keep])
+    n = x.numel()
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - p)) < 5 * (p * (1 - p) / n) ** 0.5 + 1e-9, rate
+    gy = torch.rand(shape, device="cuda", generator=g).to(dtype) + 1.0
+    y.backward(gy)
+    gk = x.grad != 0
+    assert torch.equal(gk, keep)
+    assert torch.equal(x.grad[keep], (gy.float() * (1.0 / (1.0 - p))).to(dtype)[keep])
+    if n > 1000:
+        y2 = AG.dropout(x.detach(), p)
+        assert not torch.equal(y2 != 0, keep)
+
+
+def test_dropout_graph_replays_draw_new_masks():
+    """Captured in a HIP graph, every replay draws a new step seed (torch's graph-safe generator)."""
+    from visual_onoma_to_wave_amd import autograd as AG
+    x = torch.ones(64, 1024, device="cuda", dtype=torch.bfloat16)
+    AG.begin_dropout_step(x.device)
+    AG.dropout(x, 0.5)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        AG.begin_dropout_step(x.device)  # the step's seed, drawn inside the graph
+        y = AG.dropout(x, 0.5)
+    masks = []
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        masks.append(y != 0)
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])

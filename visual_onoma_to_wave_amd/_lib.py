@@ -202,6 +202,7 @@ _SIGNATURES = {
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_bn_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_void_p]),
+    "vo_dropout": (c_int, [c_void_p, c_int, c_int64, c_float, c_void_p, ctypes.c_uint, c_void_p, c_void_p]),
     "vo_vfe_conv_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),
     "vo_vfe_conv_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vo_vfe_conv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

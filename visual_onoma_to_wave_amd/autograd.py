@@ -302,6 +302,55 @@ def layernorm(x, res, g, b, lens=None):
     return LayerNormFn.apply(x, res, g, b, lens)
 
 
+class DropoutFn(torch.autograd.Function):
+    """Training dropout on HIP (vo_dropout): the keep mask is a hash of (seed, site, element index), so
+    the backward re-applies it to the gradient from the saved seed -- no mask tensor."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed, salt):
+        ctx.p, ctx.salt = p, salt
+        ctx.save_for_backward(seed)
+        return ops.dropout(x, p, seed, salt)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (seed,) = ctx.saved_tensors
+        g = gy.contiguous()
+        if g.data_ptr() % 16:
+            g = g.clone()
+        return ops.dropout(g, ctx.p, seed, ctx.salt), None, None, None
+
+
+_DROP = {"seed": None, "site": 0}
+
+
+def begin_dropout_step(device):
+    """Draw the step's dropout seed (one int64 from torch's generator, on the device: graph-safe, every
+    replay of a captured step draws anew); the step's dropout sites then salt it with their call index.
+    Without it each dropout call draws its own seed (one more small kernel per call)."""
+    _DROP["seed"] = torch.randint(1, 2 ** 62, (1,), device=device, dtype=torch.int64)
+    _DROP["site"] = 0
+
+
+def dropout(x, p, training=True):
+    """F.dropout(x, p, training) for the training forward (scripts/transformer/SubLayers.py:38,87,
+    scripts/transformer/Layers.py:129-131, scripts/model/modules.py:52-56): masks differ per step and
+    per call as with F.dropout (the draws differ from ATen's)."""
+    if not training or p == 0.0:
+        return x
+    if p == 1.0:
+        return x * 0.0
+    xc = x.contiguous()
+    if xc.data_ptr() % 16:
+        xc = xc.clone()
+    seed = _DROP["seed"]
+    if seed is None or seed.device != x.device:
+        seed, salt = torch.randint(1, 2 ** 62, (1,), device=x.device, dtype=torch.int64), 0
+    else:
+        salt = _DROP["site"] = _DROP["site"] + 1
+    return DropoutFn.apply(xc, float(p), seed, salt)
+
+
 class LengthRegulateFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, dur, max_len, out_dtype):

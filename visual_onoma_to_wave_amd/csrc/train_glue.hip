@@ -204,6 +204,7 @@ template <> struct BnVec<bf16_t> {
 };
 
 constexpr int BN_NB = 128;  // row blocks (partials per channel) of the vectorised kernels
+constexpr int BN_CMAX = 2048;  // channels of the vectorised kernels (C / V <= 256 vector columns)
 
 // part[block][c] = (n, mean, m2).  Non-FLAT: CV = C / V vector columns, RL = 256 / CV row lanes, rows
 // [blockIdx.x RB, +RB) of M.  FLAT (C = 1): the M elements as M / V rows of one vector.
@@ -328,22 +329,36 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const TX* __restrict__ 
   const int CV = FLAT ? 1 : C / V;
   const int i0 = blockIdx.x * 256 + threadIdx.x;
   const int c0 = FLAT ? 0 : (i0 % CV) * V;
+  // the block's copy of the per-channel parameters (coalesced), then 8 consecutive per thread from LDS
+  // (each thread loading its own 8-channel run from global was the kernel's cost: 32 scattered loads)
+  __shared__ float sp[4][BN_CMAX];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    sp[0][c] = mean_rstd[c]; sp[1][c] = mean_rstd[C + c];
+    sp[2][c] = gamma ? gamma[c] : 1.f; sp[3][c] = gamma ? beta[c] : 0.f;
+  }
+  __syncthreads();
   float mu[V], rs[V], ga[V], be[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     const int c = FLAT ? 0 : c0 + e;
-    mu[e] = mean_rstd[c]; rs[e] = mean_rstd[C + c];
-    ga[e] = gamma ? gamma[c] : 1.f; be[e] = gamma ? beta[c] : 0.f;
+    mu[e] = sp[0][c]; rs[e] = sp[1][c]; ga[e] = sp[2][c]; be[e] = sp[3][c];
   }
-  for (int i = i0; i < nvec; i += gridDim.x * 256) {
-    float v[V];
-    VT::load(x + (int64_t)i * V, v);
+  // four vectors in flight per thread (one load, wait, compute, store at a time ran at 0.9 TB/s)
+  const int stride = gridDim.x * 256;
+  for (int i = i0; i < nvec; i += 4 * stride) {
+    float v[4][V];
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const float t = (v[e] - mu[e]) * rs[e];
-      v[e] = gamma ? t * ga[e] + be[e] : t;
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < nvec) VT::load(x + (int64_t)(i + u * stride) * V, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float t = (v[u][e] - mu[e]) * rs[e];
+        v[u][e] = gamma ? t * ga[e] + be[e] : t;
+      }
+      if (i + u * stride < nvec) VT::store(y + (int64_t)(i + u * stride) * V, v[u]);
     }
-    VT::store(y + (int64_t)i * V, v);
   }
 }
 
@@ -454,32 +469,89 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const TX* __restric
   const int CV = FLAT ? 1 : C / V;
   const int i0 = blockIdx.x * 256 + threadIdx.x;
   const int c0 = FLAT ? 0 : (i0 % CV) * V;
+  __shared__ float sp[5][BN_CMAX];  // per-channel parameters staged once per block (see bn_apply_v_kernel)
+  for (int c = threadIdx.x; c < C; c += 256) {
+    sp[0][c] = mean_rstd[c]; sp[1][c] = mean_rstd[C + c];
+    sp[2][c] = (gamma ? gamma[c] : 1.f) * mean_rstd[C + c];
+    sp[3][c] = dbeta[c] * inv_m; sp[4][c] = dgamma[c] * inv_m;
+  }
+  __syncthreads();
   float mu[V], rs[V], gr[V], db[V], dg[V];  // gr = gamma rstd, db / dg = dbeta / M, dgamma / M
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     const int c = FLAT ? 0 : c0 + e;
-    mu[e] = mean_rstd[c]; rs[e] = mean_rstd[C + c];
-    gr[e] = (gamma ? gamma[c] : 1.f) * rs[e];
-    db[e] = dbeta[c] * inv_m; dg[e] = dgamma[c] * inv_m;
+    mu[e] = sp[0][c]; rs[e] = sp[1][c]; gr[e] = sp[2][c]; db[e] = sp[3][c]; dg[e] = sp[4][c];
   }
-  for (int i = i0; i < nvec; i += gridDim.x * 256) {
-    const int64_t o = (int64_t)i * V;
-    float xv[V], gv[V];
-    BnVec<TX>::load(x + o, xv);
-    if constexpr (sizeof(TG) == sizeof(TX)) {
-      BnVec<TG>::load(dy + o, gv);
-    } else {
-      const uint2 u = *reinterpret_cast<const uint2*>(dy + o);
-      gv[0] = __uint_as_float(u.x << 16); gv[1] = __uint_as_float(u.x & 0xffff0000u);
-      gv[2] = __uint_as_float(u.y << 16); gv[3] = __uint_as_float(u.y & 0xffff0000u);
+  const int stride = gridDim.x * 256;
+  for (int i = i0; i < nvec; i += 2 * stride) {  // two vectors of x and dy in flight per thread
+    float xv[2][V], gv[2][V];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (i + u * stride >= nvec) continue;
+      const int64_t o = (int64_t)(i + u * stride) * V;
+      BnVec<TX>::load(x + o, xv[u]);
+      if constexpr (sizeof(TG) == sizeof(TX)) {
+        BnVec<TG>::load(dy + o, gv[u]);
+      } else {
+        const uint2 q = *reinterpret_cast<const uint2*>(dy + o);
+        gv[u][0] = __uint_as_float(q.x << 16); gv[u][1] = __uint_as_float(q.x & 0xffff0000u);
+        gv[u][2] = __uint_as_float(q.y << 16); gv[u][3] = __uint_as_float(q.y & 0xffff0000u);
+      }
     }
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const float xh = (xv[e] - mu[e]) * rs[e];
-      xv[e] = gr[e] * (gv[e] - db[e] - xh * dg[e]);
+    for (int u = 0; u < 2; ++u) {
+      if (i + u * stride >= nvec) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xh = (xv[u][e] - mu[e]) * rs[e];
+        xv[u][e] = gr[e] * (gv[u][e] - db[e] - xh * dg[e]);
+      }
+      BnVec<TX>::store(dx + (int64_t)(i + u * stride) * V, xv[u]);
     }
-    BnVec<TX>::store(dx + o, xv);
   }
+}
+
+// ------------------------------------------------------------------------------- dropout
+// Counter-based dropout (nn.Dropout / F.dropout in training, scripts/transformer/SubLayers.py:38,87,
+// scripts/transformer/Layers.py:129-131, scripts/model/modules.py:52-56): element i is kept iff
+// hash(seed, i) >= p 2^32, y = keep ? x / (1 - p) : 0.  The mask is a pure function of (seed, i), so
+// the backward is the same call on dy -- no mask tensor is written or read (ATen's fused_dropout writes
+// one byte per element and its masked_scale reads it back).  seed: a device int64 drawn per call from
+// torch's generator (graph-safe: every replay draws a new one).
+__device__ __forceinline__ uint32_t drop_mix(uint32_t h) {  // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t i) {
+  return drop_mix(drop_mix(i * 0x9E3779B9u ^ s0) + s1);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, int64_t n, uint32_t thr, float scale,
+                                                      const int64_t* __restrict__ seed, uint32_t salt,
+                                                      T* __restrict__ y) {
+  using VT = BnVec<T>;
+  constexpr int V = VT::V;
+  const uint64_t sd = (uint64_t)seed[0];
+  const uint32_t s0 = (uint32_t)sd ^ drop_mix(salt + 0x3C6EF372u), s1 = (uint32_t)(sd >> 32);
+  const int64_t nv = n / V;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += 4 * stride) {  // 4 vectors in flight
+    float v[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < nv) VT::load(x + (i + u * stride) * V, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t iv = i + u * stride;
+      if (iv >= nv) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[u][e] = drop_hash(s0, s1, (uint32_t)(iv * V + e)) >= thr ? v[u][e] * scale : 0.f;
+      VT::store(y + iv * V, v[u]);
+    }
+  }
+  const int64_t t = nv * V + threadIdx.x;  // the n % V tail, one element a thread of block 0
+  if (blockIdx.x == 0 && t < n) y[t] = from_f32<T>(drop_hash(s0, s1, (uint32_t)t) >= thr ? to_f32(x[t]) * scale : 0.f);
 }
 
 // ------------------------------------------------------------------------------- 3 x 3 single-channel conv
@@ -805,7 +877,7 @@ static unsigned bn_apply_blocks(int nvec, int CV) {
   int g = 256, c = CV;
   while (c) { const int t = g % c; g = c; c = t; }  // gcd(256, CV)
   const int step = CV / g;
-  int64_t blk = std::min<int64_t>((nvec + 255) / 256, 2048);
+  int64_t blk = std::min<int64_t>((nvec + 1023) / 1024, 1024);  // ~4 vectors per thread (4096 blocks: 3x slower)
   blk = (blk + step - 1) / step * step;
   return (unsigned)std::max<int64_t>(blk, step);
 }
@@ -1051,5 +1123,27 @@ extern "C" int vo_stft_loss_grad(const float* xm, const float* ym, int64_t n, co
   const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(stft_loss_grad_kernel, dim3(nb), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xm, ym, n,
                      sums, w, gx);
+  VO_RETURN_LAUNCH();
+}
+
+extern "C" int vo_dropout(const void* x, int dtype, int64_t n, float p, const int64_t* seed, unsigned salt, void* y,
+                          void* stream) {
+  VO_CHECK_ARG(x && y && seed && n >= 0, "dropout: bad arguments");
+  VO_CHECK_ARG(dtype == VO_F32 || dtype == VO_BF16, "dropout: dtype");
+  VO_CHECK_ARG(p >= 0.f && p < 1.f, "dropout: p = %g outside [0, 1)", p);
+  VO_CHECK_ARG(n < (1LL << 32), "dropout: %lld elements (the mask index is 32-bit)", (long long)n);
+  VO_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0, "dropout: x / y must be 16-byte aligned");
+  if (n == 0) return VO_OK;
+  const uint32_t thr = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+  const float scale = 1.f / (1.f - p);
+  const int V = dtype == VO_BF16 ? 8 : 4;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n / V + 255) / 256, 8192));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == VO_BF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, n, thr, scale, seed,
+                       (uint32_t)salt, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, n, thr, scale, seed,
+                       (uint32_t)salt, (float*)y);
   VO_RETURN_LAUNCH();
 }

@@ -94,7 +94,7 @@ static const char* const kSymbols[] = {
     "vo_avgpool_wav_bwd", "vo_weight_norm", "vo_weight_norm_bwd", "vo_pack_dgrad_phase", "vo_pack_batch", "vo_seq_remap", "vo_seq_remap2", "vo_lrelu_mask_add", "vo_lrelu_mask_sum", "vo_spectral_norm", "vo_gan_reduce_multi", "vo_gan_reduce_multi_workspace_size", "vo_gan_reduce_grad_multi", "vo_spectral_norm_bwd", "vo_spectral_norm_bwd_workspace_size", "vo_conv1d_wgrad_workspace_size", "vo_colsum_workspace_size", "vo_stft_mag",
     "vo_stft_mag_bwd_workspace_size", "vo_stft_mag_bwd", "vo_stft_loss", "vo_stft_loss_grad",
     "vo_bucket_embed",   "vo_embed_bwd",     "vo_adam_multi",  "vo_opt_step_increment",
-    "vo_resblock_pair_frag", "vo_pack_frag", "vo_attention_lse", "vo_attention_bwd_lse",
+    "vo_resblock_pair_frag", "vo_pack_frag", "vo_attention_lse", "vo_attention_bwd_lse", "vo_dropout",
 };
 
 extern "C" int vo_num_symbols(void) { return (int)(sizeof(kSymbols) / sizeof(kSymbols[0])); }

@@ -86,9 +86,9 @@ class VariancePredictor(HipModule):
         c, cd, k = self.conv_layer, self.compute_dtype, self.kernel
         h = AG.conv1d(x, c.conv1d_1.conv.weight, c.conv1d_1.conv.bias, K=k, pad=(k - 1) // 2, relu=True,
                       compute_dtype=cd)
-        h = F.dropout(AG.layernorm(h, None, c.layer_norm_1.weight, c.layer_norm_1.bias), self.dropout, True)
+        h = AG.dropout(AG.layernorm(h, None, c.layer_norm_1.weight, c.layer_norm_1.bias), self.dropout)
         h = AG.conv1d(h, c.conv1d_2.conv.weight, c.conv1d_2.conv.bias, K=k, pad=1, relu=True, compute_dtype=cd)
-        h = F.dropout(AG.layernorm(h, None, c.layer_norm_2.weight, c.layer_norm_2.bias), self.dropout, True)
+        h = AG.dropout(AG.layernorm(h, None, c.layer_norm_2.weight, c.layer_norm_2.bias), self.dropout)
         out = F.linear(h.float(), self.linear_layer.weight, self.linear_layer.bias).squeeze(-1)
         return out.masked_fill(mask, 0.0) if mask is not None else out
 

@@ -92,6 +92,7 @@ class vTTS(HipModule):
         """Training step forward (dropout and BatchNorm batch statistics active; autograd records
         HIP-forward ops, see visual_onoma_to_wave_amd.autograd)."""
         from .. import autograd as AG
+        AG.begin_dropout_step(texts.device)  # one device seed for every dropout site of this step
         src_masks, src_l32 = ops.mask_from_lengths(src_lens, max_src_len)
         if mels is None:
             raise ValueError("training needs mels / mel_lens / max_mel_len (teacher forcing)")

@@ -10,7 +10,6 @@ PostNet  <- scripts/transformer/Layers.py:67-137 (5 x Conv1d k5 + BatchNorm1d(ev
 import torch
 import torch.nn as nn
 
-import torch.nn.functional as F
 
 from .. import autograd as AG
 from .. import ops
@@ -40,12 +39,12 @@ class FFTBlock(HipModule):
         qkv = AG.qkv_linear(x, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
                             mha.w_vs.bias, cd)
         att = AG.attention(qkv, lens, mha.n_head)
-        y = F.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p, True)
+        y = AG.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p)
         x1 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
         k1, k2 = ffn.kernel_size
         h = AG.conv1d(x1, ffn.w_1.weight, ffn.w_1.bias, K=k1, pad=(k1 - 1) // 2, relu=True, compute_dtype=cd)
         y2 = AG.conv1d(h, ffn.w_2.weight, ffn.w_2.bias, K=k2, pad=(k2 - 1) // 2, compute_dtype=cd)
-        y2 = F.dropout(y2, ffn.dropout.p, True)
+        y2 = AG.dropout(y2, ffn.dropout.p)
         return AG.layernorm(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens)
 
     def forward(self, enc_input, mask=None, slf_attn_mask=None):
@@ -122,7 +121,7 @@ class PostNet(HipModule):
             hb = AG.batch_norm_train(h, bn, (0, 1))  # channels-last (B, T, C): no transposes
             if not last:
                 hb = torch.tanh(hb)
-            h = F.dropout(hb, self.dropout_p, True).contiguous()
+            h = AG.dropout(hb, self.dropout_p)
         return h
 
     def forward(self, x):
