@@ -64,19 +64,6 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     B, T_in, ldx = x.shape
     if x.stride(2) != 1 or x.stride(1) != ldx:
         raise ValueError("conv1d: x must be row-contiguous (B, T, C)")
-    if (K == 1 and pad == 0 and stride == 1 and groups == 1 and transposed is None and B > 1 and T_in < 64
-            and (T_out is None or T_out == T_in) and x.is_contiguous() and ymask is None
-            and (out is None or out.is_contiguous())):
-        # pointwise conv over short utterances (the glyph encoder / predictors at T_src ~ 12): the batch
-        # as one sequence of B T rows -- the kernel's time tiles never span utterances, so 12-row
-        # utterances left each tile mostly empty and re-read the weights once per utterance
-        y = conv1d(x.reshape(1, B * T_in, ldx), w_packed, bias, Co=Co, K=1, out=None if out is None else
-                   out.view(1, B * T_in, out.shape[-1]), out_dtype=out_dtype, pre_act=pre_act, pre_slope=pre_slope,
-                   post_act=post_act, post_slope=post_slope,
-                   res1=None if res1 is None else res1.reshape(1, B * T_in, res1.shape[-1]),
-                   res2=None if res2 is None else res2.reshape(1, B * T_in, res2.shape[-1]), out_scale=out_scale,
-                   compute_dtype=compute_dtype, variant=variant, tag=tag)
-        return y.view(B, T_in, y.shape[-1])
     Ci = w_packed.shape[2]
     if w_packed.shape[0] != K or w_packed.shape[1] != Co:
         raise ValueError(f"conv1d: packed weight {tuple(w_packed.shape)} != [{K}][{Co}][Ci]")
