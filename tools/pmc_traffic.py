@@ -31,7 +31,7 @@ def load(path, counter):
         if m and m.group(1) != "0":
             acc[f"mrf_s{int(m.group(1)) - 1}"].append(float(r["Counter_Value"]))
             continue
-        m = re.search(r"mrf_(?:pair2?|rb3|rr3w?|rrp)_kernel<(\d+),", name)  # fused pairs / blocks: stage by width
+        m = re.search(r"mrf_(?:pair2?|rb3|rr3w?|rrp|prw)_kernel<(\d+),", name)  # fused pairs / blocks: stage by width
         if m and int(m.group(1)) in PAIR_STAGE:
             acc[PAIR_STAGE[int(m.group(1))]].append(float(r["Counter_Value"]))
             continue

@@ -74,6 +74,20 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
 #define VO_PRW_XT 0
 #endif
   constexpr int XT = K > 2 ? VO_PRW_XT : 0;   // P2 tap whose first plane also adds the residual (see p2_extra)
+#ifndef VO_PRW_AP2
+#define VO_PRW_AP2 1
+#endif
+  // ACC == 2: the MRF accumulator rows (HBM misses, unlike the residual rows the window staging just
+  // brought into L2) requested over P2 taps 0 .. ANT - 1 and added at tap XA (AP2).  Requested with the
+  // residual in P1's last two taps, the in-order vmcnt drained them at the next tap's weight wait:
+  // those two taps ran 3,996 + 6,240 cycles for 2 x 1,168 (stamps, C = 64 k = 11); in P2 over four taps
+  // a tile takes 38.4k cycles against 42.8k (C = 64 k = 11), 61.6k against 64.5k (C = 128 k = 11)
+  constexpr bool AP2 = VO_PRW_AP2 != 0 && ACC == 2;
+#ifndef VO_PRW_ANT
+#define VO_PRW_ANT 4
+#endif
+  constexpr int ANT = VO_PRW_ANT, ARPT = NJ / ANT;  // taps carrying the requests, row tiles per tap
+  constexpr int XA = AP2 ? (ANT + 1 < K - 1 ? ANT + 1 : K - 1) : XT;
   // (XT = 1 moved the identity MFMAs' cost to tap 1 unchanged: it is their issue, not a dependency stall)
   constexpr int NB = 10, DB = 8;              // B-fragment ring / prefetch distance (steps); 12 / 14 measured no faster
   // ACC: 0 = no MRF accumulator; 1 = y = acc_out * out_scale + acc_in (epilogue add); 2 = acc_in / out_scale
@@ -267,7 +281,7 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
       {
         const int off = ((t0 + row0 + 16 * j + lr) * C + cofs) * 2;  // rows past T: read 0
         xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
-        if constexpr (ACC == 2) ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
+        if constexpr (ACC == 2 && !AP2) ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
       }
     };
     const f32x4* bias1 = reinterpret_cast<const f32x4*>(sbias + cofs);
@@ -305,6 +319,13 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
         const int i = (jj - 2 * NAP - SP2 / 2) / SP2, sl = (k - 2) * SPT + i;
         if (i < SPT && k >= 2 && sl < NWV) store_win1(sl);
       }
+      if constexpr (AP2) {  // ARPT row tiles' accumulator rows per tap in taps 0 .. ANT - 1
+        constexpr int ASP = (NST - 2 * NAP) / ARPT;
+        if (k < ANT && jj >= 2 * NAP && (jj - 2 * NAP) % ASP == 0 && (jj - 2 * NAP) / ASP < ARPT) {
+          const int j = ARPT * k + (jj - 2 * NAP) / ASP;
+          ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((t0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
+        }
+      }
       if constexpr (ACC == 1) {  // the MRF accumulator rows, RD steps before each row tile's epilogue
         // row tile j's epilogue starts at step (j + LG) NP of the last tap
         const int g = k * NST + jj, g0 = (K - 1) * NST + LG * NP - RD;
@@ -321,12 +342,14 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
     // vector of row tile j IS the B fragment of input plane w, and A = I maps its 8 channels onto the
     // accumulator rows that hold them (exact: products of 1 and bf16, fp32 accumulation)
     auto p2_extra = [&](int k, int j, int s) {
-      if (k != XT || s != 0) return;
+      if (s != 0) return;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
+        if (k == XT)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
         if constexpr (ACC == 2)
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ais[t], __builtin_bit_cast(bf16x8, ares[j]), acc[t][j], 0, 0, 0);
+          if (k == XA)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ais[t], __builtin_bit_cast(bf16x8, ares[j]), acc[t][j], 0, 0, 0);
       }
     };
     const float osc = a.out_scale;

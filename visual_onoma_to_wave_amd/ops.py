@@ -490,7 +490,8 @@ def resblock_pair(x, w1, b1, w2, b2, K, dil, slope=0.1, out=None, out_scale=1.0,
     if ev is not None:
         flops = 2.0 * 2.0 * B * T * C * C * K
         nbytes = 2.0 * x.numel() * 2 + (x.numel() * 2 if acc is not None else 0) + 2 * w1.numel() * 2
-        timer.stop(tag, ev, flops, nbytes, kernel=f"mrf_pair_kernel<C={C}, ...>")
+        name = "mrf_prw_kernel" if (C in (64, 128) and K in (7, 11)) else "mrf_pair_kernel"  # vo_pair_rw_try
+        timer.stop(tag, ev, flops, nbytes, kernel=f"{name}<C={C}, ...>")
     return out
 
 
