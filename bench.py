@@ -44,7 +44,7 @@ HOP = 256
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (no sparsity)
 F32_PEAK_TFLOPS = 157.3
-TRAFFIC_FILE = os.path.join("profiles", "traffic_r04.json")  # committed rocprofv3 PMC passes (tools/pmc_round.sh)
+TRAFFIC_FILE = os.path.join("profiles", "traffic_r05.json")  # committed rocprofv3 PMC passes (tools/pmc_round.sh)
 
 
 def parse():

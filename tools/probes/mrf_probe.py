@@ -27,7 +27,11 @@ def main():
             _lib.lib().vo_tune(b"pair_cfg", int(sys.argv[5]))
         w = [ops.pack_conv_weight(torch.randn(C, C, k, device="cuda", generator=g) / (C * k) ** 0.5, torch.bfloat16)
              for _ in range(2)]
-        fn = lambda: ops.resblock_pair(x, w[0], b, w[1], b, k, d, 0.1, out=y, out_scale=1 / 3, acc=y)  # noqa: E731
+        frag = C in (64, 128) and k in (7, 11) and os.environ.get("VO_FRAG", "1") != "0"  # as the Generator
+        if frag:
+            w = [ops.pack_frag(q) for q in w]
+        fn = lambda: ops.resblock_pair(x, w[0], b, w[1], b, k, d, 0.1, out=y, out_scale=1 / 3, acc=y,  # noqa: E731
+                                       frag=frag)
     elif kind == "conv":
         k, d = int(sys.argv[3]), int(sys.argv[4])
         if len(sys.argv) > 5:

@@ -155,11 +155,16 @@ __global__ void __launch_bounds__(256, 1) mrf_prw_kernel(PrwArgs a) {
   const int xr = tid / VPR, xc = tid % VPR;
   const int xl = (xc >> 2) * WP * 32 + rw_off(xr, xc & 3);  // + slot * RPS rows (swizzle unchanged)
   u32x4 xw[NWV];
+  // window rows c1 reads: R1 + (K - 1) dil of the R1 + 64 staged (the rest are never read: their loads
+  // are sent out of the buffer's range, which returns 0 without touching memory -- at d = 1 they were
+  // 17 % of the window's HBM reads)
+  const int wneed = R1 + (K - 1) * a.dil;
   auto load_win1 = [&](int tl, int sl) {
     const int b = tl / a.tiles_per_b;
     const int R0 = (tl - b * a.tiles_per_b) * BT - H2 - h1;
     // rows before 0 / past T are out of the utterance's range and read 0 (the conv's zero padding)
-    xw[sl] = __builtin_amdgcn_raw_buffer_load_b128(utt(a.x, b), ((R0 + xr + RPS * sl) * C + xc * 8) * 2, 0, 0);
+    const int off = xr + RPS * sl < wneed ? ((R0 + xr + RPS * sl) * C + xc * 8) * 2 : 0x7ffffff0;
+    xw[sl] = __builtin_amdgcn_raw_buffer_load_b128(utt(a.x, b), off, 0, 0);
   };
   auto store_win1 = [&](int sl) { *reinterpret_cast<u32x4*>(win + xl + sl * RPS * 32) = lrelu8(xw[sl], slope); };
 
