@@ -35,6 +35,10 @@ def main(path, marker="stft_mel_kernel", occ=6, steps=3):
             w.writerow([name, round(n / steps, 2), round(t / steps, 2), round(t / n, 3), round(100 * t / busy, 2)])
     print(f"{len(tail)} dispatches over {steps} steps: span {span / steps:.1f} us/step, kernels busy "
           f"{busy / steps:.1f} us/step -> {out}")
+    import json
+    with open(out.replace(".csv", ".json"), "w") as f:  # the tail's own clock, for reconciliation
+        json.dump({"steps": steps, "dispatches": len(tail), "span_us_per_step": round(span / steps, 1),
+                   "kernels_busy_us_per_step": round(busy / steps, 1)}, f, indent=1)
 
 
 if __name__ == "__main__":

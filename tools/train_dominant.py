@@ -27,12 +27,37 @@ def fam(rows, pred):
     return sum(r["UsPerStep"] for r in rows if pred(r["Name"]))
 
 
+def reconcile(src):
+    """The traced run's own clock: the tail's span per step (trace_tail_stats' JSON) and the bench line
+    the profiled run printed (its ms_per_step, with the profiler attached)."""
+    out = {}
+    side = src.replace(".csv", ".json")
+    if os.path.exists(side):
+        out.update(json.load(open(side)))
+    log = os.path.join(os.path.dirname(os.path.dirname(src)), os.path.basename(os.path.dirname(src)) + ".log")
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{"):
+                try:
+                    out["profiled_run_ms_per_step"] = json.loads(line)["ms_per_step"]
+                except (ValueError, KeyError):
+                    pass
+    return out
+
+
 def summary(rows, families, src):
     top = max(rows, key=lambda r: r["UsPerStep"])
     busy = sum(r["UsPerStep"] for r in rows)
     out = {"name": top["Name"], "avg_us": top["AvgUs"], "calls_per_step": top["CallsPerStep"],
            "share_of_step_kernel_time": round(top["UsPerStep"] / busy, 4), "kernel_us_per_step": round(busy, 1),
            "source": src, "families": {}}
+    rec = reconcile(src)
+    if rec:
+        # shares are of the traced step's kernel time; the traced step (profiler attached: serialized
+        # dispatches, per-dispatch overhead) is slower than the unprofiled bench line
+        out["trace_clock"] = rec
+        if rec.get("span_us_per_step"):
+            out["kernel_busy_over_span"] = round(busy / rec["span_us_per_step"], 4)
     for label, (pred, flops) in families.items():
         us = fam(rows, pred)
         out["families"][label] = {"us_per_step": round(us, 1), "flops_per_step": flops,
