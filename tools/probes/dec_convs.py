@@ -50,6 +50,26 @@ def main(cfgs):
             fl = 2.0 * B * T * ci * co * k
             line += f" | cfg {c}{same} {t:6.1f} us {fl / t / 1e6:6.0f} TF/s"
         L.vo_tune(b"gen_cfg", 0)
+        if k == 1:  # the library GEMM on the same operands (hipBLASLt through torch), for reference
+            x2, wt = x.reshape(-1, ci), torch.randn(ci, co, device="cuda").to(torch.bfloat16)
+            bb = b.to(odt)
+            if odt == torch.float32:
+                g = lambda: torch.addmm(bb, x2, wt, out_dtype=torch.float32)  # noqa: E731
+            else:
+                g = lambda: torch.addmm(bb, x2, wt)  # noqa: E731
+            g()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(5):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(20):
+                    g()
+                e.record()
+                torch.cuda.synchronize()
+                ts.append(s.elapsed_time(e) / 20 * 1e3)
+            t = sorted(ts)[2]
+            line += f" | torch.addmm {t:6.1f} us"
         print(line, flush=True)
 
 

@@ -763,6 +763,78 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
   return true;
 }
 
+// ------------------------------------------------------------------ K = 1 convs (Linear layers)
+// The transformer's fused q/k/v, fc and FFN w_2 are plain GEMMs over B*T = 16k rows with a
+// 256..1024-deep reduction (SubLayers.py:39-54,85-93).  conv1d_kernel stages one 32-channel chunk
+// per barrier with one chunk of prefetch; at 8..32 chunks that pipeline never fills (q/k/v: 21 us
+// for 33 MB, 1.6 TB/s).  Here each wave reads its own A (weight rows) and B (input rows) fragments
+// straight from L2 through a D-step register ring -- no LDS, no barriers; the waves of a workgroup
+// that share weight rows or input rows meet in L1.  Every accumulator sees the same MFMA sequence
+// as in conv1d_kernel (chunks in order, lane group q = channels 8q..8q+7, the same weight-row
+// permutation) and the same epilogue, so the outputs are bit-identical to it.
+// Measured and dropped (tools/probes/lin_probe.py, profiles/r05/lin_probe.txt): 1.3-2.2x SLOWER than
+// conv1d_kernel at every tile (q/k/v 23.0 us -> 30.8 at 128 x 128, 41.3 at 128 co x 64 rows) -- the
+// per-wave fragment loads (16 rows x 64 B per instruction) bind where the LDS tile shares them.
+// A/B library only (make abl; lin_cfg 2 / 3 / 4 / 5).
+#ifdef VO_ABLATIONS
+template <typename TOUT, int NI, int NJ, int WCO, int WT, int D, int NC>
+__global__ void __launch_bounds__(WCO * WT * 64) lin_kernel(ConvArgs a) {
+  // NC = Ci / 32 chunks, fully unrolled: straight-line code, so the compiler's vmcnt waits count
+  // exactly D - 1 chunks of loads in flight (a rolled loop got a near-drain wait at its back-edge)
+  constexpr int BCO = 16 * NI * WCO;
+  constexpr int BT = 16 * NJ * WT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wave_co0 = (wave % WCO) * 16 * NI;
+  const int wave_t0 = (wave / WCO) * 16 * NJ;
+  const int b = blockIdx.x / a.tiles_per_b;
+  const int t0 = (blockIdx.x - b * a.tiles_per_b) * BT;
+  const int co_blk = blockIdx.y * BCO;
+  const int lr = lane & 15, lq = lane >> 4;
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(a.w) + lq * 8;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x) + (int64_t)b * a.xbs + lq * 8;
+  const bf16_t* ap[NI];
+  const bf16_t* bp[NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) ap[i] = W + (int64_t)(co_blk + wave_co0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3)) * (NC * KC);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bp[j] = X + (int64_t)min(t0 + wave_t0 + 16 * j + lr, a.T_in - 1) * a.ldx;
+
+  Frag<bf16_t> af[D][NI], bfr[D][NJ];
+#pragma unroll
+  for (int d = 0; d < D && d < NC; ++d) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) af[d][i].load(ap[i] + d * KC);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bfr[d][j].load(bp[j] + d * KC);
+  }
+  // sched_barrier: keep every chunk's loads where they are written (hipcc otherwise sinks them next
+  // to their MFMAs -- fewer registers, no loads in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int d = c % D;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(af[d][i], bfr[d][j], acc[i][j]);
+    if (c + D < NC) {  // chunk c + D into the freed slot
+#pragma unroll
+      for (int i = 0; i < NI; ++i) af[d][i].load(ap[i] + (c + D) * KC);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[d][j].load(bp[j] + (c + D) * KC);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  conv_epilogue<TOUT, NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
+}
+#endif  // VO_ABLATIONS
+
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
@@ -830,6 +902,34 @@ static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL, RS, EJ>(d, st);
 }
 
+#ifdef VO_ABLATIONS
+// lin_kernel: K = 1, bf16 input and compute, Ci = 32 NC, Co % BCO == 0 (checked by the caller)
+template <typename TOUT, int NI, int NJ, int WCO, int WT, int D, int NC>
+static int launch_lin(const vo_conv1d_desc* d, hipStream_t st) {
+  constexpr int BCO = 16 * NI * WCO;
+  constexpr int BT = 16 * NJ * WT;
+  ConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = d->x; a.xbs = d->x_bstride; a.ldx = d->ldx;
+  a.w = d->w; a.bias = d->bias;
+  a.y = d->y; a.ybs = d->y_bstride; a.ldy = d->ldy;
+  a.res1 = d->res1; a.res2 = d->res2;
+  a.T_in = d->T_in; a.T_out = d->T_out; a.Ci = d->Ci; a.Co = d->Co;
+  a.K = 1; a.dil = 1; a.pad = 0;
+  a.pre_act = VO_ACT_NONE;
+  a.post_act = d->post_act; a.post_slope = d->post_slope; a.out_scale = d->out_scale;
+  a.tiles_per_b = (d->T_out + BT - 1) / BT;
+  a.co_tiles = d->Co / BCO;
+  a.B = d->B;
+  a.cig = d->Ci; a.cog = d->Co;
+  a.ymask = d->ymask; a.ymask_slope = d->ymask_slope;
+  auto kern = lin_kernel<TOUT, NI, NJ, WCO, WT, D, NC>;
+  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles);
+  hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), 0, st, a);
+  VO_RETURN_LAUNCH();
+}
+#endif  // VO_ABLATIONS
+
 // HiFi-GAN discriminator layers (strided and/or grouped, C5): 64-row tiles so that a stride-4
 // window ((64 - 1) * 4 + 1 + 40 rows) still double-buffers in LDS; output-channel tiles no
 // wider than a group where groups are narrow (block-diagonal weights: a tile spanning g
@@ -854,6 +954,19 @@ static int launch_disc(const vo_conv1d_desc* d, hipStream_t st) {
     default: vo_set_error("conv1d: stride %d unsupported (1..4, 8)", d->stride); return VO_ERR_INVALID;
   }
 }
+
+#ifdef VO_ABLATIONS
+// the lin_kernel tile for a launch; kLinSkip = Co fits no tile
+constexpr int kLinSkip = -1000;
+template <typename TOUT, int NC>
+static int lin_tile(const vo_conv1d_desc* d, hipStream_t st, int lc) {
+  if (lc == 2 && d->Co % 64 == 0) return launch_lin<TOUT, 2, 2, 2, 2, 4, NC>(d, st);
+  if (lc == 3 && d->Co % 128 == 0) return launch_lin<TOUT, 4, 4, 2, 2, 3, NC>(d, st);
+  if (lc == 4 && d->Co % 64 == 0) return launch_lin<TOUT, 2, 4, 2, 2, 4, NC>(d, st);
+  if (lc == 5 && d->Co % 128 == 0) return launch_lin<TOUT, 4, 2, 2, 2, 4, NC>(d, st);
+  return kLinSkip;
+}
+#endif  // VO_ABLATIONS
 
 template <typename TIN, typename TC, typename TOUT>
 static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
@@ -880,6 +993,21 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     return launch_cfg<TIN, TC, TOUT, 4, 4, 1, 4, 4>(d, st);  // 64 x 256
   }
   if (rows <= 2048) return launch_cfg<TIN, TC, TOUT, 2, 2, 2, 2, 2>(d, st);  // 64 x 64
+#ifdef VO_ABLATIONS
+  if constexpr (sizeof(TC) == 2 && sizeof(TIN) == 2) {
+    // K = 1 (Linear layers), A/B only: the LDS-free register-ring kernel, lin_cfg 2 / 3 / 4 / 5 =
+    // 64 x 64, 128 x 128, 64 co x 128 rows, 128 co x 64 rows (measured slower, see lin_kernel)
+    const int lc = vo_tune_get("lin_cfg");
+    if (lc >= 2 && d->K == 1 && d->pad == 0 && d->T_in == d->T_out && !d->transposed && d->variant == 0 &&
+        d->pre_act == VO_ACT_NONE && d->Ci % KC == 0 && d->x_bstride % 8 == 0) {
+      int rc = kLinSkip;
+      if (d->Ci == 256) rc = lin_tile<TOUT, 8>(d, st, lc);
+      if (d->Ci == 512) rc = lin_tile<TOUT, 16>(d, st, lc);
+      if (d->Ci == 1024) rc = lin_tile<TOUT, 32>(d, st, lc);
+      if (rc != kLinSkip) return rc;
+    }
+  }
+#endif
   if constexpr (sizeof(TC) == 2) {
     // decoder shapes at B*T = 16384 rows (tools/ab_sb.py gen): wide outputs (FFN w_1 k9 1024,
     // fused q/k/v 768) -> 256 x 256 tiles (-18 %); 1x1 convs to 256 channels -> 64 x 128
@@ -893,8 +1021,8 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       // (unless that leaves fewer than 128 workgroups: the MPD's joined period columns, ~4-5k rows x
       // 1024 channels, got 68-80 -- there the 128 x 128 tile below)
       const int64_t t256 = (int64_t)d->B * ((d->T_out + 255) / 256) * (d->Co / 256);
-      if (d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
-      if (d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
+      if (vo_tune_get("gen_cfg") != 11 && d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
+      if (vo_tune_get("gen_cfg") < 9 && d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
       // Co <= 256 k > 1 with fewer than 512 128 x 128 tiles (the C4 decoder's FFN w_1 input gradient, 1024 ->
       // 256 k9 at 16384 rows: 125 -> 106 us, tools/probes/dgrad_tiles.py): 64 x 128, twice the workgroups
       const int64_t t128 = (int64_t)d->B * ((d->T_out + 127) / 128) * ((d->Co + 127) / 128);
