@@ -1008,6 +1008,16 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     }
   }
 #endif
+#ifdef VO_ABLATIONS
+  if constexpr (sizeof(TC) == 2) {  // K = 1 staging A/B: one tap per step (TPS 1), weights by LDS-DMA (GL), role split (RS)
+    const int gq = vo_tune_get("gen_cfg");
+    if (gq == 13 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 1, 0, 0, 0, true, false>(d, st);
+    if (gq == 14 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 1, 0, 0, 0, true, true>(d, st);
+    if (gq == 15 && d->Co % 128 == 0) return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 1, 0, 0, 0, true, false>(d, st);
+    if (gq == 16 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 1>(d, st);
+    if (gq == 17) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 1>(d, st);  // 64 x 128, TPS 1
+  }
+#endif
   if constexpr (sizeof(TC) == 2) {
     // decoder shapes at B*T = 16384 rows (tools/ab_sb.py gen): wide outputs (FFN w_1 k9 1024,
     // fused q/k/v 768) -> 256 x 256 tiles (-18 %); 1x1 convs to 256 channels -> 64 x 128
