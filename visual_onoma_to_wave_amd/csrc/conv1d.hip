@@ -1132,6 +1132,9 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
         if (vo_tune_get("conv_cfg") == 2) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 3) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 2, 1, 1>(d, st);
         if (vo_tune_get("conv_cfg") == 4) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 3, 1, 1, 0, true>(d, st);
+        // one tap per step (k = 3's second 2-tap step re-fetches tap 2 as its padding tap)
+        if (vo_tune_get("conv_cfg") == 7) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 1, 1, 1, 0, true>(d, st);
+        if (vo_tune_get("conv_cfg") == 8) return launch_cfg<bf16_t, bf16_t, bf16_t, 4, 8, 4, 2, 1, 1, 1, 0, true, true>(d, st);
 #endif
         // Round 2: role-split staging (RS: half the waves issue the weight DMA, half copy the window by
         // LDS-DMA two chunks ahead; bare step barriers): k = 7 / 11 0.137 / 0.175 -> 0.130 / 0.168 ms,
