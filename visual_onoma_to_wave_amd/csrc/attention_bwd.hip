@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(256) attn2_bwd_dkdv_kernel(const bf16_t* __res
                                                              int xcd) {
   constexpr int P = AB2_P, QT = 64;
   __shared__ __attribute__((aligned(16))) bf16_t qd_lds[2][2][QT * P];  // [buf][Q | dO][query][dk]
-  __shared__ float ld_s[2][2][QT];                                      // [buf][lse | D][query]
+  __shared__ __attribute__((aligned(16))) float ld_s[2][2][QT];        // [buf][lse | D][query]
   const int D = H * AB_DK;
   const int nk = gridDim.x, wid = blockIdx.x + nk * blockIdx.y;
   const int lid = xcd ? xcd_grouped_id(wid, nk * gridDim.y) : wid;
@@ -600,16 +600,23 @@ __global__ void __launch_bounds__(256) attn2_bwd_dkdv_kernel(const bf16_t* __res
           dp[nt] = mfma(df, vf[ks], dp[nt]);
         }
       }
-      // P = exp(S * scale - lse[q]), dS = P o (dP - D[q]): lane's query 16 nt + 4 g + r, key lr
+      // P = exp(S * scale - lse[q]), dS = P o (dP - D[q]): lane's query 16 nt + 4 g + r, key lr.  The
+      // lane's four lse / D values per nt come as one 16-byte LDS read each and every exp is computed
+      // before the padded-key select: `kok ? exp(.. ld_s ..) : 0` became a branch per element with its
+      // own LDS read and lgkmcnt(0) wait -- 16 serialised LDS round trips per query tile
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 4; ++nt) {
+        const float4 lv = *reinterpret_cast<const float4*>(&ld_s[buf][0][16 * nt + 4 * g]);
+        const float4 dv4 = *reinterpret_cast<const float4*>(&ld_s[buf][1][16 * nt + 4 * g]);
+        const float lq4[4] = {lv.x, lv.y, lv.z, lv.w}, dq4[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int qq = 16 * nt + 4 * g + r;
-          const float p = kok ? __expf(sc[nt][r] * scale - ld_s[buf][0][qq]) : 0.f;
+          const float e = __expf(sc[nt][r] * scale - lq4[r]);
+          const float p = kok ? e : 0.f;
           sc[nt][r] = p;
-          dp[nt][r] = p * (dp[nt][r] - ld_s[buf][1][qq]);
+          dp[nt][r] = p * (dp[nt][r] - dq4[r]);
         }
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const Frag<bf16_t> pf = ab_acc_frag(sc[2 * ks], sc[2 * ks + 1]);
