@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lens", default="full", choices=["full", "ragged"])
     ap.add_argument("--n", type=int, default=20)
+    ap.add_argument("--att-cfg", default="0", help="comma list of att_cfg values, timed alternately (A/B)")
     a = ap.parse_args()
     B, L, D, H = 32, 512, 256, 2
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -34,21 +35,33 @@ def main():
     dq = ops.attention_bwd(qkv, out, dout, lens, H, lse=lse)
     torch.cuda.synchronize()
     assert torch.isfinite(dq.float()).all()
-    ts = []
+    from visual_onoma_to_wave_amd import _lib
+    cfgs = [int(c) for c in a.att_cfg.split(",")]
+    ts = {c: [] for c in cfgs}
+    ref = None
     for _ in range(5):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(a.n):
-            ops.attention_bwd(qkv, out, dout, lens, H, lse=lse)
-        e.record()
-        torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e) / a.n * 1e3)
-    t = sorted(ts)[2]
+        for c in cfgs:
+            _lib.lib().vo_tune(b"att_cfg", c)
+            got = ops.attention_bwd(qkv, out, dout, lens, H, lse=lse)
+            if ref is None:
+                ref = got.clone()
+            elif not torch.equal(got, ref):
+                print(f"att_cfg {c}: DIFFERS from att_cfg {cfgs[0]}", flush=True)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.n):
+                ops.attention_bwd(qkv, out, dout, lens, H, lse=lse)
+            e.record()
+            torch.cuda.synchronize()
+            ts[c].append(s.elapsed_time(e) / a.n * 1e3)
+    _lib.lib().vo_tune(b"att_cfg", 0)
     dk = D // H
     fl = 5 * 2.0 * B * H * L * L * dk
     fl_live = 5 * 2.0 * H * dk * float((lens.double() ** 2).sum())
-    print(f"attention bwd (lens {a.lens}): {t:.1f} us per call, {fl / t / 1e6:.0f} TF/s on full-L FLOPs "
-          f"({fl / t / 1e6 / PEAK * 1e12:.3f} of peak), {fl_live / t / 1e6:.0f} TF/s on live FLOPs", flush=True)
+    for c in cfgs:
+        t = sorted(ts[c])[2]
+        print(f"attention bwd (lens {a.lens}, att_cfg {c}): {t:.1f} us per call, {fl / t / 1e6:.0f} TF/s on full-L "
+              f"FLOPs ({fl / t / 1e6 / PEAK * 1e12:.3f} of peak), {fl_live / t / 1e6:.0f} TF/s on live FLOPs", flush=True)
 
 
 if __name__ == "__main__":

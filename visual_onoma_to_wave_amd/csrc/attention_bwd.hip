@@ -505,7 +505,7 @@ __global__ void __launch_bounds__(256) attn2_bwd_dq_kernel(const bf16_t* __restr
         make_uint2(pk_bf16(dq[dt][0] * scale, dq[dt][1] * scale), pk_bf16(dq[dt][2] * scale, dq[dt][3] * scale));
 }
 
-template <int NONE = 0>
+template <int V = 0>  // V = 2: the per-element lse / D reads under the padded-key branch (A/B, att_cfg 2)
 __global__ void __launch_bounds__(256) attn2_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
                                                              const bf16_t* __restrict__ dout,
                                                              const int32_t* __restrict__ lens, int L, int H,
@@ -604,8 +604,19 @@ __global__ void __launch_bounds__(256) attn2_bwd_dkdv_kernel(const bf16_t* __res
       // lane's four lse / D values per nt come as one 16-byte LDS read each and every exp is computed
       // before the padded-key select: `kok ? exp(.. ld_s ..) : 0` became a branch per element with its
       // own LDS read and lgkmcnt(0) wait -- 16 serialised LDS round trips per query tile
+      if constexpr (V == 2) {
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qq = 16 * nt + 4 * g + r;
+            const float p = kok ? __expf(sc[nt][r] * scale - ld_s[buf][0][qq]) : 0.f;
+            sc[nt][r] = p;
+            dp[nt][r] = p * (dp[nt][r] - ld_s[buf][1][qq]);
+          }
+      }
+#pragma unroll
+      for (int nt = 0; nt < (V == 2 ? 0 : 4); ++nt) {
         const float4 lv = *reinterpret_cast<const float4*>(&ld_s[buf][0][16 * nt + 4 * g]);
         const float4 dv4 = *reinterpret_cast<const float4*>(&ld_s[buf][1][16 * nt + 4 * g]);
         const float lq4[4] = {lv.x, lv.y, lv.z, lv.w}, dq4[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
@@ -695,7 +706,8 @@ extern "C" int vo_attention_bwd_lse(const void* qkv, const void* out, const void
   const int xcd = vo_tune_get("att_xcd") != 1;
   hipLaunchKernelGGL(attn2_bwd_dq_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)out,
                      (const bf16_t*)dout, lens, L, H, scale, lse, (bf16_t*)dqkv, dd, xcd);
-  hipLaunchKernelGGL(attn2_bwd_dkdv_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lens,
+  auto dkdv = vo_tune_get("att_cfg") == 2 ? attn2_bwd_dkdv_kernel<2> : attn2_bwd_dkdv_kernel<0>;
+  hipLaunchKernelGGL(dkdv, grid, dim3(256), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lens,
                      L, H, scale, lse, (const float*)dd, (bf16_t*)dqkv, xcd);
   VO_RETURN_LAUNCH();
 }
