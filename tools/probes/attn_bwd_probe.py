@@ -55,6 +55,18 @@ def main():
             torch.cuda.synchronize()
             ts[c].append(s.elapsed_time(e) / a.n * 1e3)
     _lib.lib().vo_tune(b"att_cfg", 0)
+    fw = []
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.n):
+            ops.attention(qkv, lens, H, out=out, with_lse=True)
+        e.record()
+        torch.cuda.synchronize()
+        fw.append(s.elapsed_time(e) / a.n * 1e3)
+    tf = sorted(fw)[2]
+    print(f"attention fwd (lens {a.lens}): {tf:.1f} us per call, "
+          f"{2 * 2.0 * B * H * L * L * (D // H) / tf / 1e6:.0f} TF/s on full-L FLOPs", flush=True)
     dk = D // H
     fl = 5 * 2.0 * B * H * L * L * dk
     fl_live = 5 * 2.0 * H * dk * float((lens.double() ** 2).sum())
