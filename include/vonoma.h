@@ -139,7 +139,8 @@ int vo_layernorm(const void* x, int x_dtype, const void* res, int res_dtype, con
 /* vo_layernorm with an fp32 y and, in the same pass, its bf16 copy y16 (round to nearest even;
  * pad rows 0 in both).  The mixed-precision decoder keeps its residual stream (y) in fp32, as the
  * reference's bf16 autocast does, while the next conv reads y16 -- the same bits that conv's own
- * fp32 -> bf16 staging would make, at half the bytes.  x / res: both fp32 or both bf16. */
+ * fp32 -> bf16 staging would make, at half the bytes.  x / res: both fp32, both bf16, or (round 6,
+ * the training decoder: bf16 sublayer output + fp32 residual stream) bf16 x with fp32 res. */
 int vo_layernorm_dual(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
                       const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
                       void* y16, void* stream);
@@ -154,6 +155,15 @@ int64_t vo_layernorm_bwd_workspace_size(int B, int T, int D);
 int vo_layernorm_bwd(const void* x, const void* res, int x_dtype, const void* gy, int gy_dtype,
                      const float* gamma, const int32_t* lens, int B, int T, int D, float eps, void* gh,
                      float* dgamma, float* dbeta, void* workspace, void* stream);
+
+/* vo_layernorm_bwd for the backward of vo_layernorm_dual (round 6, mixed-precision training): res may be
+ * fp32 beside a bf16 x (res_dtype), gy2 (bf16, may be NULL) is a second incoming gradient -- that of
+ * y16 -- added to gy, and gh32 (may be NULL) receives the fp32 gradient of res beside gh (x_dtype).
+ * Combinations: bf16 x + fp32 res with fp32 or bf16 gy; or x_dtype == res_dtype with gy2 = gh32 = NULL
+ * (then exactly vo_layernorm_bwd).  Same workspace. */
+int vo_layernorm_bwd_ex(const void* x, int x_dtype, const void* res, int res_dtype, const void* gy, int gy_dtype,
+                        const void* gy2, const float* gamma, const int32_t* lens, int B, int T, int D, float eps,
+                        void* gh, float* gh32, float* dgamma, float* dbeta, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------ attention
  * Scaled dot-product attention with key padding, H heads of d_k = D/H, over the fused

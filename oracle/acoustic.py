@@ -239,9 +239,10 @@ def vtts_forward(sd, audiotypes, texts, src_lens, max_src_len, mels=None, mel_le
                  d_control=1.0, energy_stats=None, training=False, bf16_back=False):
     """vTTS.forward, scripts/model/vtts.py:47-119 -> the reference's 10-tuple.
 
-    ``bf16_back``: the decoder, mel_linear and PostNet under CPU bf16 autocast -- the reference's
-    own arithmetic at the precision split of the HIP path's "mixed" mode; its distance from the
-    fp32 result is the bf16 tolerance bar of the parity tests."""
+    ``bf16_back``: the decoder, mel_linear and PostNet at bf16 -- the reference's own arithmetic at the
+    precision split of the HIP path's "mixed" mode; its distance from the fp32 result is the bf16
+    tolerance bar of the parity tests.  True / "autocast": CPU bf16 autocast; "operands": bf16 operands
+    of every contraction, fp32 accumulation and fp32 everywhere else (oracle/bf16.py)."""
     assert use_image, "only the visual-text input path is on the hot path"
     src_masks = mask_from_lengths(src_lens, max_src_len)
     mel_masks = mask_from_lengths(mel_lens, max_mel_len) if mels is not None else None
@@ -250,7 +251,13 @@ def vtts_forward(sd, audiotypes, texts, src_lens, max_src_len, mels=None, mel_le
     x, e_pred, log_d, d_rounded, mel_lens_o, mel_masks, _, _ = variance_adaptor(
         sd, x, src_masks, mel_masks, max_mel_len, e_targets, d_targets, e_control, d_control,
         energy_stats)
-    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=bf16_back):
+    import contextlib
+    import sys
+
+    from .bf16 import bf16_operands
+    ctx = (bf16_operands(sys.modules[__name__]) if bf16_back == "operands" else
+           torch.autocast("cpu", dtype=torch.bfloat16, enabled=bool(bf16_back)) if bf16_back else contextlib.nullcontext())
+    with ctx:
         x, mel_masks = decoder(sd, x, mel_masks, training=training)
         mel = linear(x, sd, "mel_linear")
         post = postnet(sd, mel, training=training) + mel

@@ -12,7 +12,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import hifigan_arrays, hifigan_h, rel_l2
+from helpers import bf16_bar, bf16_grad_check, hifigan_arrays, hifigan_h, rel_l2
 from weights import load_into
 
 pytestmark = pytest.mark.gpu
@@ -201,23 +201,13 @@ def _module_leaves(m):
     return [m.weight_v, m.weight_g] if hasattr(m, "weight_g") else [m.weight_orig]
 
 
-def test_gan_step_gradients_vs_oracle():
-    """L_D and L_G of one HiFi-GAN step and their gradients wrt every G and D parameter, HIP
-    autograd (fp32 compute) vs the CPU oracle's autograd, on the same weights and batch."""
+def _oracle_gan_step(g, dmods, mel, y, bf16):
+    """One HiFi-GAN step on the CPU oracle over leaf copies of the G and D parameters: (L_D, dL_D
+    per D leaf, L_G, dL_G per G parameter name).  bf16 ("autocast" / "operands", oracle/bf16.py): the
+    reference arithmetic of G and D at bf16 (scores, feature maps and the generated waveform cast back
+    to fp32 before the losses and the training mel, as the HIP path keeps them)."""
     from oracle import gan as O
     from oracle import vocoder as V
-    from visual_onoma_to_wave_amd.hifigan.discriminators import (MelLoss, MultiPeriodDiscriminator,
-                                                                  MultiScaleDiscriminator, discriminator_loss,
-                                                                  feature_loss, generator_loss)
-    from visual_onoma_to_wave_amd.hifigan.train import _single
-    torch.manual_seed(1)
-    B = 2
-    mel = torch.randn(B, 80, 32) - 4.0
-    y = torch.tanh(torch.randn(B, 8192) * 0.3)
-    g = _gen("cpu")
-    mpd, msd = MultiPeriodDiscriminator().eval(), MultiScaleDiscriminator().eval()
-    dmods = [m for d in list(mpd.discriminators) + list(msd.discriminators) for m in list(d.convs) + [d.conv_post]]
-    # ---- oracle on CPU leaf copies, fp32 autograd
     gp = {k: v.detach().clone().requires_grad_(True) for k, v in g.state_dict().items()}
     leaves, effs = [], []
     for m in dmods:
@@ -234,34 +224,82 @@ def test_gan_step_gradients_vs_oracle():
             i += n
         return out[:5], out[5:]
 
+    def ac():
+        if bf16 == "operands":
+            from oracle.bf16 import bf16_operands
+            return bf16_operands(O, V)
+        return torch.autocast("cpu", dtype=torch.bfloat16, enabled=bool(bf16))
+
+    def f32(o):
+        return [s.float() for s in o[0]], [[t.float() for t in f] for f in o[1]]
+
     h = hifigan_h()
-    yh_ref = V.generator(V.fold_weight_norm(gp), mel, h)[:, 0]
+    with ac():
+        yh_ref = V.generator(V.fold_weight_norm(gp), mel, h)[:, 0].float()
     y_mel = O.mel_spectrogram(y)
     mp, sp = params()
-    ld_ref = O.discriminator_loss(O.mpd(mp, y)[0], O.mpd(mp, yh_ref.detach())[0]) + \
-        O.discriminator_loss(O.msd(sp, y)[0], O.msd(sp, yh_ref.detach())[0])
-    dl_flat = [t for lv in leaves for t in lv] + dbias
-    gd_ref = torch.autograd.grad(ld_ref, dl_flat)
+    with ac():
+        r1, g1 = f32(O.mpd(mp, y)), f32(O.mpd(mp, yh_ref.detach()))
+        r2, g2 = f32(O.msd(sp, y)), f32(O.msd(sp, yh_ref.detach()))
+    ld = O.discriminator_loss(r1[0], g1[0]) + O.discriminator_loss(r2[0], g2[0])
+    gd = torch.autograd.grad(ld, [t for lv in leaves for t in lv] + dbias)
     mp, sp = params()
-    _, lg_ref, _ = O.gan_losses(mp, sp, y, yh_ref, y_mel)
-    gg_ref = torch.autograd.grad(lg_ref, [gp[k] for k in gp])
-    # ---- HIP path, fp32 compute (D in eval: spectral norm without power iteration)
-    g = g.cuda().set_compute_dtype(torch.float32)
+    with ac():
+        fr1, fg1 = f32(O.mpd(mp, y)), f32(O.mpd(mp, yh_ref))
+        fr2, fg2 = f32(O.msd(sp, y)), f32(O.msd(sp, yh_ref))
+    lg = (O.generator_loss(fg1[0]) + O.generator_loss(fg2[0]) + O.feature_loss(fr1[1], fg1[1])
+          + O.feature_loss(fr2[1], fg2[1]) + torch.nn.functional.l1_loss(y_mel, O.mel_spectrogram(yh_ref)) * 45)
+    gg = torch.autograd.grad(lg, [gp[k] for k in gp])
+    return float(ld), gd, float(lg), dict(zip(gp, gg)), yh_ref.detach()
+
+
+def _gan_setup(converged=True):
+    torch.manual_seed(1)
+    B = 2
+    mel = torch.randn(B, 80, 32) - 4.0
+    y = torch.tanh(torch.randn(B, 8192) * 0.3)
+    from visual_onoma_to_wave_amd.hifigan.discriminators import MultiPeriodDiscriminator, MultiScaleDiscriminator
+    g = _gen("cpu")
+    mpd, msd = MultiPeriodDiscriminator().eval(), MultiScaleDiscriminator().eval()
+    # the spectral-normed convs' (u, v) as training leaves them (power iteration converged), not as
+    # constructed: with the random initial pair the eval-mode sigma is a small fraction of the true one
+    # and the first scale's scores run to ~1e11 (losses ~1e22) -- a regime no training step sees.
+    # (converged=False: the constructed pair, where the fp32 comparison's 2e-3 was set; in the converged
+    # regime a few fp32 L1 sign flips of the feature-matching / mel terms move one G gradient to 2.2e-3)
+    with torch.no_grad():
+        for m in msd.modules() if converged else ():
+            if hasattr(m, "weight_u"):
+                W = m.weight_orig.reshape(m.weight_orig.shape[0], -1)
+                u, v = m.weight_u.clone(), m.weight_v.clone()
+                for _ in range(50):
+                    v = F.normalize(W.t() @ u, dim=0, eps=1e-12)
+                    u = F.normalize(W @ v, dim=0, eps=1e-12)
+                m.weight_u.copy_(u)
+                m.weight_v.copy_(v)
+    return g, mpd, msd, mel, y
+
+
+def _dmods(mpd, msd):
+    return [m for d in list(mpd.discriminators) + list(msd.discriminators) for m in list(d.convs) + [d.conv_post]]
+
+
+def _hip_gan_step(g, mpd, msd, mel, y, dt):
+    """The same step on the HIP path (compute dtype dt; D in eval: spectral norm without power
+    iteration): (L_D, dL_D per D leaf, L_G, {G parameter: dL_G}, generated waveform)."""
+    from visual_onoma_to_wave_amd.hifigan.discriminators import (MelLoss, discriminator_loss, feature_loss,
+                                                                  generator_loss)
+    from visual_onoma_to_wave_amd.hifigan.train import _single
+    g = g.cuda().set_compute_dtype(dt)
     g.train()
-    mpd, msd = mpd.cuda().set_compute_dtype(torch.float32), msd.cuda().set_compute_dtype(torch.float32)
-    dmods = [m for d in list(mpd.discriminators) + list(msd.discriminators) for m in list(d.convs) + [d.conv_post]]
+    mpd, msd = mpd.cuda().set_compute_dtype(dt), msd.cuda().set_compute_dtype(dt)
+    dmods = _dmods(mpd, msd)
     mloss = MelLoss().cuda()
     yc = y.cuda()
     yh = g.train_forward(mel.transpose(1, 2).contiguous().cuda())
-    assert rel_l2(yh.detach().cpu(), yh_ref.detach()) < 1e-4
     r1, g1, _, _ = mpd(yc, yh.detach())
     r2, g2, _, _ = msd(yc, yh.detach())
     ld = discriminator_loss(r1, g1)[0] + discriminator_loss(r2, g2)[0]
-    assert abs(float(ld) - float(ld_ref)) < 1e-4 * abs(float(ld_ref))
     gd = torch.autograd.grad(ld, [t for m in dmods for t in _module_leaves(m)] + [m.bias for m in dmods])
-    assert len(gd) == len(gd_ref)
-    for i, (a, r) in enumerate(zip(gd, gd_ref)):
-        assert rel_l2(a.cpu(), r) < 2e-3, (i, rel_l2(a.cpu(), r))
     # generator step (D frozen, real features without graph)
     with torch.no_grad():
         y_mel_c = mloss.mel(yc)
@@ -274,12 +312,50 @@ def test_gan_step_gradients_vs_oracle():
     sg_s, fg_s = _single(msd, yh, True)
     lg = (generator_loss(sg_f)[0] + generator_loss(sg_s)[0] + feature_loss(fr_f, fg_f) + feature_loss(fr_s, fg_s)
           + loss_mel)
-    assert abs(float(lg) - float(lg_ref)) < 1e-4 * abs(float(lg_ref))
-    names = list(gp)
     named = dict(g.named_parameters())
+    names = list(named)
     gg = torch.autograd.grad(lg, [named[k] for k in names])
-    for k, a, r in zip(names, gg, gg_ref):
-        assert rel_l2(a.cpu(), r) < 2e-3, (k, rel_l2(a.cpu(), r))
+    return (float(ld), [t.float().cpu() for t in gd], float(lg), {k: t.float().cpu() for k, t in zip(names, gg)},
+            yh.detach().float().cpu())
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_gan_step_gradients_vs_oracle(mode):
+    """L_D and L_G of one HiFi-GAN step and their gradients wrt every G and D parameter, HIP
+    autograd vs the CPU oracle's fp32 autograd, on the same weights and batch.
+    fp32 compute: rel-L2 <= 2e-3 per gradient (1e-4 on the losses and the waveform).  bf16 compute (the
+    bench's C5 precision): waveform and losses within max(1e-2, the oracle's own bf16 drift on them),
+    the gradients at helpers.bf16_grad_check's bar (the oracle's bf16 arithmetics, autocast and bf16
+    operands, on the same step)."""
+    bf16 = mode == "bf16"
+    g, mpd, msd, mel, y = _gan_setup(converged=bf16)
+    dmods = _dmods(mpd, msd)
+    torch.set_num_threads(16)
+    ld_ref, gd_ref, lg_ref, gg_ref, yh_ref = _oracle_gan_step(g, dmods, mel, y, False)
+    bfs = [_oracle_gan_step(g, dmods, mel, y, m) for m in ("autocast", "operands")] if bf16 else []
+    ld, gd, lg, gg, yh = _hip_gan_step(g, mpd, msd, mel, y, torch.bfloat16 if bf16 else torch.float32)
+    if not bf16:
+        assert rel_l2(yh, yh_ref) < 1e-4
+        assert abs(ld - ld_ref) < 1e-4 * abs(ld_ref) and abs(lg - lg_ref) < 1e-4 * abs(lg_ref)
+        for i, (a, r) in enumerate(zip(gd, gd_ref)):
+            assert rel_l2(a, r) < 2e-3, ("D", i, rel_l2(a, r))
+        for k, r in gg_ref.items():
+            assert rel_l2(gg[k], r) < 2e-3, ("G", k, rel_l2(gg[k], r))
+        return
+    e, bar = rel_l2(yh, yh_ref), max(bf16_bar(yh_ref, b[4]) for b in bfs)
+    print(f"waveform {e:.2e} (bar {bar:.2e})")
+    assert e <= bar
+    for name, got, ref, j in (("L_D", ld, ld_ref, 0), ("L_G", lg, lg_ref, 2)):
+        drift = max(abs(b[j] - ref) for b in bfs)
+        assert abs(got - ref) <= max(1e-2 * abs(ref), drift), (name, got, ref, drift)
+    for name, got, ref, j in (("D", dict(enumerate(gd)), dict(enumerate(gd_ref)), 1), ("G", gg, gg_ref, 3)):
+        bf = [dict(enumerate(b[j])) if j == 1 else b[j] for b in bfs]
+        # every G gradient flows through the sign of the mel / feature-matching L1 terms; D's through the
+        # squared discriminator loss only
+        rows, (n, n_noise, rms_e, rms_d) = bf16_grad_check(got, ref, bf, discontinuous=name == "G")
+        rows.sort(reverse=True)
+        print(f"{name}: {n} gradients; noise-dominated group of {n_noise}: RMS error {rms_e:.3e} vs the oracle's "
+              f"bf16 drift {rms_d:.3e}; worst rows {[(round(r[0], 3), r[1]) for r in rows[:4]]}")
 
 
 def test_trainer_step_bf16():

@@ -226,10 +226,13 @@ def test_capturable_lr_survives_load_state_dict():
             fl.step()
 
 
-def test_step_captured_before_load_state_dict_follows_it():
+@pytest.mark.parametrize("missing", [False, True])
+def test_step_captured_before_load_state_dict_follows_it(missing):
     """A step captured BEFORE load_state_dict: the load copies the step count and the moments into the
     device tensors the graph reads and writes (as it does the learning rate), so the replay continues
-    from the loaded state exactly as an eager optimizer that loaded the same state."""
+    from the loaded state exactly as an eager optimizer that loaded the same state.  missing: the
+    loaded state has no moments for one parameter (it never had a gradient there) -- the moments the
+    graph reads are zeroed and stay in the state, as the eager optimizer starts that one from zeros."""
     from visual_onoma_to_wave_amd.optim import FusedAdam
     init = _params(5, 4)
     grads = [[g.cuda() for g in gs] for gs in _grads(7, init, 3)]
@@ -249,10 +252,11 @@ def test_step_captured_before_load_state_dict_follows_it():
     src = [torch.nn.Parameter(p.clone().cuda()) for p in init]
     other = torch.optim.Adam(src, lr=2e-3)
     for gs in grads:
-        for p, g in zip(src, gs):
-            p.grad = g.clone() * 0.5
+        for i, (p, g) in enumerate(zip(src, gs)):
+            p.grad = None if (missing and i == 2) else g.clone() * 0.5
         other.step()
     sd = other.state_dict()
+    assert (2 in sd["state"]) != missing
     opt.load_state_dict(sd)
     with torch.no_grad():
         for p, q in zip(ps, src):
@@ -269,6 +273,8 @@ def test_step_captured_before_load_state_dict_follows_it():
     for a, b in zip(ps, eager):
         assert torch.equal(a.detach(), b.detach())
     assert float(opt.state[ps[0]]["step"]) == 4.0
+    if missing:
+        assert "exp_avg" in opt.state[ps[2]]
 
 
 def test_load_state_dict_refuses_unequal_steps():

@@ -247,6 +247,43 @@ def test_layernorm_bwd_vs_torch(B, T, D, dt, with_res, with_lens):
     assert rel_l2(dg.cpu(), rg) < 1e-5 and rel_l2(db.cpu(), rb) < 1e-5
 
 
+@pytest.mark.parametrize("B,T,D,with_lens", [(3, 37, 256, True), (32, 512, 256, True), (2, 5, 512, False)])
+@pytest.mark.parametrize("use", ["both", "copy"])
+def test_layernorm_dual_train_vs_torch(B, T, D, with_lens, use):
+    """autograd.layernorm_dual (the mixed training decoder's LayerNorm: bf16 sublayer output x, fp32
+    residual stream res -> fp32 y and its bf16 copy y16) vs the fp32 autograd of LayerNorm(x + res) +
+    pad-row masked_fill; the two incoming gradients (y's and y16's) summed in the backward kernel.
+    use = "copy": only y16 is read downstream (the last decoder layer)."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import autograd as AG
+    gen = torch.Generator().manual_seed(B * T + D)
+    x = torch.randn(B, T, D, generator=gen).to(torch.bfloat16)
+    res = torch.randn(B, T, D, generator=gen)
+    g = 1.0 + 0.1 * torch.randn(D, generator=gen)
+    bta = 0.1 * torch.randn(D, generator=gen)
+    lens = torch.randint(1, T + 1, (B,), generator=gen).int() if with_lens else None
+    gy = torch.randn(B, T, D, generator=gen)
+    gy16 = torch.randn(B, T, D, generator=gen).to(torch.bfloat16)
+    xi, ri = x.float().requires_grad_(True), res.clone().requires_grad_(True)
+    gi, bi = g.clone().requires_grad_(True), bta.clone().requires_grad_(True)
+    y = F.layer_norm(xi + ri, (D,), gi, bi, 1e-5)
+    if with_lens:
+        y = y.masked_fill((torch.arange(T)[None, :] >= lens.long()[:, None])[..., None], 0.0)
+    gtot = gy16.float() + (gy if use == "both" else 0.0)
+    rx, rr, rg, rb = torch.autograd.grad(y, (xi, ri, gi, bi), gtot)
+    xc, rc = x.cuda().requires_grad_(True), res.cuda().requires_grad_(True)
+    gc, bc = g.cuda().requires_grad_(True), bta.cuda().requires_grad_(True)
+    y32, y16 = AG.layernorm_dual(xc, rc, gc, bc, lens.cuda() if with_lens else None)
+    assert y32.dtype == torch.float32 and y16.dtype == torch.bfloat16
+    assert rel_l2(y32.detach().cpu(), y.detach()) < 1e-6
+    assert torch.equal(y16.detach(), y32.detach().to(torch.bfloat16))
+    outs, grads = ((y32, y16), (gy.cuda(), gy16.cuda())) if use == "both" else ((y16,), (gy16.cuda(),))
+    dx, dr, dg, db = torch.autograd.grad(outs, (xc, rc, gc, bc), grads)
+    assert dx.dtype == torch.bfloat16 and dr.dtype == torch.float32
+    assert rel_l2(dr.cpu(), rr) < 1e-5 and rel_l2(dx.float().cpu(), rx) < 1e-2
+    assert rel_l2(dg.cpu(), rg) < 1e-5 and rel_l2(db.cpu(), rb) < 1e-5
+
+
 def _torch_attention(qkv, lens, n_head):
     """fp32 reference of vo_attention: head split of SubLayers.py:39-46, SDPA of Modules.py:14-25
     with the key-padding mask of Models.py:104 / 187."""

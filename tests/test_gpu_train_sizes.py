@@ -15,6 +15,7 @@ Parity of the HiFi-GAN training side is unpinned (the reference has no training 
 """
 
 import os
+import re
 import socket
 
 import numpy as np
@@ -22,7 +23,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from helpers import configs, hifigan_arrays, hifigan_h, rel_l2, stats, vtts_arrays
+from helpers import bf16_grad_check, configs, hifigan_arrays, hifigan_h, rel_l2, stats, vtts_arrays
 from weights import load_into
 
 pytestmark = pytest.mark.gpu
@@ -91,6 +92,81 @@ def test_c4_step_full_size_vs_oracle(device):
             bad.append((k, err, float(gr.norm())))
     assert not bad, bad[:10]
     assert len(set(subset)) > 50
+
+
+def _c4_oracle(arrays, bc, bf16_back):
+    """(six loss values, {parameter: gradient}) of one oracle step on the CPU; bf16_back: the decoder,
+    mel_linear and PostNet under CPU bf16 autocast (the precision split of the HIP "mixed" mode)."""
+    from oracle import acoustic as A
+    from oracle import training as TR
+    sd = A.complete_state_dict(arrays, stats()["energy"])
+    for k, v in sd.items():
+        if v.dtype == torch.float32 and "position_enc" not in k and "bins" not in k and "running" not in k:
+            v.requires_grad_(True)
+    ro = A.vtts_forward(sd, *bc[1:12], energy_stats=stats()["energy"], training=True, bf16_back=bf16_back)
+    ref = TR.fastspeech2_loss(bc, ro)
+    ref[0].backward()
+    return [float(x) for x in ref], {k: v.grad for k, v in sd.items() if v.grad is not None}
+
+
+# gradients that are exactly zero in exact arithmetic (rounding noise on every side), with the sibling
+# whose gradient sets their scale: conv biases feeding a train-mode BatchNorm (its beta), and the key
+# projection's bias (softmax is invariant to a per-query constant: the query bias of the same layer)
+_STRUCTURAL_ZEROS = [(re.compile(r"(.*VisualFeatureExtractor\.embedder\.)([036])\.bias$"),
+                      lambda m: f"{m.group(1)}{int(m.group(2)) + 1}.bias"),
+                     (re.compile(r"(postnet\.convolutions\.\d+\.)0\.conv\.bias$"), lambda m: f"{m.group(1)}1.bias"),
+                     (re.compile(r"(.*slf_attn\.)w_ks\.bias$"), lambda m: f"{m.group(1)}w_qs.bias")]
+
+
+def _zero_sibling(k):
+    for rx, fn in _STRUCTURAL_ZEROS:
+        m = rx.match(k)
+        if m:
+            return fn(m)
+    return None
+
+
+def test_c4_step_mixed_full_size_vs_oracle(device):
+    """The bench's C4 precision ("mixed": encoder and variance adaptor fp32, decoder / mel_linear /
+    PostNet bf16 -- attention backward v2, step-batched packs, vectorised BatchNorm all on this path)
+    at B = 32, T_src = 12, T_mel = 512: the six losses and EVERY parameter gradient against the fp32
+    oracle, at the bar of the oracle's own bf16 arithmetic on the same batch and precision split
+    (bf16_grad_check; losses per value within max(1e-2, that drift))."""
+    from visual_onoma_to_wave_amd.model import FastSpeech2Loss, vTTS
+    arrays = vtts_arrays()
+    m = vTTS(*configs())
+    load_into(m, arrays)
+    m = m.to(device).train().set_precision("mixed")
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    m.postnet.dropout_p = 0.0
+    for vp in (m.variance_adaptor.duration_predictor, m.variance_adaptor.energy_predictor):
+        vp.dropout = 0.0
+    batch = _c4_batch(device)
+    out = m(*(batch[1:]), True)
+    losses = FastSpeech2Loss()(batch, out)
+    losses[0].backward()
+    got = [float(x) for x in losses]
+
+    torch.set_num_threads(16)
+    bc = _c4_batch("cpu")
+    ref, ref_g = _c4_oracle(arrays, bc, False)
+    bf = [_c4_oracle(arrays, bc, mode) for mode in ("autocast", "operands")]
+    for i, (a, r) in enumerate(zip(got, ref)):
+        drift = max(abs(b[0][i] - r) for b in bf)
+        assert abs(a - r) <= max(1e-2 * abs(r), drift) + 1e-6, ("loss", i, a, r, drift)
+
+    named = dict(m.named_parameters())
+    ours = {k: p.grad.cpu() for k, p in named.items() if p.grad is not None}
+    rows, (n, n_noise, rms_e, rms_d) = bf16_grad_check(ours, ref_g, [b[1] for b in bf], sibling=_zero_sibling)
+    rows.sort(reverse=True)
+    print(f"C4 mixed: {n} gradients; signal-dominated worst error / 1e-2: "
+          f"{max(e for _, _, e, d in rows if d <= 1e-2) / 1e-2:.3f}; noise-dominated group of {n_noise}: "
+          f"RMS error {rms_e:.3e} vs the oracle's bf16 drift {rms_d:.3e}")
+    for row in rows[:8]:
+        print("  %.3f %-60s ours %.2e oracle-bf16 %.2e" % row)
+    assert n > 180  # every parameter with a gradient but the 13 structural zeros
 
 
 # ------------------------------------------------------------------------------------------- C5

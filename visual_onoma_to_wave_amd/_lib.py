@@ -119,6 +119,9 @@ _SIGNATURES = {
     "vo_layernorm_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),
     "vo_layernorm_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                  c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vo_layernorm_bwd_ex": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                    c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
     "vo_attention": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float,
                              c_void_p, c_void_p]),
     "vo_attention_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),

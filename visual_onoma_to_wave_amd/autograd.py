@@ -152,7 +152,13 @@ def _refresh(store):
 def _params_of(w):
     """The fp32 parameter(s) behind a conv weight argument (a Linear's weight[:, :, None] view -> the
     Linear's weight), or None when it is not a plain contiguous fp32 tensor."""
-    base = w._base if (w._base is not None and w.dim() == 3 and w.shape[2] == 1) else w
+    base = w
+    if w._base is not None and w.dim() == 3 and w.shape[2] == 1:
+        # only exactly base[:, :, None]: a view that slices Ci or starts at an offset would be packed
+        # from the whole base and keyed on its id
+        base = w._base
+        if tuple(base.shape) != tuple(w.shape[:2]) or w.data_ptr() != base.data_ptr():
+            return None
     if base.dtype != torch.float32 or not base.is_contiguous() or base.shape[0] != w.shape[0]:
         return None
     return (base,)
@@ -302,6 +308,38 @@ def layernorm(x, res, g, b, lens=None):
     return LayerNormFn.apply(x, res, g, b, lens)
 
 
+class LayerNormDualFn(torch.autograd.Function):
+    """The mixed training decoder's LayerNorm (round 6): y = LN(x + res) * g + b (pad rows zeroed) with a
+    bf16 sublayer output x and the fp32 residual stream res; returns (y fp32 -- the next residual --, its
+    bf16 copy y16 -- what the next conv reads and saves).  Forward and backward are one kernel each
+    (vo_layernorm_dual / vo_layernorm_bwd_ex: the two incoming gradients are added in the kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, res, g, b, lens):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, res, g, lens)
+        return ops.layernorm(x.contiguous(), g.detach().float().contiguous(), b.detach().float().contiguous(),
+                             res=res.contiguous(), lens=lens, out_dtype=torch.float32, with_bf16=True)
+
+    @staticmethod
+    def backward(ctx, gy, gy16):
+        x, res, g, lens = ctx.saved_tensors
+        if gy is None and gy16 is None:
+            return None, None, None, None, None
+        if gy is None:  # only the copy was read (the last layer feeds mel_linear its y16)
+            gy, gy16 = gy16, None
+        gy2 = None if gy16 is None else gy16.contiguous()
+        if gy2 is not None and gy2.dtype != torch.bfloat16:
+            gy, gy2 = gy + gy2.to(gy.dtype), None
+        gh, gh32, gg, gb = ops.layernorm_bwd_ex(x.contiguous(), gy.contiguous(), g.detach().float().contiguous(),
+                                                res.contiguous(), lens=lens, gy2=gy2)
+        return gh, gh32, gg.to(g.dtype), gb.to(g.dtype), None
+
+
+def layernorm_dual(x, res, g, b, lens=None):
+    return LayerNormDualFn.apply(x, res, g, b, lens)
+
+
 class DropoutFn(torch.autograd.Function):
     """Training dropout on HIP (vo_dropout): the keep mask is a hash of (seed, site, element index), so
     the backward re-applies it to the gradient from the saved seed -- no mask tensor."""
@@ -338,8 +376,8 @@ def dropout(x, p, training=True):
     per call as with F.dropout (the draws differ from ATen's)."""
     if not training or p == 0.0:
         return x
-    if p == 1.0:
-        return x * 0.0
+    if p == 1.0:  # F.dropout's exact zeros (x * 0 would turn Inf / NaN inputs into NaN)
+        return x.masked_fill(torch.ones((), dtype=torch.bool, device=x.device), 0.0)
     xc = x.contiguous()
     if xc.data_ptr() % 16:
         xc = xc.clone()

@@ -96,12 +96,17 @@ static int ln_launch(const void* x, const void* res, const float* g, const float
 constexpr int LN_BWD_RPW = 4;   // rows per wave
 constexpr int LN_BWD_NW = 16;   // waves per workgroup: 64 rows, 256 partials at C2
 
-template <typename TX, typename TG, int NPL>
-__global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restrict__ x, const TX* __restrict__ res,
+// Round 6 (vo_layernorm_bwd_ex): res may be fp32 beside a bf16 x (the mixed decoder's fp32 residual stream,
+// vo_layernorm_dual's forward), a second incoming gradient gy2 (bf16: the gradient of y16, the copy the convs
+// read) is added to gy in registers, and gh32 (optional) receives the fp32 gradient of res beside gh.
+template <typename TX, typename TR, typename TG, int NPL>
+__global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restrict__ x, const TR* __restrict__ res,
                                                              const TG* __restrict__ gy,
+                                                             const bf16_t* __restrict__ gy2,
                                                              const float* __restrict__ gamma,
                                                              const int32_t* __restrict__ lens, int B, int T,
                                                              float eps, TX* __restrict__ gh,
+                                                             float* __restrict__ gh32,
                                                              float* __restrict__ partial) {
   constexpr int D = NPL * 64;
   __shared__ float red[LN_BWD_NW][2][D];
@@ -137,6 +142,12 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
       else
         e[0] = e[1] = e[2] = e[3] = 0.f;
       load4(gy + rr * D + c0 + i, d);
+      if (gy2) {
+        float d2[4];
+        load4(gy2 + rr * D + c0 + i, d2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] += d2[k];
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         v[r][i + k] = q[k] + e[k];
@@ -178,6 +189,7 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = sc * (g[i + e] * dy[r][i + e] - m1 - v[r][i + e] * m2);
       store4(gr + i, o);
+      if (gh32) store4(gh32 + row * D + c0 + i, o);
     }
   }
 #pragma unroll
@@ -229,18 +241,18 @@ __global__ void __launch_bounds__(1024) ln_partial_sum_kernel(const float* __res
   }
 }
 
-template <typename TX, typename TG>
+template <typename TX, typename TG, typename TR = TX>
 static int ln_bwd_launch(const void* x, const void* res, const void* gy, const float* g, const int32_t* lens,
                          int B, int T, int D, float eps, void* gh, float* dgamma, float* dbeta, float* ws,
-                         hipStream_t st) {
+                         hipStream_t st, const void* gy2 = nullptr, float* gh32 = nullptr) {
   const int64_t rows = (int64_t)B * T;
   const int nblk = (int)((rows + LN_BWD_NW * LN_BWD_RPW - 1) / (LN_BWD_NW * LN_BWD_RPW));
   if (D == 256)
-    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 4>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
-                       (const TX*)res, (const TG*)gy, g, lens, B, T, eps, (TX*)gh, ws);
+    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TR, TG, 4>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
+                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, gh32, ws);
   else
-    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TG, 8>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
-                       (const TX*)res, (const TG*)gy, g, lens, B, T, eps, (TX*)gh, ws);
+    hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TR, TG, 8>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
+                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, gh32, ws);
   hipLaunchKernelGGL(ln_partial_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, st, (const float*)ws, nblk,
                      2 * D, dgamma, dbeta);
   VO_RETURN_LAUNCH();
@@ -281,7 +293,9 @@ extern "C" int vo_layernorm_dual(const void* x, int x_dtype, const void* res, in
     return ln_launch<float, float, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16);
   if (x_dtype == VO_BF16 && res_dtype == VO_BF16)
     return ln_launch<bf16_t, bf16_t, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16);
-  vo_set_error("layernorm_dual: unsupported dtype combination (fp32 y, fp32 or bf16 x / res)");
+  if (x_dtype == VO_BF16 && res_dtype == VO_F32)  // round 6: bf16 sublayer output + fp32 residual stream (training)
+    return ln_launch<bf16_t, float, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16);
+  vo_set_error("layernorm_dual: unsupported dtype combination (fp32 y; fp32 / fp32, bf16 / bf16 or bf16 / fp32 x / res)");
   return VO_ERR_INVALID;
 }
 
@@ -305,5 +319,29 @@ extern "C" int vo_layernorm_bwd(const void* x, const void* res, int x_dtype, con
   if (x_dtype == VO_F32 && gy_dtype == VO_BF16) VO_LNB(float, bf16_t);
 #undef VO_LNB
   vo_set_error("layernorm_bwd: unsupported dtype combination");
+  return VO_ERR_INVALID;
+}
+
+extern "C" int vo_layernorm_bwd_ex(const void* x, int x_dtype, const void* res, int res_dtype, const void* gy,
+                                   int gy_dtype, const void* gy2, const float* gamma, const int32_t* lens, int B,
+                                   int T, int D, float eps, void* gh, float* gh32, float* dgamma, float* dbeta,
+                                   void* workspace, void* stream) {
+  VO_CHECK_ARG(x && gy && gamma && gh && dgamma && dbeta && workspace, "layernorm_bwd_ex: null pointer");
+  VO_CHECK_ARG(D == 256 || D == 512, "layernorm_bwd_ex: D=%d unsupported (256 or 512)", D);
+  VO_CHECK_ARG(B > 0 && T > 0, "layernorm_bwd_ex: empty");
+  VO_CHECK_ARG(gh32 == nullptr || ((const void*)gh32 != x && (const void*)gh32 != gh), "layernorm_bwd_ex: gh32 aliases");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* ws = (float*)workspace;
+  if (!res) res_dtype = x_dtype;
+  if (x_dtype == VO_BF16 && res_dtype == VO_F32 && gy_dtype == VO_F32)
+    return ln_bwd_launch<bf16_t, float, float>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st, gy2,
+                                               gh32);
+  if (x_dtype == VO_BF16 && res_dtype == VO_F32 && gy_dtype == VO_BF16)
+    return ln_bwd_launch<bf16_t, bf16_t, float>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st,
+                                                gy2, gh32);
+  if (x_dtype == res_dtype && gy2 == nullptr && gh32 == nullptr)
+    return vo_layernorm_bwd(x, res, x_dtype, gy, gy_dtype, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, workspace,
+                            stream);
+  vo_set_error("layernorm_bwd_ex: unsupported dtype combination (bf16 x with fp32 res, or equal x / res without gy2 / gh32)");
   return VO_ERR_INVALID;
 }

@@ -573,6 +573,9 @@ int vo_rb3_wave_try(const void* x, const void* const* w1, const float* const* b1
 int vo_rb3_rr_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
                   const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
                   float out_scale, int cfg, hipStream_t st, int* handled);  // resblock_rr.hip
+int vo_rb3_pb_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                  const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
+                  float out_scale, hipStream_t st, int* handled, int frag);  // resblock_pb3.hip
 
 extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
                             const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C,
@@ -603,6 +606,11 @@ extern "C" int vo_resblock3(const void* x, const void* const* w1, const float* c
   // rb3_cfg (A/B): 1 = 128-row frames (C = 32: 512-row), 4 = a 3-deep LDS-DMA ring of half / whole
   // taps (C = 128 / 64; within 2 % of double buffering: the DMA latency is not what binds).
   const int cfg = vo_tune_get("rb3_cfg");
+  if (cfg == 0) {  // round 6: wave-owned output planes (resblock_pb3.hip) for C = 64 / 128; rb3_cfg 90: the LDS-tile block
+    int handled = 0;
+    const int rc = vo_rb3_pb_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, st, &handled, 0);
+    if (handled) return rc;
+  }
   {  // round 4: register-resident frames (resblock_rr.hip) for C = 32, dilations (1, 3, 5); rb3_cfg 77-89 (A/B)
     int handled = 0;
     const int rc = vo_rb3_rr_try(x, w1, b1, w2, b2, dil, y, acc, B, T, C, slope, out_scale, cfg, st, &handled);

@@ -1,0 +1,394 @@
+// HiFi-GAN ResBlock1 with kernel size 3 -- the whole block (three (c1_d, c2) iterations, dilations
+// (1, 3, 5)) in one launch, in the "wave-owned output planes" form of resblock_rw.hip:
+//   x1 = x  + c2_0(lrelu(c1_1(lrelu x )))        (x1, x2 rounded to bf16 as between per-pair launches)
+//   x2 = x1 + c2_1(lrelu(c1_3(lrelu x1)))
+//   y  = (x2 + c2_2(lrelu(c1_5(lrelu x2)))) * out_scale (+ acc)
+// (scripts/hifigan/models.py:96-103; the MRF sum and 1/num_kernels scale of models.py:155-160 ride in the
+// last epilogue).
+//
+// Why (round 6).  The LDS-tile block (resblock3.hip) shares every streamed weight tap between its waves
+// through LDS: 0.37 (C = 128) / 0.27 (C = 64) of the dense bf16 peak, and 13 M LDS bank conflicts at
+// C = 64.  Here, as in the k = 7 / 11 pair kernel that lifted stage 1 to 0.50:
+//   * 4 waves, one per SIMD; wave w owns the 32 output channels of plane w % NP for 256 frame rows, in
+//     all six convs of the block.  Its weights (32 co x C ci per tap) stream from L2 straight into its
+//     registers one tap ahead -- no weight goes through LDS, no tap needs a barrier;
+//   * the activations are shared through LDS: the lrelu'd window (lrelu x, then lrelu x1, lrelu x2 written
+//     over it) and c1's output T1.  6 barriers per tile (one per conv);
+//   * x1 / x2 never leave the chip: a wave's P2 accumulators ARE the x_{s+1} rows of its plane, kept as
+//     bf16 in registers (the next P2's residual, entered by identity MFMAs: exact) and written lrelu'd
+//     into the window for the next c1;
+//   * every conv runs on the whole F-row frame; the valid rows shrink by the halos (1+1+3+1+5+1 = 12 per
+//     side), so a tile yields F - 24 output rows (F = 256 at C = 128: 9 % extra MFMA work; F = 512 at C = 64);
+//   * LDS rows [plane][row][32 ch], 16-byte chunk q of row r at q ^ ((r >> 1) & 3) (rw_off): the B-fragment
+//     reads at any row shift, the T1 / window stores of the epilogues and the window staging (odd plane
+//     stride) are bank-conflict free.
+// Weights: [K][C_out][C_in] bf16 packs (vo_pack_weight) or the fragment order of vo_pack_frag (FR);
+// biases fp32.
+
+#include <algorithm>
+#include <cmath>
+
+#include "mrf_common.h"
+
+namespace vo {
+
+struct Pb3Args {
+  const bf16_t* x;
+  const bf16_t* w[6];  // conv v = 2 s + ph: c1 of stage s (ph 0), c2 of stage s (ph 1)
+  const float* b[6];
+  bf16_t* y; const bf16_t* acc;
+  int T, dil[3], tiles_per_b, ntiles;
+  float slope, out_scale;
+};
+
+constexpr int PB_HP = 8;     // LDS pad rows per side (dilation <= 8; a multiple of 8 keeps the swizzle)
+constexpr int PB_HALO = 12;  // valid rows lost per side: sum over the six convs of dil * (k - 1) / 2
+constexpr int pb_np(int C) { return C / 32; }
+constexpr int pb_f(int C) { return 256 * (4 / pb_np(C)); }        // frame rows per tile
+constexpr int pb_rp(int C) { return pb_f(C) + 2 * PB_HP + 1; }    // LDS rows per plane (odd)
+constexpr size_t pb_lds(int C) { return (size_t)2 * pb_np(C) * pb_rp(C) * 32 * sizeof(bf16_t) + 6 * C * sizeof(float); }
+
+__device__ __forceinline__ int pb_off(int r, int q) { return r * 32 + 8 * (q ^ ((r >> 1) & 3)); }
+
+template <int C, int ACC, bool FR>
+__global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
+  constexpr int NP = pb_np(C), F = pb_f(C), NJ = 16, RP = pb_rp(C), PL = RP * 32;
+  constexpr int BT = F - 2 * PB_HALO;
+  constexpr int VPR = C / 8, RPS = 256 / VPR, NWV = F / RPS;  // window: 16-byte vectors per row, rows per slot, slots
+  constexpr int NAP = 2 * NP;                                  // A pieces (KiB) per tap and wave
+  constexpr int NST = NJ * NP;                                 // (row tile, plane) steps per tap
+  constexpr int NB = 10, DB = 8;                               // B-fragment ring / prefetch distance (steps)
+  constexpr int NU = 18;                                       // taps per tile (6 convs x 3)
+  static_assert(RPS % 8 == 0 && NWV * RPS == F && NST >= 2 * NAP, "geometry");
+  // the next tile's window: NWV slots loaded over the first two taps of stage 2's c1 (the window is still
+  // being read there; registers only) and written, lrelu'd, over the first two taps of its c2
+  // (every global load of a tap is issued after the tap's A pieces: vmcnt retires in issue order, so a
+  // load issued before an A piece would hold up the next tap's first MFMAs until it returned)
+  constexpr int WSP = (NST - 2 * NAP) / ((NWV + 1) / 2);       // steps between a tap's window slots
+  static_assert(WSP >= 2 && ((NWV + 1) / 2) * WSP <= NST - 2 * NAP, "window staging");
+  // written over c2's first tap, after its A pieces (WSS steps apart); ACC == 2: the MRF accumulator rows are
+  // requested in the same steps -- after the row tiles' residual MFMAs (plane 0, steps 0 .. 15) freed x2's
+  // registers, two taps before they enter through an identity MFMA in c2's last tap (at C = 128, loaded
+  // with the window in c1 they pushed the live registers past 512 and spilled)
+  constexpr int WSS = (NST - 2 * NAP) / NWV;
+  static_assert(WSS >= 1 && NJ <= NWV, "window stores / accumulator requests");
+
+  const int T = a.T;
+  const float slope = a.slope;
+
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* win = reinterpret_cast<bf16_t*>(smem_raw);       // [NP][RP][32]: lrelu x_s
+  bf16_t* t1 = win + NP * PL;                               // [NP][RP][32]: c1's output
+  float* sbias = reinterpret_cast<float*>(t1 + NP * PL);    // [6][C]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pw = w % NP, row0 = (w / NP) * 256;  // the wave's plane and first frame row
+  const int lr = lane & 15, lg = lane >> 4;
+
+  const int G = gridDim.x;
+  int tile = (int)(((int64_t)blockIdx.x * a.ntiles) / G);
+  const int tile_end = (int)(((int64_t)(blockIdx.x + 1) * a.ntiles) / G);
+  if (tile >= tile_end) return;  // uniform per workgroup
+
+  for (int i = tid; i < 6 * C; i += 256) sbias[i] = a.b[i / C][i % C];
+  // pad rows (read only by taps of frame rows whose outputs the halo discards): zeros, never NaN
+  for (int i = tid; i < 2 * NP * (2 * PB_HP + 1) * 4; i += 256) {
+    const int q = i & 3, r0 = (i >> 2) % (2 * PB_HP + 1), pb = (i >> 2) / (2 * PB_HP + 1);
+    const int r = r0 < PB_HP ? r0 : F + r0;
+    *reinterpret_cast<u32x4*>(win + pb * PL + pb_off(r, q)) = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  // ---- A fragments (as resblock_rw.hip): lane l holds W[tap][co][ci], co = 32pw + 8(lr>>2) + 4t + (lr&3),
+  // ci = 32s + 8lg .. +7; accumulator register i of co tile t is then channel 32pw + 8lg + 4t + i
+  const int aoff = ((32 * pw + 8 * (lr >> 2) + (lr & 3)) * C + 8 * lg) * (int)sizeof(bf16_t);
+  const int afr = pw * NAP * 1024 + lane * 16;
+  __amdgpu_buffer_rsrc_t rw[6];
+#pragma unroll
+  for (int v = 0; v < 6; ++v) rw[v] = __builtin_amdgcn_make_buffer_rsrc((void*)a.w[v], (short)0, 3 * C * C * 2, 0x00020000);
+  bf16x8 A[2][NP][2];  // tap u's fragments in slot u & 1 (18 taps per tile: the parity carries over)
+  auto loadA_piece = [&](int u, int i) {
+    const int uu = u % NU, v = uu / 3, k = uu % 3;
+    const int s = i >> 1, t = i & 1;
+    const int lo = FR ? afr + i * 1024 : aoff + t * 4 * C * 2 + s * 64;
+    A[uu & 1][s][t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw[v], lo, k * (C * C * 2), 0));
+  };
+  auto utt = [&](const bf16_t* p, int b) {  // one utterance of a (B, T, C) tensor: rows outside read 0
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (int64_t)b * T * C), (short)0, T * C * 2, 0x00020000);
+  };
+
+  // ---- window staging: vector v = tid + 256 slot = (frame row xr + RPS slot, 16-byte column xc)
+  const int xr = tid / VPR, xc = tid % VPR;
+  const int xl = (xc >> 2) * PL + pb_off(xr + PB_HP, xc & 3);  // + slot * RPS rows (swizzle unchanged)
+  u32x4 xw[NWV];
+  auto load_win = [&](int tl, int sl) {
+    const int b = tl / a.tiles_per_b;
+    const int p0 = (tl - b * a.tiles_per_b) * BT - PB_HALO;
+    // positions before 0 wrap to huge offsets and past T exceed the range: both read 0 (zero padding)
+    xw[sl] = __builtin_amdgcn_raw_buffer_load_b128(utt(a.x, b), ((p0 + xr + RPS * sl) * C + xc * 8) * 2, 0, 0);
+  };
+  auto store_win = [&](int sl) { *reinterpret_cast<u32x4*>(win + xl + sl * RPS * 32) = lrelu8(xw[sl], slope); };
+
+#pragma unroll
+  for (int i = 0; i < NAP; ++i) loadA_piece(0, i);
+#pragma unroll
+  for (int sl = 0; sl < NWV; ++sl) load_win(tile, sl);
+#pragma unroll
+  for (int sl = 0; sl < NWV; ++sl) store_win(sl);
+
+  f32x4 acc[2][NJ];
+  bf16x8 Bq[NB];
+  u32x4 xres[NJ];  // the wave's residual rows (x from HBM for stage 0, then x1, x2 from its own epilogues)
+  u32x4 ares[NJ];
+  bf16x8 aid[2], ais[2];  // identity A fragments (co tile t); ais scaled by 1 / out_scale (ACC == 2)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool one = (lr >> 2) == lg && e == 4 * t + (lr & 3);
+      aid[t][e] = (__bf16)(one ? 1.0f : 0.0f);
+      ais[t][e] = (__bf16)(one ? 1.0f / a.out_scale : 0.0f);
+    }
+
+  // One conv of the block over the frame: 3 taps x NP input planes x 16 row tiles; steps plane-major inside
+  // taps 0 / 1 and row-tile-major in tap 2, whose row tile j is final after its NP steps and runs its
+  // epilogue (four parts) under row tile j + 1's MFMAs.  Each step: one B-fragment read (DB steps ahead),
+  // two MFMAs, and one piece of the side work (the next tap's A pieces, the hook).
+  auto conv = [&](auto vc, auto hook, auto post, auto extra) {
+    constexpr int V = decltype(vc)::value, PH = V & 1, S = V >> 1;
+    const bf16_t* src = PH ? t1 : win;
+    const int step = PH ? 1 : a.dil[S];
+    int lro = lr, lgo = lg;
+    asm volatile("" : "+v"(lro), "+v"(lgo));
+    auto rt = [&](int k, int jj) { return k < 2 ? jj % NJ : jj / NP; };
+    auto pl = [&](int k, int jj) { return k < 2 ? jj / NJ : jj % NP; };
+    auto readB = [&](int q) {
+      const int k = q / NST, j = rt(k, q % NST), s = pl(k, q % NST);
+      const bf16_t* base = src + (s >> 1) * 2 * PL + pb_off(PB_HP + (k - 1) * step + row0 + lro, lgo);
+      Bq[q % NB] = *reinterpret_cast<const bf16x8*>(base + (s & 1) * PL + j * 512);
+    };
+    const f32x4* bz = reinterpret_cast<const f32x4*>(sbias + V * C + 32 * pw + 8 * lg);
+    const f32x4 bz0 = bz[0], bz1 = bz[1];
+#pragma unroll
+    for (int q = 0; q < DB; ++q) readB(q);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int u = 3 * V + k;
+      const bf16x8(&Ak)[NP][2] = A[u & 1];
+#pragma unroll
+      for (int jj = 0; jj < NST; ++jj) {
+        const int q = k * NST + jj;
+        const int j = rt(k, jj), s = pl(k, jj);
+        if (q + DB < 3 * NST) readB(q + DB);
+        if (jj < 2 * NAP && jj % 2 == 0) loadA_piece(u + 1, jj / 2);
+        hook(k, jj);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 b = Bq[q % NB];
+        if (k == 0 && s == 0) {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, bz0, 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, bz1, 0, 0, 0);
+        } else {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, acc[1][j], 0, 0, 0);
+        }
+        extra(k, j, s);
+        if (k == 2 && jj >= NP) {  // row tile jj / NP - 1's epilogue, 4 / NP of its 4 parts per step
+          const int r = jj % NP, j0 = jj / NP - 1;
+#pragma unroll
+          for (int p = r * 4 / NP; p < (r + 1) * 4 / NP; ++p) post(j0, p);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) post(NJ - 1, p);
+  };
+
+  const int cofs = 32 * pw + 8 * lg;
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / a.tiles_per_b;
+    const int t0 = (tile - b * a.tiles_per_b) * BT;
+    const int p0 = t0 - PB_HALO;  // position of frame row 0
+    const int ntile = tile + 1 < tile_end ? tile + 1 : tile;
+    const bool interior = p0 >= 0 && p0 + F <= T;
+    const __amdgpu_buffer_rsrc_t rsx = utt(a.x, b);
+    const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
+
+    lds_barrier();  // window staged; the previous tile's T1 reads are done
+
+    uint32_t pv[4];
+    // P1 epilogue: T1 = lrelu(acc) (bias in acc), frame rows outside [0, T) = 0 (c2's zero padding)
+    auto p1_post = [&](int j, int p) {
+      const int t = p >> 1, e = 2 * (p & 1);
+      pv[p] = pk_bf16(lrelu_max(acc[t][j][e], slope), lrelu_max(acc[t][j][e + 1], slope));
+      if (p == 3) {
+        const int f = row0 + 16 * j + lr, pos = p0 + f;
+        u32x4 v = u32x4{pv[0], pv[1], pv[2], pv[3]};
+        if (!interior) v &= (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        *reinterpret_cast<u32x4*>(t1 + pw * PL + pb_off(f + PB_HP, lg)) = v;
+      }
+    };
+    // P2 epilogue of stages 0 / 1: x_{s+1} = bf16(acc) kept in xres; lrelu(x_{s+1}) into the window (rows
+    // outside [0, T) = 0: the next c1's zero padding)
+    auto p2_mid_post = [&](int j, int p) {
+      const int e = 2 * p;
+      pv[p] = pk_bf16(acc[e >> 2][j][e & 3], acc[e >> 2][j][(e & 3) + 1]);
+      if (p == 3) {
+        const int f = row0 + 16 * j + lr, pos = p0 + f;
+        xres[j] = u32x4{pv[0], pv[1], pv[2], pv[3]};
+        u32x4 v = lrelu8(xres[j], slope);
+        if (!interior) v &= (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        *reinterpret_cast<u32x4*>(win + pw * PL + pb_off(f + PB_HP, lg)) = v;
+      }
+    };
+    // the residual (and acc_in / out_scale) through identity MFMAs at plane 0's step of row tile j:
+    // the lane's residual vector of row tile j IS a B fragment of its own plane
+    auto res_extra = [&](int k, int j, int s) {
+      if (s != 0 || k != 0) return;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
+    };
+    auto no_hook = [&](int, int) {};
+    auto no_extra = [&](int, int, int) {};
+
+    // ---- stage 0, c1 (dilation dil[0]) over lrelu x; x's rows of this wave's plane requested in taps 1 / 2
+    // (L2 hits: the window staging just read them), the residual of stage 0's c2
+    auto s0_hook = [&](int k, int jj) {
+      constexpr int RSP = (NST - 2 * NAP) / (NJ / 2);
+      if (k == 0 || jj < 2 * NAP || (jj - 2 * NAP) % RSP != 0) return;
+      const int i = (jj - 2 * NAP) / RSP;
+      if (i >= NJ / 2) return;
+      const int j = (k - 1) * (NJ / 2) + i;
+      xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
+    };
+    conv(std::integral_constant<int, 0>{}, s0_hook, p1_post, no_extra);
+    lds_barrier();
+    conv(std::integral_constant<int, 1>{}, no_hook, p2_mid_post, res_extra);
+    lds_barrier();
+    conv(std::integral_constant<int, 2>{}, no_hook, p1_post, no_extra);
+    lds_barrier();
+    conv(std::integral_constant<int, 3>{}, no_hook, p2_mid_post, res_extra);
+    lds_barrier();
+
+    // ---- stage 2: c1 loads the next tile's window into registers (taps 0 / 1) and, for ACC == 2, the MRF
+    // accumulator rows of row tiles 0 .. 7 (tap 2)
+    auto s2a_hook = [&](int k, int jj) {
+      if (jj < 2 * NAP) return;
+      const int i = (jj - 2 * NAP) / WSP;
+      if (k < 2 && (jj - 2 * NAP) % WSP == 0 && i < (NWV + 1) / 2 && k * ((NWV + 1) / 2) + i < NWV)
+        load_win(ntile, k * ((NWV + 1) / 2) + i);
+    };
+    conv(std::integral_constant<int, 4>{}, s2a_hook, p1_post, no_extra);
+    lds_barrier();  // T1 complete; the window is dead until the next tile
+
+    // ---- stage 2, c2: y = (x2 + c2) * out_scale (+ acc) -> HBM; the next window written lrelu'd (taps 0 / 1)
+    const int valid = min(BT, T - t0);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
+    auto s2b_hook = [&](int k, int jj) {
+      if (k != 0 || jj < 2 * NAP || (jj - 2 * NAP) % WSS != 0) return;
+      const int i = (jj - 2 * NAP) / WSS;
+      if (i < NWV) store_win(i);
+      if constexpr (ACC == 2)
+        if (i < NJ) ares[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * i + lr) * C + cofs) * 2, 0, 0);
+    };
+    auto s2b_extra = [&](int k, int j, int s) {
+      if (s != 0) return;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (k == 0)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
+        if constexpr (ACC == 2)
+          if (k == 2)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ais[t], __builtin_bit_cast(bf16x8, ares[j]), acc[t][j], 0, 0, 0);
+      }
+    };
+    const float osc = a.out_scale;
+    auto s2b_post = [&](int j, int p) {
+      float q[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = 2 * p + u;
+        q[u] = acc[e >> 2][j][e & 3] * osc;
+        if constexpr (ACC == 1) {
+          const uint32_t aw2 = ares[j][p];
+          q[u] += __uint_as_float(u ? (aw2 & 0xffff0000u) : (aw2 << 16));
+        }
+      }
+      pv[p] = pk_bf16(q[0], q[1]);
+      if (p == 3)  // frame rows before the halo wrap to huge offsets, rows past `valid` exceed the range
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{pv[0], pv[1], pv[2], pv[3]}, yrs,
+                                               ((row0 + 16 * j + lr - PB_HALO) * C + cofs) * (int)sizeof(bf16_t), 0, 0);
+    };
+    if constexpr (ACC == 1) {  // epilogue add: the accumulator rows requested at the start of the conv
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
+    }
+    conv(std::integral_constant<int, 5>{}, s2b_hook, s2b_post, s2b_extra);
+  }
+}
+
+template <int C, int ACC, bool FR>
+static int pb3_launch(Pb3Args a, int B, hipStream_t st) {
+  constexpr int BT = pb_f(C) - 2 * PB_HALO;
+  a.tiles_per_b = (a.T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  auto kern = mrf_pb3_kernel<C, ACC, FR>;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const int grid = (int)std::min<int64_t>((int64_t)cus, a.ntiles);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), pb_lds(C), st, a);
+  VO_RETURN_LAUNCH();
+}
+
+}  // namespace vo
+
+using namespace vo;
+
+// Entry from vo_resblock3 / vo_resblock3_frag: *handled = 1 when this kernel covers the shape (C = 64 / 128,
+// every dilation <= 8 and their halo sum <= 12).
+int vo_rb3_pb_try(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                  const float* const* b2, const int* dil, void* y, const void* acc, int B, int T, int C, float slope,
+                  float out_scale, hipStream_t st, int* handled, int frag) {
+  *handled = 0;
+  if (!(C == 64 || C == 128)) return VO_OK;
+  int halo = 0;
+  for (int s = 0; s < 3; ++s) {
+    if (dil[s] < 1 || dil[s] > PB_HP) return VO_OK;
+    halo += dil[s] + 1;
+  }
+  if (halo > PB_HALO) return VO_OK;
+  Pb3Args a;
+  a.x = (const bf16_t*)x;
+  for (int s = 0; s < 3; ++s) {
+    a.w[2 * s] = (const bf16_t*)w1[s]; a.b[2 * s] = b1[s];
+    a.w[2 * s + 1] = (const bf16_t*)w2[s]; a.b[2 * s + 1] = b2[s];
+    a.dil[s] = dil[s];
+  }
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
+  a.T = T; a.slope = slope; a.out_scale = out_scale;
+  a.tiles_per_b = a.ntiles = 0;
+  *handled = 1;
+  int accm = 0;
+  if (acc) {  // acc_in / out_scale through the identity MFMA when 1 / out_scale is a bf16 value (3)
+    const float inv = 1.0f / out_scale;
+    const float invb = __bfloat162float(__float2bfloat16(inv));
+    accm = (invb == inv && std::isfinite(inv) && inv * out_scale == 1.0f) ? 2 : 1;
+  }
+#define VO_PB3_DISPATCH(CC, FF) \
+  return accm == 2 ? pb3_launch<CC, 2, FF>(a, B, st) : accm == 1 ? pb3_launch<CC, 1, FF>(a, B, st) \
+                                                   : pb3_launch<CC, 0, FF>(a, B, st)
+  if (C == 64) {
+    if (frag) VO_PB3_DISPATCH(64, true);
+    VO_PB3_DISPATCH(64, false);
+  }
+  if (frag) VO_PB3_DISPATCH(128, true);
+  VO_PB3_DISPATCH(128, false);
+#undef VO_PB3_DISPATCH
+}

@@ -52,6 +52,7 @@ class vTTS(HipModule):
         self.variance_adaptor.set_compute_dtype(front)
         self.decoder.set_compute_dtype(back)
         self.postnet.set_compute_dtype(back)
+        self.postnet.train_act_dtype = self.stream_dtype
         return self
 
     def _build(self, device, dtype):
@@ -102,7 +103,7 @@ class vTTS(HipModule):
             x = x + self.audiotype_emb(audiotypes).to(x.dtype)[:, None, :]
         x, e_pred, k_pred, log_d, d_rounded, mel_len, mel_masks = self.variance_adaptor.train_run(
             x, src_masks, src_l32, mel_masks, max_mel_len, e_targets, k_targets, d_targets,
-            out_dtype=self.decoder.compute_dtype)
+            out_dtype=self.stream_dtype)
         x, mel_masks = self.decoder.train_run(x, mel_masks, mel_l32)
         mel = AG.linear(x, self.mel_linear.weight, self.mel_linear.bias, compute_dtype=self.compute_dtype,
                         out_dtype=torch.float32)

@@ -224,6 +224,32 @@ def layernorm_bwd(x, gy, gamma, res=None, lens=None, eps=1e-5):
     return gh, dg, db
 
 
+def layernorm_bwd_ex(x, gy, gamma, res, lens=None, gy2=None, eps=1e-5):
+    """Backward of ``layernorm(x, ..., res=res, out_dtype=float32, with_bf16=True)`` with a bf16 x and an
+    fp32 res (the training decoder's fp32 residual stream): gy (fp32 or bf16) the gradient of y, gy2
+    (bf16, optional) that of the y16 copy -- added in the kernel.  Returns (gh in x's dtype, gh32 =
+    the same gradient in fp32 for res, dgamma, dbeta) (vo_layernorm_bwd_ex)."""
+    B, T, D = x.shape
+    for t, n in ((x, "x"), (gy, "gy"), (res, "res")):
+        _contig(t, n)
+    if x.dtype != torch.bfloat16 or res.dtype != torch.float32 or res.shape != x.shape or gy.shape != x.shape:
+        raise ValueError("layernorm_bwd_ex: bf16 x, fp32 res, gy of x's shape")
+    if gy2 is not None:
+        _contig(gy2, "gy2")
+        if gy2.dtype != torch.bfloat16 or gy2.shape != x.shape:
+            raise ValueError("layernorm_bwd_ex: gy2 must be bf16 of x's shape")
+    L = _lib.lib()
+    gh = torch.empty_like(x)
+    gh32 = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_layernorm_bwd_workspace_size(B, T, D)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_layernorm_bwd_ex(_ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res), _ptr(gy), vo_dtype(gy),
+                                     _ptr(gy2), _ptr(gamma), _ptr(lens), B, T, D, eps, _ptr(gh), _ptr(gh32), _ptr(dg),
+                                     _ptr(db), _ptr(ws), _stream(x)), "vo_layernorm_bwd_ex")
+    return gh, gh32, dg, db
+
+
 # ----------------------------------------------------------------------------- attention
 
 def attention(qkv, lens, n_head, out=None, with_lse=False):

@@ -95,9 +95,15 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 st = self.state.get(p, {})
                 for k in ("exp_avg", "exp_avg_sq"):
-                    if k not in st:
-                        continue
                     keep = moments[p].get(k)
+                    if k not in st:
+                        if keep is not None:
+                            # no loaded moments for a parameter a captured step still reads: zero them
+                            # (an eager step would start it from zeros) and keep them in the state
+                            keep.zero_()
+                            st[k] = keep
+                            self.state[p] = st
+                        continue
                     if keep is not None and keep.shape == st[k].shape:
                         keep.copy_(st[k])
                         st[k] = keep

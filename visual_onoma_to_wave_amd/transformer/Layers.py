@@ -33,19 +33,30 @@ class FFTBlock(HipModule):
             y, y16 = self.slf_attn.run(x, lens, mask_rows=True), None
         return self.pos_ffn.run(y, lens, x16=y16, want16=want16 and dual)
 
-    def train_run(self, x, lens):
-        """Training forward (autograd; dropout active), scripts/transformer/Layers.py:21-30."""
+    def train_run(self, x, lens, x16=None):
+        """Training forward (autograd; dropout active), scripts/transformer/Layers.py:21-30.  Mixed
+        precision (fp32 x, bf16 compute): the residual stream stays fp32 as in inference (a bf16 stream
+        raised the decoder's forward drift from fp32 from 3.2e-3 to 6.0e-3 at C4, past the reference's
+        own bf16 arithmetic) and the convs read the bf16 copies the LayerNorms write beside it; returns
+        (y, y16), y16 None unless mixed.  x16: the bf16 copy of x (None: cast here)."""
         mha, ffn, cd = self.slf_attn, self.pos_ffn, self.compute_dtype
-        qkv = AG.qkv_linear(x, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
+        dual = x.dtype == torch.float32 and cd == torch.bfloat16
+        xin = (x16 if x16 is not None else x.to(cd)) if dual else x
+        qkv = AG.qkv_linear(xin, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
                             mha.w_vs.bias, cd)
         att = AG.attention(qkv, lens, mha.n_head)
         y = AG.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p)
-        x1 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
         k1, k2 = ffn.kernel_size
-        h = AG.conv1d(x1, ffn.w_1.weight, ffn.w_1.bias, K=k1, pad=(k1 - 1) // 2, relu=True, compute_dtype=cd)
+        if dual:
+            x1, x1_16 = AG.layernorm_dual(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
+        else:
+            x1 = x1_16 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
+        h = AG.conv1d(x1_16, ffn.w_1.weight, ffn.w_1.bias, K=k1, pad=(k1 - 1) // 2, relu=True, compute_dtype=cd)
         y2 = AG.conv1d(h, ffn.w_2.weight, ffn.w_2.bias, K=k2, pad=(k2 - 1) // 2, compute_dtype=cd)
         y2 = AG.dropout(y2, ffn.dropout.p)
-        return AG.layernorm(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens)
+        if dual:
+            return AG.layernorm_dual(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens)
+        return AG.layernorm(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens), None
 
     def forward(self, enc_input, mask=None, slf_attn_mask=None):
         self._check_inference()
@@ -76,6 +87,7 @@ class PostNet(HipModule):
                  [n_mel_channels])
         self.kernel_size = postnet_kernel_size
         self.dropout_p = 0.5  # F.dropout(..., 0.5, training), scripts/transformer/Layers.py:129-131
+        self.train_act_dtype = torch.float32  # vTTS.set_precision: bf16 in the all-bf16 mode
         self.convolutions = nn.ModuleList(
             nn.Sequential(
                 ConvNorm(cin, cout, kernel_size=postnet_kernel_size,
@@ -116,8 +128,11 @@ class PostNet(HipModule):
         for i, seq in enumerate(self.convolutions):
             conv, bn = seq[0].conv, seq[1]
             last = i == n - 1
+            # mixed precision: the conv outputs (BatchNorm / tanh / dropout operands) stay fp32 -- BatchNorm's
+            # backward then hands the conv an fp32 dY, whose column sums (the conv bias gradient, exactly 0
+            # before a train-mode BatchNorm) are not the noise of 16 k bf16-rounded terms
             h = AG.conv1d(h, conv.weight, conv.bias, K=k, pad=(k - 1) // 2, compute_dtype=self.compute_dtype,
-                          out_dtype=torch.float32 if last else self.compute_dtype)
+                          out_dtype=torch.float32 if last else self.train_act_dtype)
             hb = AG.batch_norm_train(h, bn, (0, 1))  # channels-last (B, T, C): no transposes
             if not last:
                 hb = torch.tanh(hb)

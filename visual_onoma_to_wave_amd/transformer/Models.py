@@ -95,7 +95,7 @@ class Encoder(HipModule):
             x = self.src_word_emb(src_seq).to(self.compute_dtype)
         x = (x + pe[None]).contiguous()
         for layer in self.layer_stack:
-            x = layer.train_run(x, lens)
+            x, _ = layer.train_run(x, lens)
         return x
 
     def forward(self, src_seq, mask, return_attns=False, images=None, use_image=True):
@@ -147,9 +147,11 @@ class Decoder(HipModule):
         T = min(T, self.max_seq_len)
         x = (x[:, :T] + self.position_enc[0, :T].to(x.dtype)[None]).contiguous()
         mask = mask[:, :T]
+        x16 = None
         for layer in self.layer_stack:
-            x = layer.train_run(x, lens)
-        return x, mask
+            x, x16 = layer.train_run(x, lens, x16)
+        # mixed: the fp32 stream's bf16 copy is what mel_linear reads (its forward operand and saved input)
+        return (x16 if x16 is not None else x), mask
 
     def forward(self, enc_seq, mask, return_attns=False):
         self._check_inference()
