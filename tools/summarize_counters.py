@@ -8,7 +8,7 @@ from collections import defaultdict
 d = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if not any(s in r["Kernel_Name"] for s in ("conv1d", "pair", "rb3", "rr3", "ups", "prw", "attn")):
+        if not any(s in r["Kernel_Name"] for s in ("conv1d", "pair", "rb3", "pb3", "rr3", "ups", "prw", "attn")):
             continue
         k = r["Kernel_Name"].split("(")[0][-80:]
         d[k][r["Counter_Name"]].append(float(r["Counter_Value"]))

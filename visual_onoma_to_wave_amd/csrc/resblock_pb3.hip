@@ -30,6 +30,10 @@
 
 #include "mrf_common.h"
 
+#ifndef VO_PB3_PK
+#define VO_PB3_PK 0  // epilogue leaky ReLU with one packed multiply per value pair (A/B)
+#endif
+
 namespace vo {
 
 struct Pb3Args {
@@ -39,39 +43,60 @@ struct Pb3Args {
   bf16_t* y; const bf16_t* acc;
   int T, dil[3], tiles_per_b, ntiles;
   float slope, out_scale;
+  unsigned long long* stamps;  // diagnostic builds only (-DVO_PB3_STAMPS, tools/probes/pb3_stamps.py)
 };
+constexpr int PB_NSTW = 16, PB_NSTT = 4, PB_NPT = 30;  // stamp geometry: workgroups, tiles, stamps per tile
 
 constexpr int PB_HP = 8;     // LDS pad rows per side (dilation <= 8; a multiple of 8 keeps the swizzle)
 constexpr int PB_HALO = 12;  // valid rows lost per side: sum over the six convs of dil * (k - 1) / 2
 constexpr int pb_np(int C) { return C / 32; }
-constexpr int pb_f(int C) { return 256 * (4 / pb_np(C)); }        // frame rows per tile
+// row tiles (16 rows) per wave: the frame is 16 NJ rows per row group.  C = 128: 13 (208-row frames, 184 output
+// rows: 88.5 % of the MFMA work is kept, against 90.6 % at 16); C = 64: 14 (448-row frames, 94.6 %).  At 16 the
+// accumulators, x2, the next window and the MRF accumulator rows exceed 512 registers, and the spill reloads'
+// vmcnt(0) waits drained every prefetch in flight (C = 128 0.65 -> 0.98 ms, C = 64 0.40 -> 0.72 ms)
+#ifndef VO_PB3_NJ128
+#define VO_PB3_NJ128 13
+#endif
+#ifndef VO_PB3_NJ64
+#define VO_PB3_NJ64 14
+#endif
+constexpr int pb_nj(int C) { return C == 128 ? VO_PB3_NJ128 : VO_PB3_NJ64; }
+constexpr int pb_f(int C) { return 16 * pb_nj(C) * (4 / pb_np(C)); }  // frame rows per tile
 constexpr int pb_rp(int C) { return pb_f(C) + 2 * PB_HP + 1; }    // LDS rows per plane (odd)
 constexpr size_t pb_lds(int C) { return (size_t)2 * pb_np(C) * pb_rp(C) * 32 * sizeof(bf16_t) + 6 * C * sizeof(float); }
 
 __device__ __forceinline__ int pb_off(int r, int q) { return r * 32 + 8 * (q ^ ((r >> 1) & 3)); }
 
-template <int C, int ACC, bool FR>
+template <int C, int ACC, bool FR, bool ST = false>
 __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
-  constexpr int NP = pb_np(C), F = pb_f(C), NJ = 16, RP = pb_rp(C), PL = RP * 32;
+  constexpr int NP = pb_np(C), F = pb_f(C), NJ = pb_nj(C), RP = pb_rp(C), PL = RP * 32;
   constexpr int BT = F - 2 * PB_HALO;
   constexpr int VPR = C / 8, RPS = 256 / VPR, NWV = F / RPS;  // window: 16-byte vectors per row, rows per slot, slots
   constexpr int NAP = 2 * NP;                                  // A pieces (KiB) per tap and wave
   constexpr int NST = NJ * NP;                                 // (row tile, plane) steps per tap
   constexpr int NB = 10, DB = 8;                               // B-fragment ring / prefetch distance (steps)
   constexpr int NU = 18;                                       // taps per tile (6 convs x 3)
+#ifndef VO_PB3_LAG
+#define VO_PB3_LAG 1
+#endif
+  constexpr int LAG = VO_PB3_LAG;  // a row tile's epilogue runs during the steps of row tile j + LAG (A/B)
   static_assert(RPS % 8 == 0 && NWV * RPS == F && NST >= 2 * NAP, "geometry");
-  // the next tile's window: NWV slots loaded over the first two taps of stage 2's c1 (the window is still
-  // being read there; registers only) and written, lrelu'd, over the first two taps of its c2
+  // The next tile's window (NWV slots).  Slots 0 .. NW1-1 are loaded over the first two taps of stage 2's c1
+  // (the window is still being read there: registers only) and written, lrelu'd, in c2's first tap; slots
+  // NW1 .. NWV-1 are loaded in c2's first tap -- after the row tiles' residual MFMAs (plane 0, steps 0 .. 15)
+  // freed x2's registers -- and written in c2's last tap.  At C = 128 all 16 slots in flight beside x2 pushed
+  // the live registers past 512 (scratch spills); the MRF accumulator rows (ACC) are requested in c2's first
+  // tap too, two taps before they enter (identity MFMA or epilogue add) in its last.
   // (every global load of a tap is issued after the tap's A pieces: vmcnt retires in issue order, so a
   // load issued before an A piece would hold up the next tap's first MFMAs until it returned)
-  constexpr int WSP = (NST - 2 * NAP) / ((NWV + 1) / 2);       // steps between a tap's window slots
-  static_assert(WSP >= 2 && ((NWV + 1) / 2) * WSP <= NST - 2 * NAP, "window staging");
-  // written over c2's first tap, after its A pieces (WSS steps apart); ACC == 2: the MRF accumulator rows are
-  // requested in the same steps -- after the row tiles' residual MFMAs (plane 0, steps 0 .. 15) freed x2's
-  // registers, two taps before they enter through an identity MFMA in c2's last tap (at C = 128, loaded
-  // with the window in c1 they pushed the live registers past 512 and spilled)
-  constexpr int WSS = (NST - 2 * NAP) / NWV;
-  static_assert(WSS >= 1 && NJ <= NWV, "window stores / accumulator requests");
+#ifndef VO_PB3_NW1
+#define VO_PB3_NW1 16
+#endif
+  constexpr int NW1 = VO_PB3_NW1 < NWV ? VO_PB3_NW1 : NWV;
+  constexpr int WSP = (NST - 2 * NAP) / ((NW1 + 1) / 2);       // c1 taps 0 / 1: steps between window loads
+  constexpr int WSS = (NST - 2 * NAP) / NJ;                    // c2 tap 0: steps between requests / stores
+  constexpr int WS2 = NWV > NW1 ? (NST - 2 * NAP) / (NWV - NW1) : 1;  // c2 tap 2: steps between stores
+  static_assert(WSP >= 1 && WSS >= 1 && WS2 >= 1 && NW1 <= NJ && NWV - NW1 <= NJ, "window staging");
 
   const int T = a.T;
   const float slope = a.slope;
@@ -83,8 +108,18 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pw = w % NP, row0 = (w / NP) * 256;  // the wave's plane and first frame row
+  const int pw = w % NP, row0 = (w / NP) * 16 * NJ;  // the wave's plane and first frame row
   const int lr = lane & 15, lg = lane >> 4;
+
+  // ST (diagnostic builds): s_memtime at conv v's barrier (5v), its taps (5v + 1 + k) and its end (5v + 4),
+  // first PB_NSTT tiles of workgroups 0 .. PB_NSTW-1, written by lane 0 of each wave (vector stores)
+  int st_tile = 0;
+  auto stamp = [&](int idx) {
+    if constexpr (ST) {
+      if (blockIdx.x < PB_NSTW && st_tile < PB_NSTT && lane == 0)
+        a.stamps[((blockIdx.x * 4 + w) * PB_NSTT + st_tile) * PB_NPT + idx] = __builtin_amdgcn_s_memtime();
+    }
+  };
 
   const int G = gridDim.x;
   int tile = (int)(((int64_t)blockIdx.x * a.ntiles) / G);
@@ -174,6 +209,7 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int u = 3 * V + k;
+      stamp(5 * V + 1 + k);
       const bf16x8(&Ak)[NP][2] = A[u & 1];
 #pragma unroll
       for (int jj = 0; jj < NST; ++jj) {
@@ -192,8 +228,8 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
           acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, acc[1][j], 0, 0, 0);
         }
         extra(k, j, s);
-        if (k == 2 && jj >= NP) {  // row tile jj / NP - 1's epilogue, 4 / NP of its 4 parts per step
-          const int r = jj % NP, j0 = jj / NP - 1;
+        if (k == 2 && jj >= LAG * NP) {  // row tile jj / NP - LAG's epilogue, 4 / NP of its 4 parts per step
+          const int r = jj % NP, j0 = jj / NP - LAG;
 #pragma unroll
           for (int p = r * 4 / NP; p < (r + 1) * 4 / NP; ++p) post(j0, p);
         }
@@ -201,7 +237,8 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
       }
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) post(NJ - 1, p);
+    for (int q = 0; q < 4 * LAG; ++q) post(NJ - LAG + q / 4, q % 4);
+    stamp(5 * V + 4);
   };
 
   const int cofs = 32 * pw + 8 * lg;
@@ -210,34 +247,48 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     const int t0 = (tile - b * a.tiles_per_b) * BT;
     const int p0 = t0 - PB_HALO;  // position of frame row 0
     const int ntile = tile + 1 < tile_end ? tile + 1 : tile;
-    const bool interior = p0 >= 0 && p0 + F <= T;
+    // (the epilogues' zero-padding masks are branch-free selects: skipping them in interior tiles put a branch
+    // per row tile into the unrolled loop, and hipcc copied eight accumulators out of the AGPRs at every join)
     const __amdgpu_buffer_rsrc_t rsx = utt(a.x, b);
     const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
 
+    stamp(0);
     lds_barrier();  // window staged; the previous tile's T1 reads are done
 
     uint32_t pv[4];
     // P1 epilogue: T1 = lrelu(acc) (bias in acc), frame rows outside [0, T) = 0 (c2's zero padding)
     auto p1_post = [&](int j, int p) {
       const int t = p >> 1, e = 2 * (p & 1);
+#if VO_PB3_PK
+      pv[p] = lrelu_pk(acc[t][j][e], acc[t][j][e + 1], slope);
+#else
       pv[p] = pk_bf16(lrelu_max(acc[t][j][e], slope), lrelu_max(acc[t][j][e + 1], slope));
+#endif
       if (p == 3) {
         const int f = row0 + 16 * j + lr, pos = p0 + f;
         u32x4 v = u32x4{pv[0], pv[1], pv[2], pv[3]};
-        if (!interior) v &= (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        v &= (unsigned)pos < (unsigned)T ? 0xffffffffu : 0u;  // branch-free (see below)
         *reinterpret_cast<u32x4*>(t1 + pw * PL + pb_off(f + PB_HP, lg)) = v;
       }
     };
     // P2 epilogue of stages 0 / 1: x_{s+1} = bf16(acc) kept in xres; lrelu(x_{s+1}) into the window (rows
-    // outside [0, T) = 0: the next c1's zero padding)
+    // outside [0, T) = 0: the next c1's zero padding).  The lrelu'd copy is taken from the fp32 sum (one
+    // multiply and max per value, no unpacking of the rounded bf16 -- as resblock3.hip's epilogues)
+    uint32_t lv[4];
     auto p2_mid_post = [&](int j, int p) {
       const int e = 2 * p;
-      pv[p] = pk_bf16(acc[e >> 2][j][e & 3], acc[e >> 2][j][(e & 3) + 1]);
+      const float a0 = acc[e >> 2][j][e & 3], a1 = acc[e >> 2][j][(e & 3) + 1];
+      pv[p] = pk_bf16(a0, a1);
+#if VO_PB3_PK
+      lv[p] = lrelu_pk(a0, a1, slope);
+#else
+      lv[p] = pk_bf16(lrelu_max(a0, slope), lrelu_max(a1, slope));
+#endif
       if (p == 3) {
         const int f = row0 + 16 * j + lr, pos = p0 + f;
         xres[j] = u32x4{pv[0], pv[1], pv[2], pv[3]};
-        u32x4 v = lrelu8(xres[j], slope);
-        if (!interior) v &= (pos >= 0 && pos < T) ? 0xffffffffu : 0u;
+        u32x4 v = u32x4{lv[0], lv[1], lv[2], lv[3]};
+        v &= (unsigned)pos < (unsigned)T ? 0xffffffffu : 0u;
         *reinterpret_cast<u32x4*>(win + pw * PL + pb_off(f + PB_HP, lg)) = v;
       }
     };
@@ -255,20 +306,24 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     // ---- stage 0, c1 (dilation dil[0]) over lrelu x; x's rows of this wave's plane requested in taps 1 / 2
     // (L2 hits: the window staging just read them), the residual of stage 0's c2
     auto s0_hook = [&](int k, int jj) {
-      constexpr int RSP = (NST - 2 * NAP) / (NJ / 2);
+      constexpr int H = (NJ + 1) / 2, RSP = (NST - 2 * NAP) / H;  // row tiles 0 .. H-1 in tap 1, the rest in tap 2
       if (k == 0 || jj < 2 * NAP || (jj - 2 * NAP) % RSP != 0) return;
       const int i = (jj - 2 * NAP) / RSP;
-      if (i >= NJ / 2) return;
-      const int j = (k - 1) * (NJ / 2) + i;
+      const int j = (k - 1) * H + i;
+      if (i >= H || j >= NJ) return;
       xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
     };
     conv(std::integral_constant<int, 0>{}, s0_hook, p1_post, no_extra);
+    stamp(5);
     lds_barrier();
     conv(std::integral_constant<int, 1>{}, no_hook, p2_mid_post, res_extra);
+    stamp(10);
     lds_barrier();
     conv(std::integral_constant<int, 2>{}, no_hook, p1_post, no_extra);
+    stamp(15);
     lds_barrier();
     conv(std::integral_constant<int, 3>{}, no_hook, p2_mid_post, res_extra);
+    stamp(20);
     lds_barrier();
 
     // ---- stage 2: c1 loads the next tile's window into registers (taps 0 / 1) and, for ACC == 2, the MRF
@@ -276,10 +331,11 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     auto s2a_hook = [&](int k, int jj) {
       if (jj < 2 * NAP) return;
       const int i = (jj - 2 * NAP) / WSP;
-      if (k < 2 && (jj - 2 * NAP) % WSP == 0 && i < (NWV + 1) / 2 && k * ((NWV + 1) / 2) + i < NWV)
-        load_win(ntile, k * ((NWV + 1) / 2) + i);
+      if (k < 2 && (jj - 2 * NAP) % WSP == 0 && i < (NW1 + 1) / 2 && k * ((NW1 + 1) / 2) + i < NW1)
+        load_win(ntile, k * ((NW1 + 1) / 2) + i);
     };
     conv(std::integral_constant<int, 4>{}, s2a_hook, p1_post, no_extra);
+    stamp(25);
     lds_barrier();  // T1 complete; the window is dead until the next tile
 
     // ---- stage 2, c2: y = (x2 + c2) * out_scale (+ acc) -> HBM; the next window written lrelu'd (taps 0 / 1)
@@ -287,11 +343,16 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
     auto s2b_hook = [&](int k, int jj) {
-      if (k != 0 || jj < 2 * NAP || (jj - 2 * NAP) % WSS != 0) return;
-      const int i = (jj - 2 * NAP) / WSS;
-      if (i < NWV) store_win(i);
-      if constexpr (ACC == 2)
-        if (i < NJ) ares[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * i + lr) * C + cofs) * 2, 0, 0);
+      if (jj < 2 * NAP) return;
+      if (k == 0 && (jj - 2 * NAP) % WSS == 0) {
+        const int i = (jj - 2 * NAP) / WSS;
+        if (i < NW1) store_win(i);
+        if (i < NWV - NW1) load_win(ntile, NW1 + i);
+        if constexpr (ACC != 0)
+          if (i < NJ) ares[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * i + lr) * C + cofs) * 2, 0, 0);
+      }
+      if (k == 2 && NWV > NW1 && (jj - 2 * NAP) % WS2 == 0 && (jj - 2 * NAP) / WS2 < NWV - NW1)
+        store_win(NW1 + (jj - 2 * NAP) / WS2);
     };
     auto s2b_extra = [&](int k, int j, int s) {
       if (s != 0) return;
@@ -321,12 +382,8 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{pv[0], pv[1], pv[2], pv[3]}, yrs,
                                                ((row0 + 16 * j + lr - PB_HALO) * C + cofs) * (int)sizeof(bf16_t), 0, 0);
     };
-    if constexpr (ACC == 1) {  // epilogue add: the accumulator rows requested at the start of the conv
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
-    }
     conv(std::integral_constant<int, 5>{}, s2b_hook, s2b_post, s2b_extra);
+    ++st_tile;
   }
 }
 
@@ -374,6 +431,7 @@ int vo_rb3_pb_try(const void* x, const void* const* w1, const float* const* b1, 
   a.y = (bf16_t*)y; a.acc = (const bf16_t*)acc;
   a.T = T; a.slope = slope; a.out_scale = out_scale;
   a.tiles_per_b = a.ntiles = 0;
+  a.stamps = nullptr;
   *handled = 1;
   int accm = 0;
   if (acc) {  // acc_in / out_scale through the identity MFMA when 1 / out_scale is a bf16 value (3)
@@ -392,3 +450,37 @@ int vo_rb3_pb_try(const void* x, const void* const* w1, const float* const* b1, 
   VO_PB3_DISPATCH(128, false);
 #undef VO_PB3_DISPATCH
 }
+
+#ifdef VO_PB3_STAMPS
+// Diagnostic entry (tools/probes/pb3_stamps.py builds its own library with -DVO_PB3_STAMPS): one stamped launch
+// of the k = 3 block (dilations 1 / 3 / 5, MRF accumulator on, out_scale 1/3, [K][Co][Ci] weights) at C = 64 / 128;
+// host_out receives PB_NSTW x 4 waves x PB_NSTT tiles x PB_NPT stamps.
+extern "C" int vo_pb3_stamps(const void* x, const void* const* w1, const float* const* b1, const void* const* w2,
+                             const float* const* b2, void* y, int B, int T, int C, unsigned long long* host_out) {
+  const size_t n = (size_t)PB_NSTW * 4 * PB_NSTT * PB_NPT;
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, n * 8) != hipSuccess) return -1;
+  (void)hipMemset(d, 0, n * 8);
+  Pb3Args a;
+  a.x = (const bf16_t*)x;
+  for (int s = 0; s < 3; ++s) {
+    a.w[2 * s] = (const bf16_t*)w1[s]; a.b[2 * s] = b1[s];
+    a.w[2 * s + 1] = (const bf16_t*)w2[s]; a.b[2 * s + 1] = b2[s];
+    a.dil[s] = 2 * s + 1;
+  }
+  a.y = (bf16_t*)y; a.acc = (const bf16_t*)y;
+  a.T = T; a.slope = 0.1f; a.out_scale = 1.f / 3; a.stamps = d;
+  const int BT = pb_f(C) - 2 * PB_HALO;
+  a.tiles_per_b = (T + BT - 1) / BT;
+  a.ntiles = a.tiles_per_b * B;
+  const int grid = std::min(256, a.ntiles);
+  if (C == 64)
+    hipLaunchKernelGGL((mrf_pb3_kernel<64, 2, false, true>), dim3(grid), dim3(256), pb_lds(64), 0, a);
+  else
+    hipLaunchKernelGGL((mrf_pb3_kernel<128, 2, false, true>), dim3(grid), dim3(256), pb_lds(128), 0, a);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(host_out, d, n * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return 0;
+}
+#endif
