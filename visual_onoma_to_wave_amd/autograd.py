@@ -168,7 +168,7 @@ class Conv1dFn(torch.autograd.Function):
     """y = post(conv1d(x, w, b, K, dil, pad)), post in {none, relu}; x (B, T, Ci), w (Co, Ci, K)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, K, dil, pad, relu, compute_dtype, out_dtype):
+    def forward(ctx, x, w, b, K, dil, pad, relu, compute_dtype, out_dtype, bias_before_bn=False):
         Co = w.shape[0]
         src = _params_of(w) if PREPACK else None
         wp = _packed_weight(src, compute_dtype, "fwd") if src else ops.pack_conv_weight(w, compute_dtype)
@@ -176,18 +176,25 @@ class Conv1dFn(torch.autograd.Function):
                        K=K, dil=dil, pad=pad, post_act=ops.ACT_RELU if relu else ops.ACT_NONE,
                        out_dtype=out_dtype, compute_dtype=compute_dtype)
         ctx.save_for_backward(x, w, y if relu else None)
-        ctx.cfg = (K, dil, pad, relu, compute_dtype, b is not None)
+        ctx.cfg = (K, dil, pad, relu, compute_dtype, b is not None, bias_before_bn)
+        ctx.bias_like = b.detach() if (b is not None and bias_before_bn) else None
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        K, dil, pad, relu, cdt, has_b = ctx.cfg
+        K, dil, pad, relu, cdt, has_b, bias_before_bn = ctx.cfg
         gz = gy.contiguous()
         if relu:
             gz = ops.lrelu_mask(gz, y, 0.0)
         gx = gw = gb = None
         want_b = has_b and ctx.needs_input_grad[2]
+        if want_b and bias_before_bn:
+            # the output feeds a train-mode BatchNorm, whose batch mean subtracts any per-channel constant: the
+            # bias gradient is exactly 0 (the column sums of dY cancel); computed as 0, not as the rounding noise
+            # of 16 k bf16 terms
+            gb = torch.zeros_like(ctx.bias_like)
+            want_b = False
         if ctx.needs_input_grad[0]:
             src = _params_of(w) if PREPACK else None
             wd = _packed_weight(src, cdt, "dgrad") if src else ops.pack_dgrad_weight(w, cdt)
@@ -209,11 +216,12 @@ class Conv1dFn(torch.autograd.Function):
                                                  padding=pad, dilation=dil)
         if want_b and gb is None:
             gb = ops.colsum(gz.contiguous())
-        return gx, gw, gb, None, None, None, None, None, None
+        return gx, gw, gb, None, None, None, None, None, None, None
 
 
-def conv1d(x, w, b, K=1, dil=1, pad=0, relu=False, compute_dtype=torch.bfloat16, out_dtype=None):
-    return Conv1dFn.apply(x, w, b, K, dil, pad, relu, compute_dtype, out_dtype or x.dtype)
+def conv1d(x, w, b, K=1, dil=1, pad=0, relu=False, compute_dtype=torch.bfloat16, out_dtype=None, bias_before_bn=False):
+    """bias_before_bn: the output feeds a train-mode BatchNorm (PostNet): the bias gradient is exactly 0."""
+    return Conv1dFn.apply(x, w, b, K, dil, pad, relu, compute_dtype, out_dtype or x.dtype, bias_before_bn)
 
 
 def linear(x, weight, bias, relu=False, compute_dtype=torch.bfloat16, out_dtype=None):

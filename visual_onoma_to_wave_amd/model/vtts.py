@@ -52,7 +52,6 @@ class vTTS(HipModule):
         self.variance_adaptor.set_compute_dtype(front)
         self.decoder.set_compute_dtype(back)
         self.postnet.set_compute_dtype(back)
-        self.postnet.train_act_dtype = self.stream_dtype
         return self
 
     def _build(self, device, dtype):

@@ -87,7 +87,6 @@ class PostNet(HipModule):
                  [n_mel_channels])
         self.kernel_size = postnet_kernel_size
         self.dropout_p = 0.5  # F.dropout(..., 0.5, training), scripts/transformer/Layers.py:129-131
-        self.train_act_dtype = torch.float32  # vTTS.set_precision: bf16 in the all-bf16 mode
         self.convolutions = nn.ModuleList(
             nn.Sequential(
                 ConvNorm(cin, cout, kernel_size=postnet_kernel_size,
@@ -128,11 +127,10 @@ class PostNet(HipModule):
         for i, seq in enumerate(self.convolutions):
             conv, bn = seq[0].conv, seq[1]
             last = i == n - 1
-            # mixed precision: the conv outputs (BatchNorm / tanh / dropout operands) stay fp32 -- BatchNorm's
-            # backward then hands the conv an fp32 dY, whose column sums (the conv bias gradient, exactly 0
-            # before a train-mode BatchNorm) are not the noise of 16 k bf16-rounded terms
+            # the conv bias feeds a train-mode BatchNorm: its gradient is exactly 0 (bias_before_bn), not the
+            # rounding noise of the column sums of a bf16 dY (measured 2x the reference's own bf16 noise)
             h = AG.conv1d(h, conv.weight, conv.bias, K=k, pad=(k - 1) // 2, compute_dtype=self.compute_dtype,
-                          out_dtype=torch.float32 if last else self.train_act_dtype)
+                          out_dtype=torch.float32 if last else self.compute_dtype, bias_before_bn=True)
             hb = AG.batch_norm_train(h, bn, (0, 1))  # channels-last (B, T, C): no transposes
             if not last:
                 hb = torch.tanh(hb)
