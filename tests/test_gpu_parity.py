@@ -411,8 +411,8 @@ def test_attention_vs_oracle(B, L, lens, dt, tol, cfg):
                                  (128, 233), (32, 488 * 3 + 7), (64, 131072), (32, 65536), (128, 32768),
                                  # register-resident frames: 104 (C = 32) / 72 (C = 64) output rows per tile
                                  (32, 104), (32, 105), (32, 24), (64, 72), (64, 73), (64, 16), (64, 72 * 5 - 1),
-                                 # wave-owned planes (resblock_pb3.hip): 184 (C = 128) / 424 (C = 64) output rows per tile
-                                 (128, 184), (128, 185), (128, 184 * 4 + 3), (64, 424), (64, 425), (64, 424 * 3 + 5)])
+                                 # wave-owned planes (resblock_pb3.hip): 200 (C = 128) / 488 (C = 64) output rows per tile
+                                 (128, 200), (128, 201), (128, 200 * 4 + 3), (64, 488), (64, 489), (64, 488 * 3 + 5)])
 @pytest.mark.parametrize("with_acc", [True, False])
 # cfg 0: the shipped dispatch (C = 32: register-resident frames); 80: any rb3_cfg != 0 keeps the LDS-frame
 # kernel (the A/B variants 80-87 of resblock_rr.hip are in the VO_ABLATIONS library)

@@ -1,14 +1,16 @@
 """Per-conv timeline of the k = 3 ResBlock in the wave-owned-plane form (csrc/resblock_pb3.hip) from s_memtime
 stamps.  Diagnostic library built here (never the product one):
 
-    hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -DVO_PB3_STAMPS \\
+    hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -mllvm -pragma-unroll-threshold=1000000 \\
+        -mllvm -amdgpu-mfma-vgpr-form=1 -DVO_PB3_STAMPS \\
         visual_onoma_to_wave_amd/csrc/resblock_pb3.hip visual_onoma_to_wave_amd/csrc/vo_runtime.cpp \\
         -o tools/probes/build/libpb3_stamps.so
     python tools/probes/pb3_stamps.py [C]
 
 Prints, for tiles 1-3 of workgroups 0-15 (median over waves and workgroups), the shader cycles of each conv's
-barrier, its three taps (tap 2 includes all but the last row tile's epilogue) and its tail.
-Ideal tap at C = 128: 64 steps x 2 MFMAs x 16 cycles = 2,048 (C = 64: 1,024).
+barrier, its phase 0 ("tap 0": tap 0), the two halves of phase 1 ("tap 1", "tap 2": taps 1 and 2 interleaved,
+with the epilogues) and its tail.  Ideal tap at C = 128 (14 row tiles): 56 steps x 2 MFMAs x 16 cycles = 1,792.
+(The stamped build is not the product code: its extra stores and waits cost ~10 % or more.)
 """
 import ctypes
 import os

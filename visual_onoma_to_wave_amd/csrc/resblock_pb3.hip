@@ -50,15 +50,15 @@ constexpr int PB_NSTW = 16, PB_NSTT = 4, PB_NPT = 30;  // stamp geometry: workgr
 constexpr int PB_HP = 8;     // LDS pad rows per side (dilation <= 8; a multiple of 8 keeps the swizzle)
 constexpr int PB_HALO = 12;  // valid rows lost per side: sum over the six convs of dil * (k - 1) / 2
 constexpr int pb_np(int C) { return C / 32; }
-// row tiles (16 rows) per wave: the frame is 16 NJ rows per row group.  C = 128: 13 (208-row frames, 184 output
-// rows: 88.5 % of the MFMA work is kept, against 90.6 % at 16); C = 64: 14 (448-row frames, 94.6 %).  At 16 the
-// accumulators, x2, the next window and the MRF accumulator rows exceed 512 registers, and the spill reloads'
-// vmcnt(0) waits drained every prefetch in flight (C = 128 0.65 -> 0.98 ms, C = 64 0.40 -> 0.72 ms)
+// row tiles (16 rows) per wave (even: phase 1 runs blocks of two): the frame is 16 NJ rows per row group.
+// C = 128: 14 (224-row frames, 200 output rows: 89.3 % of the MFMA work kept); C = 64: 16 (512-row frames, 488
+// output rows, 95.3 %).  One more block (C = 128: 16) exceeds 512 registers, and the spill reloads' vmcnt(0)
+// waits drain every prefetch in flight (measured 1.5x slower in an earlier layout)
 #ifndef VO_PB3_NJ128
-#define VO_PB3_NJ128 13
+#define VO_PB3_NJ128 14
 #endif
 #ifndef VO_PB3_NJ64
-#define VO_PB3_NJ64 14
+#define VO_PB3_NJ64 16
 #endif
 constexpr int pb_nj(int C) { return C == 128 ? VO_PB3_NJ128 : VO_PB3_NJ64; }
 constexpr int pb_f(int C) { return 16 * pb_nj(C) * (4 / pb_np(C)); }  // frame rows per tile
@@ -76,27 +76,8 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
   constexpr int NST = NJ * NP;                                 // (row tile, plane) steps per tap
   constexpr int NB = 10, DB = 8;                               // B-fragment ring / prefetch distance (steps)
   constexpr int NU = 18;                                       // taps per tile (6 convs x 3)
-#ifndef VO_PB3_LAG
-#define VO_PB3_LAG 1
-#endif
-  constexpr int LAG = VO_PB3_LAG;  // a row tile's epilogue runs during the steps of row tile j + LAG (A/B)
-  static_assert(RPS % 8 == 0 && NWV * RPS == F && NST >= 2 * NAP, "geometry");
-  // The next tile's window (NWV slots).  Slots 0 .. NW1-1 are loaded over the first two taps of stage 2's c1
-  // (the window is still being read there: registers only) and written, lrelu'd, in c2's first tap; slots
-  // NW1 .. NWV-1 are loaded in c2's first tap -- after the row tiles' residual MFMAs (plane 0, steps 0 .. 15)
-  // freed x2's registers -- and written in c2's last tap.  At C = 128 all 16 slots in flight beside x2 pushed
-  // the live registers past 512 (scratch spills); the MRF accumulator rows (ACC) are requested in c2's first
-  // tap too, two taps before they enter (identity MFMA or epilogue add) in its last.
-  // (every global load of a tap is issued after the tap's A pieces: vmcnt retires in issue order, so a
-  // load issued before an A piece would hold up the next tap's first MFMAs until it returned)
-#ifndef VO_PB3_NW1
-#define VO_PB3_NW1 16
-#endif
-  constexpr int NW1 = VO_PB3_NW1 < NWV ? VO_PB3_NW1 : NWV;
-  constexpr int WSP = (NST - 2 * NAP) / ((NW1 + 1) / 2);       // c1 taps 0 / 1: steps between window loads
-  constexpr int WSS = (NST - 2 * NAP) / NJ;                    // c2 tap 0: steps between requests / stores
-  constexpr int WS2 = NWV > NW1 ? (NST - 2 * NAP) / (NWV - NW1) : 1;  // c2 tap 2: steps between stores
-  static_assert(WSP >= 1 && WSS >= 1 && WS2 >= 1 && NW1 <= NJ && NWV - NW1 <= NJ, "window staging");
+  constexpr int BS = 4 * NP;                                   // phase-1 block: 2 taps x NP planes x 2 row tiles
+  static_assert(RPS % 8 == 0 && NWV * RPS == F && NJ % 2 == 0 && NST >= 4 * NAP, "geometry");
 
   const int T = a.T;
   const float slope = a.slope;
@@ -111,10 +92,11 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
   const int pw = w % NP, row0 = (w / NP) * 16 * NJ;  // the wave's plane and first frame row
   const int lr = lane & 15, lg = lane >> 4;
 
-  // ST (diagnostic builds): s_memtime at conv v's barrier (5v), its taps (5v + 1 + k) and its end (5v + 4),
-  // first PB_NSTT tiles of workgroups 0 .. PB_NSTW-1, written by lane 0 of each wave (vector stores)
+  // ST (diagnostic builds): s_memtime at conv v's barrier (5v), its phase 0 (5v + 1), phase 1 (5v + 2), the middle
+  // of phase 1 (5v + 3) and its end (5v + 4), first PB_NSTT tiles of workgroups 0 .. PB_NSTW-1, written by lane 0
+  // of each wave (vector stores)
   int st_tile = 0;
-  auto stamp = [&](int idx) {
+  auto stamp = [&](int idx) __attribute__((always_inline)) {
     if constexpr (ST) {
       if (blockIdx.x < PB_NSTW && st_tile < PB_NSTT && lane == 0)
         a.stamps[((blockIdx.x * 4 + w) * PB_NSTT + st_tile) * PB_NPT + idx] = __builtin_amdgcn_s_memtime();
@@ -135,34 +117,38 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
   }
 
   // ---- A fragments (as resblock_rw.hip): lane l holds W[tap][co][ci], co = 32pw + 8(lr>>2) + 4t + (lr&3),
-  // ci = 32s + 8lg .. +7; accumulator register i of co tile t is then channel 32pw + 8lg + 4t + i
+  // ci = 32s + 8lg .. +7; accumulator register i of co tile t is then channel 32pw + 8lg + 4t + i.
+  // Three tap slots (tap u in slot u % 3; 18 taps per tile): a conv's taps 1 and 2 run interleaved (phase 1),
+  // so both are resident while the next conv's tap 0 is fetched into the slot tap 0 freed
   const int aoff = ((32 * pw + 8 * (lr >> 2) + (lr & 3)) * C + 8 * lg) * (int)sizeof(bf16_t);
   const int afr = pw * NAP * 1024 + lane * 16;
   __amdgpu_buffer_rsrc_t rw[6];
 #pragma unroll
   for (int v = 0; v < 6; ++v) rw[v] = __builtin_amdgcn_make_buffer_rsrc((void*)a.w[v], (short)0, 3 * C * C * 2, 0x00020000);
-  bf16x8 A[2][NP][2];  // tap u's fragments in slot u & 1 (18 taps per tile: the parity carries over)
-  auto loadA_piece = [&](int u, int i) {
+  bf16x8 A[3][NP][2];
+  auto loadA_piece = [&](int u, int i) __attribute__((always_inline)) {
     const int uu = u % NU, v = uu / 3, k = uu % 3;
     const int s = i >> 1, t = i & 1;
     const int lo = FR ? afr + i * 1024 : aoff + t * 4 * C * 2 + s * 64;
-    A[uu & 1][s][t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw[v], lo, k * (C * C * 2), 0));
+    A[uu % 3][s][t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw[v], lo, k * (C * C * 2), 0));
   };
-  auto utt = [&](const bf16_t* p, int b) {  // one utterance of a (B, T, C) tensor: rows outside read 0
+  auto utt = [&](const bf16_t* p, int b) __attribute__((always_inline)) {  // one utterance of a (B, T, C) tensor: rows outside read 0
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (int64_t)b * T * C), (short)0, T * C * 2, 0x00020000);
   };
+  // op i of n spread over the steps [lo, lo + span) of a phase: does step jj carry it?
+  auto at = [](int jj, int lo, int span, int n, int i) __attribute__((always_inline)) { return jj == lo + i * span / n; };
 
   // ---- window staging: vector v = tid + 256 slot = (frame row xr + RPS slot, 16-byte column xc)
   const int xr = tid / VPR, xc = tid % VPR;
   const int xl = (xc >> 2) * PL + pb_off(xr + PB_HP, xc & 3);  // + slot * RPS rows (swizzle unchanged)
   u32x4 xw[NWV];
-  auto load_win = [&](int tl, int sl) {
+  auto load_win = [&](int tl, int sl) __attribute__((always_inline)) {
     const int b = tl / a.tiles_per_b;
     const int p0 = (tl - b * a.tiles_per_b) * BT - PB_HALO;
     // positions before 0 wrap to huge offsets and past T exceed the range: both read 0 (zero padding)
     xw[sl] = __builtin_amdgcn_raw_buffer_load_b128(utt(a.x, b), ((p0 + xr + RPS * sl) * C + xc * 8) * 2, 0, 0);
   };
-  auto store_win = [&](int sl) { *reinterpret_cast<u32x4*>(win + xl + sl * RPS * 32) = lrelu8(xw[sl], slope); };
+  auto store_win = [&](int sl) __attribute__((always_inline)) { *reinterpret_cast<u32x4*>(win + xl + sl * RPS * 32) = lrelu8(xw[sl], slope); };
 
 #pragma unroll
   for (int i = 0; i < NAP; ++i) loadA_piece(0, i);
@@ -185,20 +171,27 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
       ais[t][e] = (__bf16)(one ? 1.0f / a.out_scale : 0.0f);
     }
 
-  // One conv of the block over the frame: 3 taps x NP input planes x 16 row tiles; steps plane-major inside
-  // taps 0 / 1 and row-tile-major in tap 2, whose row tile j is final after its NP steps and runs its
-  // epilogue (four parts) under row tile j + 1's MFMAs.  Each step: one B-fragment read (DB steps ahead),
-  // two MFMAs, and one piece of the side work (the next tap's A pieces, the hook).
-  auto conv = [&](auto vc, auto hook, auto post, auto extra) {
+  // One conv of the block over the frame, in two phases:
+  //   phase 0: tap 0, plane-major over the NJ row tiles (NST steps);
+  //   phase 1: taps 1 and 2 interleaved, in blocks of 2 row tiles (plane, tap, row tile inner: the two row
+  //            tiles alternate, so no MFMA depends on the one just issued); a block's accumulators are final
+  //            after its BS steps and its epilogue (8 parts) runs under the next block's MFMAs -- twice the MFMA
+  //            time a last-tap-only epilogue had (the k = 3 block's six epilogues per tile were VALU-bound:
+  //            0.50 MFMA busy, 2.5 VALU per MFMA).
+  // Each step: one B-fragment read (DB steps ahead), two MFMAs, and the side work (A pieces: taps 1 / 2 in
+  // phase 0, the next conv's tap 0 in phase 1; the hook).
+  auto conv = [&](auto vc, auto hook, auto post, auto extra) __attribute__((always_inline)) {
     constexpr int V = decltype(vc)::value, PH = V & 1, S = V >> 1;
     const bf16_t* src = PH ? t1 : win;
     const int step = PH ? 1 : a.dil[S];
     int lro = lr, lgo = lg;
     asm volatile("" : "+v"(lro), "+v"(lgo));
-    auto rt = [&](int k, int jj) { return k < 2 ? jj % NJ : jj / NP; };
-    auto pl = [&](int k, int jj) { return k < 2 ? jj / NJ : jj % NP; };
-    auto readB = [&](int q) {
-      const int k = q / NST, j = rt(k, q % NST), s = pl(k, q % NST);
+    // step q of the conv (0 .. 3 NST) -> (tap, row tile, plane)
+    auto dk = [&](int q) __attribute__((always_inline)) { return q < NST ? 0 : 1 + (((q - NST) % BS) / 2) % 2; };
+    auto dj = [&](int q) __attribute__((always_inline)) { return q < NST ? q % NJ : 2 * ((q - NST) / BS) + (q - NST) % 2; };
+    auto ds = [&](int q) __attribute__((always_inline)) { return q < NST ? q / NJ : ((q - NST) % BS) / 4; };
+    auto readB = [&](int q) __attribute__((always_inline)) {
+      const int k = dk(q), j = dj(q), s = ds(q);
       const bf16_t* base = src + (s >> 1) * 2 * PL + pb_off(PB_HP + (k - 1) * step + row0 + lro, lgo);
       Bq[q % NB] = *reinterpret_cast<const bf16x8*>(base + (s & 1) * PL + j * 512);
     };
@@ -206,20 +199,23 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     const f32x4 bz0 = bz[0], bz1 = bz[1];
 #pragma unroll
     for (int q = 0; q < DB; ++q) readB(q);
+    auto phase = [&](auto phc) __attribute__((always_inline)) {
+      constexpr int ph = decltype(phc)::value, n = ph ? 2 * NST : NST;
+      stamp(5 * V + 1 + ph);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int u = 3 * V + k;
-      stamp(5 * V + 1 + k);
-      const bf16x8(&Ak)[NP][2] = A[u & 1];
-#pragma unroll
-      for (int jj = 0; jj < NST; ++jj) {
-        const int q = k * NST + jj;
-        const int j = rt(k, jj), s = pl(k, jj);
+      for (int jj = 0; jj < n; ++jj) {
+        const int q = ph * NST + jj;
+        const int k = dk(q), j = dj(q), s = ds(q);
+        if (ST && ph == 1 && jj == NST) stamp(5 * V + 3);
         if (q + DB < 3 * NST) readB(q + DB);
-        if (jj < 2 * NAP && jj % 2 == 0) loadA_piece(u + 1, jj / 2);
-        hook(k, jj);
+        if (jj % 2 == 0) {
+          if (ph == 0 && jj < 4 * NAP) loadA_piece(3 * V + 1 + jj / (2 * NAP), (jj / 2) % NAP);
+          if (ph == 1 && jj < 2 * NAP) loadA_piece(3 * V + 3, jj / 2);
+        }
+        hook(ph, jj);
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 b = Bq[q % NB];
+        const bf16x8(&Ak)[NP][2] = A[(3 * V + k) % 3];
         if (k == 0 && s == 0) {
           acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][0], b, bz0, 0, 0, 0);
           acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, bz1, 0, 0, 0);
@@ -228,16 +224,19 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
           acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ak[s][1], b, acc[1][j], 0, 0, 0);
         }
         extra(k, j, s);
-        if (k == 2 && jj >= LAG * NP) {  // row tile jj / NP - LAG's epilogue, 4 / NP of its 4 parts per step
-          const int r = jj % NP, j0 = jj / NP - LAG;
+        if (ph == 1 && jj >= BS) {  // the previous block's epilogue: 8 parts over this block's BS steps
+          const int bb = jj / BS - 1, r = jj % BS;
 #pragma unroll
-          for (int p = r * 4 / NP; p < (r + 1) * 4 / NP; ++p) post(j0, p);
+          for (int p = 0; p < 8; ++p)
+            if (r == p * BS / 8) post(2 * bb + p / 4, p % 4);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
 #pragma unroll
-    for (int q = 0; q < 4 * LAG; ++q) post(NJ - LAG + q / 4, q % 4);
+    for (int p = 0; p < 8; ++p) post(NJ - 2 + p / 4, p % 4);
     stamp(5 * V + 4);
   };
 
@@ -247,8 +246,19 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
     const int t0 = (tile - b * a.tiles_per_b) * BT;
     const int p0 = t0 - PB_HALO;  // position of frame row 0
     const int ntile = tile + 1 < tile_end ? tile + 1 : tile;
-    // (the epilogues' zero-padding masks are branch-free selects: skipping them in interior tiles put a branch
-    // per row tile into the unrolled loop, and hipcc copied eight accumulators out of the AGPRs at every join)
+    // Zero padding: the epilogues write every frame row unmasked (a mask per row tile cost 5 of its ~38 vector
+    // instructions, in the VALU-bound epilogue phase; a branch around it made hipcc copy eight accumulators out
+    // of the AGPRs at every join); in the tiles whose frame crosses an utterance end, the rows outside [0, T) of
+    // the wave's own plane are zeroed after the epilogue, before the barrier that publishes them
+    const bool edge = p0 < 0 || p0 + F > T;
+    const int zlo = p0 < 0 ? -p0 : 0, zhi = T - p0;  // frame rows [zlo, zhi) are inside the utterance
+    auto zero_rows = [&](bf16_t* buf) __attribute__((always_inline)) {
+      if (!edge) return;
+      for (int f = row0 + lane; f < row0 + 16 * NJ; f += 64)
+        if (f < zlo || f >= zhi)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) *reinterpret_cast<u32x4*>(buf + pw * PL + pb_off(f + PB_HP, q)) = u32x4{0u, 0u, 0u, 0u};
+    };
     const __amdgpu_buffer_rsrc_t rsx = utt(a.x, b);
     const __amdgpu_buffer_rsrc_t rsa = utt(ACC ? a.acc : a.x, b);
 
@@ -257,7 +267,7 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
 
     uint32_t pv[4];
     // P1 epilogue: T1 = lrelu(acc) (bias in acc), frame rows outside [0, T) = 0 (c2's zero padding)
-    auto p1_post = [&](int j, int p) {
+    auto p1_post = [&](int j, int p) __attribute__((always_inline)) {
       const int t = p >> 1, e = 2 * (p & 1);
 #if VO_PB3_PK
       pv[p] = lrelu_pk(acc[t][j][e], acc[t][j][e + 1], slope);
@@ -265,17 +275,15 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
       pv[p] = pk_bf16(lrelu_max(acc[t][j][e], slope), lrelu_max(acc[t][j][e + 1], slope));
 #endif
       if (p == 3) {
-        const int f = row0 + 16 * j + lr, pos = p0 + f;
-        u32x4 v = u32x4{pv[0], pv[1], pv[2], pv[3]};
-        v &= (unsigned)pos < (unsigned)T ? 0xffffffffu : 0u;  // branch-free (see below)
-        *reinterpret_cast<u32x4*>(t1 + pw * PL + pb_off(f + PB_HP, lg)) = v;
+        const int f = row0 + 16 * j + lr;
+        *reinterpret_cast<u32x4*>(t1 + pw * PL + pb_off(f + PB_HP, lg)) = u32x4{pv[0], pv[1], pv[2], pv[3]};
       }
     };
     // P2 epilogue of stages 0 / 1: x_{s+1} = bf16(acc) kept in xres; lrelu(x_{s+1}) into the window (rows
     // outside [0, T) = 0: the next c1's zero padding).  The lrelu'd copy is taken from the fp32 sum (one
     // multiply and max per value, no unpacking of the rounded bf16 -- as resblock3.hip's epilogues)
     uint32_t lv[4];
-    auto p2_mid_post = [&](int j, int p) {
+    auto p2_mid_post = [&](int j, int p) __attribute__((always_inline)) {
       const int e = 2 * p;
       const float a0 = acc[e >> 2][j][e & 3], a1 = acc[e >> 2][j][(e & 3) + 1];
       pv[p] = pk_bf16(a0, a1);
@@ -285,76 +293,80 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
       lv[p] = pk_bf16(lrelu_max(a0, slope), lrelu_max(a1, slope));
 #endif
       if (p == 3) {
-        const int f = row0 + 16 * j + lr, pos = p0 + f;
+        const int f = row0 + 16 * j + lr;
         xres[j] = u32x4{pv[0], pv[1], pv[2], pv[3]};
-        u32x4 v = u32x4{lv[0], lv[1], lv[2], lv[3]};
-        v &= (unsigned)pos < (unsigned)T ? 0xffffffffu : 0u;
-        *reinterpret_cast<u32x4*>(win + pw * PL + pb_off(f + PB_HP, lg)) = v;
+        *reinterpret_cast<u32x4*>(win + pw * PL + pb_off(f + PB_HP, lg)) = u32x4{lv[0], lv[1], lv[2], lv[3]};
       }
     };
     // the residual (and acc_in / out_scale) through identity MFMAs at plane 0's step of row tile j:
     // the lane's residual vector of row tile j IS a B fragment of its own plane
-    auto res_extra = [&](int k, int j, int s) {
+    auto res_extra = [&](int k, int j, int s) __attribute__((always_inline)) {
       if (s != 0 || k != 0) return;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aid[t], __builtin_bit_cast(bf16x8, xres[j]), acc[t][j], 0, 0, 0);
     };
-    auto no_hook = [&](int, int) {};
-    auto no_extra = [&](int, int, int) {};
+    auto no_hook = [&](int, int) __attribute__((always_inline)) {};
+    auto no_extra = [&](int, int, int) __attribute__((always_inline)) {};
 
-    // ---- stage 0, c1 (dilation dil[0]) over lrelu x; x's rows of this wave's plane requested in taps 1 / 2
-    // (L2 hits: the window staging just read them), the residual of stage 0's c2
-    auto s0_hook = [&](int k, int jj) {
-      constexpr int H = (NJ + 1) / 2, RSP = (NST - 2 * NAP) / H;  // row tiles 0 .. H-1 in tap 1, the rest in tap 2
-      if (k == 0 || jj < 2 * NAP || (jj - 2 * NAP) % RSP != 0) return;
-      const int i = (jj - 2 * NAP) / RSP;
-      const int j = (k - 1) * H + i;
-      if (i >= H || j >= NJ) return;
-      xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
+    // ---- stage 0, c1 (dilation dil[0]) over lrelu x; x's rows of this wave's plane requested in phase 1 (L2
+    // hits: the window staging just read them), the residual of stage 0's c2
+    auto s0_hook = [&](int ph, int jj) __attribute__((always_inline)) {
+      if (ph != 1 || jj < 2 * NAP) return;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (at(jj, 2 * NAP, 2 * NST - 2 * NAP, NJ, j))
+          xres[j] = __builtin_amdgcn_raw_buffer_load_b128(rsx, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
     };
     conv(std::integral_constant<int, 0>{}, s0_hook, p1_post, no_extra);
+    zero_rows(t1);
     stamp(5);
     lds_barrier();
     conv(std::integral_constant<int, 1>{}, no_hook, p2_mid_post, res_extra);
+    zero_rows(win);
     stamp(10);
     lds_barrier();
     conv(std::integral_constant<int, 2>{}, no_hook, p1_post, no_extra);
+    zero_rows(t1);
     stamp(15);
     lds_barrier();
     conv(std::integral_constant<int, 3>{}, no_hook, p2_mid_post, res_extra);
+    zero_rows(win);
     stamp(20);
     lds_barrier();
 
-    // ---- stage 2: c1 loads the next tile's window into registers (taps 0 / 1) and, for ACC == 2, the MRF
-    // accumulator rows of row tiles 0 .. 7 (tap 2)
-    auto s2a_hook = [&](int k, int jj) {
-      if (jj < 2 * NAP) return;
-      const int i = (jj - 2 * NAP) / WSP;
-      if (k < 2 && (jj - 2 * NAP) % WSP == 0 && i < (NW1 + 1) / 2 && k * ((NW1 + 1) / 2) + i < NW1)
-        load_win(ntile, k * ((NW1 + 1) / 2) + i);
+    // ---- stage 2: c1 loads the next tile's window into registers (phase 1, after the A pieces: vmcnt retires in
+    // issue order, so a load issued before an A piece would hold up the next phase's first MFMAs)
+    auto s2a_hook = [&](int ph, int jj) __attribute__((always_inline)) {
+      if (ph != 1 || jj < 2 * NAP) return;
+#pragma unroll
+      for (int sl = 0; sl < NWV; ++sl)
+        if (at(jj, 2 * NAP, 2 * NST - 2 * NAP, NWV, sl)) load_win(ntile, sl);
     };
     conv(std::integral_constant<int, 4>{}, s2a_hook, p1_post, no_extra);
+    zero_rows(t1);
     stamp(25);
     lds_barrier();  // T1 complete; the window is dead until the next tile
 
-    // ---- stage 2, c2: y = (x2 + c2) * out_scale (+ acc) -> HBM; the next window written lrelu'd (taps 0 / 1)
+    // ---- stage 2, c2: y = (x2 + c2) * out_scale (+ acc) -> HBM.  Phase 0, after its A pieces: the next window
+    // written lrelu'd, and the MRF accumulator rows requested (x2's registers are free after the residual
+    // MFMAs of plane 0); they enter in phase 1 (identity MFMA, ACC == 2) or the epilogue (ACC == 1)
     const int valid = min(BT, T - t0);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.y + ((int64_t)b * T + t0) * C), (short)0, valid * C * (int)sizeof(bf16_t), 0x00020000);
-    auto s2b_hook = [&](int k, int jj) {
-      if (jj < 2 * NAP) return;
-      if (k == 0 && (jj - 2 * NAP) % WSS == 0) {
-        const int i = (jj - 2 * NAP) / WSS;
-        if (i < NW1) store_win(i);
-        if (i < NWV - NW1) load_win(ntile, NW1 + i);
-        if constexpr (ACC != 0)
-          if (i < NJ) ares[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * i + lr) * C + cofs) * 2, 0, 0);
+    auto s2b_hook = [&](int ph, int jj) __attribute__((always_inline)) {
+      if (ph != 0 || jj < 4 * NAP) return;
+#pragma unroll
+      for (int sl = 0; sl < NWV; ++sl)
+        if (at(jj, 4 * NAP, NST - 4 * NAP, NWV, sl)) store_win(sl);
+      if constexpr (ACC != 0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          if (at(jj, 4 * NAP, NST - 4 * NAP, NJ, j))
+            ares[j] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ((p0 + row0 + 16 * j + lr) * C + cofs) * 2, 0, 0);
       }
-      if (k == 2 && NWV > NW1 && (jj - 2 * NAP) % WS2 == 0 && (jj - 2 * NAP) / WS2 < NWV - NW1)
-        store_win(NW1 + (jj - 2 * NAP) / WS2);
     };
-    auto s2b_extra = [&](int k, int j, int s) {
+    auto s2b_extra = [&](int k, int j, int s) __attribute__((always_inline)) {
       if (s != 0) return;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -366,7 +378,7 @@ __global__ void __launch_bounds__(256, 1) mrf_pb3_kernel(Pb3Args a) {
       }
     };
     const float osc = a.out_scale;
-    auto s2b_post = [&](int j, int p) {
+    auto s2b_post = [&](int j, int p) __attribute__((always_inline)) {
       float q[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
