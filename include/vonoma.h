@@ -165,6 +165,20 @@ int vo_layernorm_bwd_ex(const void* x, int x_dtype, const void* res, int res_dty
                         const void* gy2, const float* gamma, const int32_t* lens, int B, int T, int D, float eps,
                         void* gh, float* gh32, float* dgamma, float* dbeta, void* workspace, void* stream);
 
+/* Training FFT blocks (round 6): the sublayer output's dropout (scripts/transformer/SubLayers.py:51,88) fused
+ * into the LayerNorm that follows it.  Forward: y = LN(dropout(x) + res) * gamma + beta (pad rows 0), element i
+ * of x kept iff it is kept by vo_dropout(p, seed, salt) on the same tensor, scaled by 1 / (1 - p); y16 (may be
+ * NULL; fp32 y only) its bf16 copy.  x / res / y: fp32 / fp32 / fp32, bf16 / fp32 / fp32, bf16 / bf16 / bf16.
+ * Backward: gh = dL/dx (through the mask, x_dtype), gres = dL/dres (res_dtype), gy2 (bf16, may be NULL) the
+ * gradient of y16 added to gy; dgamma / dbeta as vo_layernorm_bwd (same workspace).  B*T*D < 2^32. */
+int vo_layernorm_drop(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
+                      const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y, int y_dtype,
+                      void* y16, float p, const int64_t* seed, unsigned salt, void* stream);
+int vo_layernorm_bwd_drop(const void* x, int x_dtype, const void* res, int res_dtype, const void* gy, int gy_dtype,
+                          const void* gy2, const float* gamma, const int32_t* lens, int B, int T, int D, float eps,
+                          float p, const int64_t* seed, unsigned salt, void* gh, void* gres, float* dgamma,
+                          float* dbeta, void* workspace, void* stream);
+
 /* ------------------------------------------------------------------ attention
  * Scaled dot-product attention with key padding, H heads of d_k = D/H, over the fused
  * qkv activations (B, L, 3D) (columns [q | k | v], head h at h*d_k) -> out (B, L, D)

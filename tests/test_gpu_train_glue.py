@@ -307,3 +307,59 @@ def test_dropout_graph_replays_draw_new_masks():
         torch.cuda.synchronize()
         masks.append(y != 0)
     assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+
+
+@pytest.mark.parametrize("xdt,rdt,dual", [(torch.bfloat16, torch.float32, True), (torch.float32, torch.float32, False),
+                                          (torch.bfloat16, torch.bfloat16, False)])
+@pytest.mark.parametrize("B,T,D,p,use", [(32, 512, 256, 0.2, "both"), (3, 37, 256, 0.5, "both"), (32, 12, 256, 0.2, "y"),
+                                         (2, 5, 512, 0.1, "copy")])
+def test_layernorm_dropout_fused(B, T, D, p, use, xdt, rdt, dual):
+    """autograd.layernorm_drop (the training FFT block's sublayer dropout inside its LayerNorm kernels) vs the fp32
+    autograd of LayerNorm(mask * x / (1 - p) + res) + pad-row zeroing, the mask taken from vo_dropout with the SAME
+    (seed, salt) on a tensor of ones: the forward, the x gradient's zero pattern -- exactly the dropout mask (a
+    round-5 fusion attempt got it wrong and was dropped) -- and values, the residual / gamma / beta gradients.
+    use: which outputs feed the loss ("copy": only the bf16 copy, as the last decoder layer)."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import autograd as AG
+    from visual_onoma_to_wave_amd import ops
+    if use == "copy" and not dual:
+        pytest.skip("the copy exists in the dual form only")
+    g = torch.Generator(device="cuda").manual_seed(B * T + D)
+    x = torch.randn(B, T, D, device="cuda", generator=g).to(xdt)
+    res = torch.randn(B, T, D, device="cuda", generator=g).to(rdt)
+    gam = (1.0 + 0.1 * torch.randn(D, device="cuda", generator=g))
+    bet = 0.1 * torch.randn(D, device="cuda", generator=g)
+    lens = torch.randint(1, T + 1, (B,), device="cuda", generator=g).int()
+    AG.begin_dropout_step(x.device)
+    seed = AG._DROP["seed"]
+    salt = AG._DROP["site"] + 1  # the salt layernorm_drop takes next
+    mask = ops.dropout(torch.ones(B, T, D, device="cuda"), p, seed, salt) != 0  # vo_dropout's draw
+    xi, ri = x.float().requires_grad_(True), res.float().requires_grad_(True)
+    gi, bi = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    yref = F.layer_norm(xi * mask * (1.0 / (1.0 - p)) + ri, (D,), gi, bi, 1e-5)
+    yref = yref.masked_fill((torch.arange(T, device="cuda")[None, :] >= lens.long()[:, None])[..., None], 0.0)
+    gy = torch.randn(B, T, D, device="cuda", generator=g)
+    gy16 = torch.randn(B, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    gtot = (gy if use != "copy" else 0.0) + (gy16.float() if (dual and use != "y") else 0.0)
+    rx, rr, rg, rb = torch.autograd.grad(yref, (xi, ri, gi, bi), gtot)
+    xc, rc = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+    gc, bc = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    out = AG.layernorm_drop(xc, rc, gc, bc, lens, p, dual)
+    y, y16 = out if dual else (out, None)
+    assert AG._DROP["site"] == salt
+    tol = 1e-5 if xdt == torch.float32 and rdt == torch.float32 else 1e-2
+    assert y.dtype == rdt and rel_l2(y.detach().float().cpu(), yref.detach().cpu()) < (1e-5 if rdt == torch.float32 else 1e-2)
+    if dual:
+        assert torch.equal(y16.detach(), y.detach().to(torch.bfloat16))
+    outs, grads = [], []
+    if use != "copy":
+        outs.append(y), grads.append(gy.to(y.dtype))
+    if dual and use != "y":
+        outs.append(y16), grads.append(gy16)
+    dx, dr, dg, db = torch.autograd.grad(outs, (xc, rc, gc, bc), grads)
+    live = (torch.arange(T, device="cuda")[None, :] < lens.long()[:, None])[..., None].expand(B, T, D)
+    # the x gradient is zero exactly where the mask dropped (or the row is padding): the same mask both ways
+    assert torch.equal((dx != 0) | ~live, mask | ~live)
+    assert dx.dtype == xdt and dr.dtype == rdt
+    assert rel_l2(dx.float().cpu(), rx.cpu()) < tol and rel_l2(dr.float().cpu(), rr.cpu()) < tol
+    assert rel_l2(dg.cpu(), rg.cpu()) < max(tol, 1e-5) and rel_l2(db.cpu(), rb.cpu()) < max(tol, 1e-5)

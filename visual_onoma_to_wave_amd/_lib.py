@@ -122,6 +122,12 @@ _SIGNATURES = {
     "vo_layernorm_bwd_ex": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
+    "vo_layernorm_drop": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                  c_int, c_float, c_void_p, c_int, c_void_p, c_float, c_void_p, ctypes.c_uint,
+                                  c_void_p]),
+    "vo_layernorm_bwd_drop": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_int, c_int, c_int, c_float, c_float, c_void_p, ctypes.c_uint,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vo_attention": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float,
                              c_void_p, c_void_p]),
     "vo_attention_bwd_workspace_size": (ctypes.c_int64, [c_int, c_int, c_int]),

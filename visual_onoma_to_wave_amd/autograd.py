@@ -348,6 +348,42 @@ def layernorm_dual(x, res, g, b, lens=None):
     return LayerNormDualFn.apply(x, res, g, b, lens)
 
 
+class LayerNormDropFn(torch.autograd.Function):
+    """The training FFT block's sublayer dropout fused into the LayerNorm after it (round 6): y = LN(dropout_p(x) +
+    res) * g + b, pad rows zeroed; x the sublayer output (before its dropout), res the residual stream.  dual
+    (fp32 res, bf16 compute): returns (y fp32, its bf16 copy y16) as LayerNormDualFn; else y in res's dtype.  The
+    mask is vo_dropout's for the same (seed, salt) -- recomputed in the backward kernel, no mask tensor."""
+
+    @staticmethod
+    def forward(ctx, x, res, g, b, lens, p, seed, salt, dual):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, res, g, lens, seed)
+        ctx.p, ctx.salt, ctx.dual = p, salt, dual
+        return ops.layernorm_drop(x.contiguous(), g.detach().float().contiguous(), b.detach().float().contiguous(),
+                                  res.contiguous(), p, seed, salt, lens=lens, with_bf16=dual)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        x, res, g, lens, seed = ctx.saved_tensors
+        gy, gy16 = (grads[0], grads[1]) if ctx.dual else (grads[0], None)
+        if gy is None and gy16 is None:
+            return (None,) * 9
+        if gy is None:  # only the copy was read (the last decoder layer feeds mel_linear its y16)
+            gy, gy16 = gy16, None
+        gy2 = None if gy16 is None else gy16.contiguous()
+        if gy2 is not None and (gy2.dtype != torch.bfloat16 or gy.dtype != torch.float32):
+            gy, gy2 = gy.float() + gy2.float(), None
+        gh, gres, gg, gb = ops.layernorm_bwd_drop(x.contiguous(), gy.contiguous(), g.detach().float().contiguous(),
+                                                  res.contiguous(), ctx.p, seed, ctx.salt, lens=lens, gy2=gy2)
+        return gh, gres, gg.to(g.dtype), gb.to(g.dtype), None, None, None, None, None
+
+
+def layernorm_drop(x, res, g, b, lens, p, dual):
+    """LN(dropout_p(x) + res) in one kernel each way; dual: (y fp32, y16) as layernorm_dual."""
+    seed, salt = _dropout_seed_salt(x.device)
+    return LayerNormDropFn.apply(x, res, g, b, lens, float(p), seed, salt, dual)
+
+
 class DropoutFn(torch.autograd.Function):
     """Training dropout on HIP (vo_dropout): the keep mask is a hash of (seed, site, element index), so
     the backward re-applies it to the gradient from the saved seed -- no mask tensor."""
@@ -389,12 +425,18 @@ def dropout(x, p, training=True):
     xc = x.contiguous()
     if xc.data_ptr() % 16:
         xc = xc.clone()
-    seed = _DROP["seed"]
-    if seed is None or seed.device != x.device:
-        seed, salt = torch.randint(1, 2 ** 62, (1,), device=x.device, dtype=torch.int64), 0
-    else:
-        salt = _DROP["site"] = _DROP["site"] + 1
+    seed, salt = _dropout_seed_salt(x.device)
     return DropoutFn.apply(xc, float(p), seed, salt)
+
+
+def _dropout_seed_salt(device):
+    """(device seed, salt) of the next dropout site: the step's seed salted by the site's index, or a fresh seed
+    when no step seed is set (begin_dropout_step)."""
+    seed = _DROP["seed"]
+    if seed is None or seed.device != device:
+        return torch.randint(1, 2 ** 62, (1,), device=device, dtype=torch.int64), 0
+    _DROP["site"] = _DROP["site"] + 1
+    return seed, _DROP["site"]
 
 
 class LengthRegulateFn(torch.autograd.Function):

@@ -4,6 +4,8 @@
 // (scripts/transformer/Layers.py:25,28), and the VariancePredictor LayerNorms
 // (scripts/model/modules.py:197-206).  HBM-bound: reads x (+res), writes y.
 
+#include <algorithm>
+
 #include "vo_common.h"
 
 namespace vo {
@@ -11,12 +13,22 @@ namespace vo {
 // DUAL (round 4): a bf16 copy of y beside it (y16) -- the next conv of the "mixed" decoder, whose
 // residual stream is fp32, reads the copy: half the bytes per re-read of its input tiles, and the same
 // bits as the conv's own fp32 -> bf16 staging (round to nearest even)
+// Dropout of x in the same pass (round 6, training: the sublayer output's nn.Dropout before the residual add,
+// scripts/transformer/SubLayers.py:51,88): x_i kept iff drop_hash(seed, salt, i) >= thr (i = the flat element
+// index -- the mask vo_dropout would draw for the same (seed, salt)), then scaled by 1 / (1 - p).
+struct LnDrop {
+  const int64_t* seed;  // nullptr: no dropout
+  uint32_t salt, thr;
+  float scale;
+};
+
 template <typename TX, typename TR, typename TY, int NPL, bool DUAL = false>
 __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x, const TR* __restrict__ res,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         const int32_t* __restrict__ lens, int B, int T,
-                                                        float eps, TY* __restrict__ y, bf16_t* __restrict__ y16) {
+                                                        float eps, TY* __restrict__ y, bf16_t* __restrict__ y16,
+                                                        LnDrop dr = LnDrop{nullptr, 0u, 0u, 1.f}) {
   constexpr int D = NPL * 64;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -34,10 +46,17 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x
     return;
   }
   float v[NPL];
+  uint32_t s0 = 0, s1 = 0;
+  if (dr.seed) drop_keys(dr.seed, dr.salt, s0, s1);
 #pragma unroll
   for (int i = 0; i < NPL; i += 4) {
     float q[4];
     load4(x + row * D + c0 + i, q);
+    if (dr.seed) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        q[e] = drop_hash(s0, s1, (uint32_t)(row * D + c0 + i + e)) >= dr.thr ? q[e] * dr.scale : 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[i + e] = q[e];
     if (res) {
@@ -69,15 +88,16 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const TX* __restrict__ x
 
 template <typename TX, typename TR, typename TY, bool DUAL = false>
 static int ln_launch(const void* x, const void* res, const float* g, const float* bt, const int32_t* lens,
-                     int B, int T, int D, float eps, void* y, hipStream_t st, void* y16 = nullptr) {
+                     int B, int T, int D, float eps, void* y, hipStream_t st, void* y16 = nullptr,
+                     LnDrop dr = LnDrop{nullptr, 0u, 0u, 1.f}) {
   const int64_t rows = (int64_t)B * T;
   dim3 grid((unsigned)((rows + 3) / 4));
   if (D == 256)
     hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 4, DUAL>), grid, dim3(256), 0, st, (const TX*)x,
-                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16);
+                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16, dr);
   else
     hipLaunchKernelGGL((layernorm_kernel<TX, TR, TY, 8, DUAL>), grid, dim3(256), 0, st, (const TX*)x,
-                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16);
+                       (const TR*)res, g, bt, lens, B, T, eps, (TY*)y, (bf16_t*)y16, dr);
   VO_RETURN_LAUNCH();
 }
 
@@ -106,8 +126,9 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
                                                              const float* __restrict__ gamma,
                                                              const int32_t* __restrict__ lens, int B, int T,
                                                              float eps, TX* __restrict__ gh,
-                                                             float* __restrict__ gh32,
-                                                             float* __restrict__ partial) {
+                                                             TR* __restrict__ gres,
+                                                             float* __restrict__ partial,
+                                                             LnDrop dr = LnDrop{nullptr, 0u, 0u, 1.f}) {
   constexpr int D = NPL * 64;
   __shared__ float red[LN_BWD_NW][2][D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -122,6 +143,10 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
   }
   const int64_t row0 = ((int64_t)blockIdx.x * LN_BWD_NW + wv) * LN_BWD_RPW;
   float v[LN_BWD_RPW][NPL], dy[LN_BWD_RPW][NPL];
+  // (the dropout keys are named apart from the row sums s1 / s2 below: shadowed, the mask of the x gradient
+  // was drawn with a row sum as its key -- how a fused LayerNorm + dropout went wrong in round 5)
+  uint32_t dk0 = 0, dk1 = 0;
+  if (dr.seed) drop_keys(dr.seed, dr.salt, dk0, dk1);
   bool live[LN_BWD_RPW];
 #pragma unroll
   for (int r = 0; r < LN_BWD_RPW; ++r) {
@@ -137,6 +162,11 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
     for (int i = 0; i < NPL; i += 4) {
       float q[4], e[4], d[4];
       load4(x + rr * D + c0 + i, q);
+      if (dr.seed) {  // the forward's dropout of x, recomputed
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          q[k] = drop_hash(dk0, dk1, (uint32_t)(rr * D + c0 + i + k)) >= dr.thr ? q[k] * dr.scale : 0.f;
+      }
       if (res)
         load4(res + rr * D + c0 + i, e);
       else
@@ -188,8 +218,13 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = sc * (g[i + e] * dy[r][i + e] - m1 - v[r][i + e] * m2);
+      if (gres) store4(gres + row * D + c0 + i, o);  // res: the gradient of x + res as it is
+      if (dr.seed) {  // x: through its dropout
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = drop_hash(dk0, dk1, (uint32_t)(row * D + c0 + i + e)) >= dr.thr ? o[e] * dr.scale : 0.f;
+      }
       store4(gr + i, o);
-      if (gh32) store4(gh32 + row * D + c0 + i, o);
     }
   }
 #pragma unroll
@@ -244,15 +279,18 @@ __global__ void __launch_bounds__(1024) ln_partial_sum_kernel(const float* __res
 template <typename TX, typename TG, typename TR = TX>
 static int ln_bwd_launch(const void* x, const void* res, const void* gy, const float* g, const int32_t* lens,
                          int B, int T, int D, float eps, void* gh, float* dgamma, float* dbeta, float* ws,
-                         hipStream_t st, const void* gy2 = nullptr, float* gh32 = nullptr) {
+                         hipStream_t st, const void* gy2 = nullptr, void* gres = nullptr,
+                         LnDrop dr = LnDrop{nullptr, 0u, 0u, 1.f}) {
   const int64_t rows = (int64_t)B * T;
   const int nblk = (int)((rows + LN_BWD_NW * LN_BWD_RPW - 1) / (LN_BWD_NW * LN_BWD_RPW));
   if (D == 256)
     hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TR, TG, 4>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
-                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, gh32, ws);
+                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, (TR*)gres,
+                       ws, dr);
   else
     hipLaunchKernelGGL((layernorm_bwd_kernel<TX, TR, TG, 8>), dim3(nblk), dim3(1024), 0, st, (const TX*)x,
-                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, gh32, ws);
+                       (const TR*)res, (const TG*)gy, (const bf16_t*)gy2, g, lens, B, T, eps, (TX*)gh, (TR*)gres,
+                       ws, dr);
   hipLaunchKernelGGL(ln_partial_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, st, (const float*)ws, nblk,
                      2 * D, dgamma, dbeta);
   VO_RETURN_LAUNCH();
@@ -343,5 +381,74 @@ extern "C" int vo_layernorm_bwd_ex(const void* x, int x_dtype, const void* res, 
     return vo_layernorm_bwd(x, res, x_dtype, gy, gy_dtype, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, workspace,
                             stream);
   vo_set_error("layernorm_bwd_ex: unsupported dtype combination (bf16 x with fp32 res, or equal x / res without gy2 / gh32)");
+  return VO_ERR_INVALID;
+}
+
+// ---- round 6: the training FFT blocks' dropout fused into their LayerNorms (x = the sublayer output before its
+// dropout).  Forward: y = LN(dropout(x) + res) (+ its bf16 copy y16 when y is fp32 and y16 != NULL).  Backward:
+// gh = d/dx (through the mask), gres = d/dres (both 0 on pad rows), the dropout mask recomputed from (seed, salt).
+static LnDrop ln_drop(float p, const int64_t* seed, unsigned salt) {
+  LnDrop d;
+  d.seed = seed;
+  d.salt = salt;
+  d.thr = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+  d.scale = 1.f / (1.f - p);
+  return d;
+}
+
+extern "C" int vo_layernorm_drop(const void* x, int x_dtype, const void* res, int res_dtype, const float* gamma,
+                                 const float* beta, const int32_t* lens, int B, int T, int D, float eps, void* y,
+                                 int y_dtype, void* y16, float p, const int64_t* seed, unsigned salt, void* stream) {
+  VO_CHECK_ARG(x && res && gamma && beta && y && seed, "layernorm_drop: null pointer");
+  VO_CHECK_ARG(D == 256 || D == 512, "layernorm_drop: D=%d unsupported (256 or 512)", D);
+  VO_CHECK_ARG(B > 0 && T > 0 && (int64_t)B * T * D < (1LL << 32), "layernorm_drop: empty or > 2^32 elements");
+  VO_CHECK_ARG(p >= 0.f && p < 1.f, "layernorm_drop: p = %g outside [0, 1)", p);
+  VO_CHECK_ARG(y16 == nullptr || (y_dtype == VO_F32 && y16 != y && y16 != x && y16 != res),
+               "layernorm_drop: y16 needs an fp32 y and its own buffer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const LnDrop dr = ln_drop(p, seed, salt);
+  if (y16) {
+    if (x_dtype == VO_BF16 && res_dtype == VO_F32)
+      return ln_launch<bf16_t, float, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16, dr);
+    if (x_dtype == VO_F32 && res_dtype == VO_F32)
+      return ln_launch<float, float, float, true>(x, res, gamma, beta, lens, B, T, D, eps, y, st, y16, dr);
+  } else {
+    if (x_dtype == VO_F32 && res_dtype == VO_F32 && y_dtype == VO_F32)
+      return ln_launch<float, float, float>(x, res, gamma, beta, lens, B, T, D, eps, y, st, nullptr, dr);
+    if (x_dtype == VO_BF16 && res_dtype == VO_BF16 && y_dtype == VO_BF16)
+      return ln_launch<bf16_t, bf16_t, bf16_t>(x, res, gamma, beta, lens, B, T, D, eps, y, st, nullptr, dr);
+    if (x_dtype == VO_BF16 && res_dtype == VO_F32 && y_dtype == VO_F32)
+      return ln_launch<bf16_t, float, float>(x, res, gamma, beta, lens, B, T, D, eps, y, st, nullptr, dr);
+  }
+  vo_set_error("layernorm_drop: unsupported dtype combination");
+  return VO_ERR_INVALID;
+}
+
+extern "C" int vo_layernorm_bwd_drop(const void* x, int x_dtype, const void* res, int res_dtype, const void* gy,
+                                     int gy_dtype, const void* gy2, const float* gamma, const int32_t* lens, int B,
+                                     int T, int D, float eps, float p, const int64_t* seed, unsigned salt, void* gh,
+                                     void* gres, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  VO_CHECK_ARG(x && res && gy && gamma && gh && gres && dgamma && dbeta && workspace && seed,
+               "layernorm_bwd_drop: null pointer");
+  VO_CHECK_ARG(D == 256 || D == 512, "layernorm_bwd_drop: D=%d unsupported (256 or 512)", D);
+  VO_CHECK_ARG(B > 0 && T > 0 && (int64_t)B * T * D < (1LL << 32), "layernorm_bwd_drop: empty or > 2^32 elements");
+  VO_CHECK_ARG(p >= 0.f && p < 1.f, "layernorm_bwd_drop: p = %g outside [0, 1)", p);
+  VO_CHECK_ARG(gres != gh && gres != x && gh != x, "layernorm_bwd_drop: outputs alias");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* ws = (float*)workspace;
+  const LnDrop dr = ln_drop(p, seed, salt);
+  if (x_dtype == VO_BF16 && res_dtype == VO_F32 && gy_dtype == VO_F32)
+    return ln_bwd_launch<bf16_t, float, float>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st, gy2,
+                                               gres, dr);
+  if (x_dtype == VO_BF16 && res_dtype == VO_F32 && gy_dtype == VO_BF16)
+    return ln_bwd_launch<bf16_t, bf16_t, float>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st, gy2,
+                                                gres, dr);
+  if (x_dtype == VO_F32 && res_dtype == VO_F32 && gy_dtype == VO_F32 && gy2 == nullptr)
+    return ln_bwd_launch<float, float, float>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st, nullptr,
+                                              gres, dr);
+  if (x_dtype == VO_BF16 && res_dtype == VO_BF16 && gy_dtype == VO_BF16 && gy2 == nullptr)
+    return ln_bwd_launch<bf16_t, bf16_t, bf16_t>(x, res, gy, gamma, lens, B, T, D, eps, gh, dgamma, dbeta, ws, st,
+                                                 nullptr, gres, dr);
+  vo_set_error("layernorm_bwd_drop: unsupported dtype combination");
   return VO_ERR_INVALID;
 }

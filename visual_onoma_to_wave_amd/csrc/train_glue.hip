@@ -518,13 +518,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const TX* __restric
 // the backward is the same call on dy -- no mask tensor is written or read (ATen's fused_dropout writes
 // one byte per element and its masked_scale reads it back).  seed: a device int64 drawn per call from
 // torch's generator (graph-safe: every replay draws a new one).
-__device__ __forceinline__ uint32_t drop_mix(uint32_t h) {  // murmur3 finaliser
-  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
-  return h;
-}
-__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t i) {
-  return drop_mix(drop_mix(i * 0x9E3779B9u ^ s0) + s1);
-}
+// (drop_mix / drop_hash / drop_keys: vo_common.h -- the LayerNorm kernels apply the same mask in-pass)
 
 template <typename T>
 __global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, int64_t n, uint32_t thr, float scale,
@@ -532,8 +526,8 @@ __global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, i
                                                       T* __restrict__ y) {
   using VT = BnVec<T>;
   constexpr int V = VT::V;
-  const uint64_t sd = (uint64_t)seed[0];
-  const uint32_t s0 = (uint32_t)sd ^ drop_mix(salt + 0x3C6EF372u), s1 = (uint32_t)(sd >> 32);
+  uint32_t s0, s1;
+  drop_keys(seed, salt, s0, s1);
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += 4 * stride) {  // 4 vectors in flight

@@ -66,6 +66,22 @@ __device__ __forceinline__ int xcd_grouped_id(int w, int n) {
 // need their own vmcnt wait before this barrier; no global memory is handed between waves.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// ---------------------------------------------------------------- counter-based dropout mask
+// Element i of a dropout site is kept iff drop_hash(s0, s1, i) >= p 2^32 (vo_dropout, and the LayerNorm kernels
+// that apply a sublayer's dropout in-pass): (s0, s1) from the step's device seed and the site's salt.
+__device__ __forceinline__ uint32_t drop_mix(uint32_t h) {  // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t i) {
+  return drop_mix(drop_mix(i * 0x9E3779B9u ^ s0) + s1);
+}
+__device__ __forceinline__ void drop_keys(const int64_t* seed, uint32_t salt, uint32_t& s0, uint32_t& s1) {
+  const uint64_t sd = (uint64_t)seed[0];
+  s0 = (uint32_t)sd ^ drop_mix(salt + 0x3C6EF372u);
+  s1 = (uint32_t)(sd >> 32);
+}
+
 // ---------------------------------------------------------------- 8-element vectors
 // Load 8 consecutive elements (16 B for bf16, 32 B for f32) as floats.
 __device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {

@@ -87,7 +87,7 @@ static const char* const kSymbols[] = {
     "vo_pack_grouped",   "vo_pack_grouped_blocks", "vo_period_fold",   "vo_wav_cl8",     "vo_avgpool_wav",  "vo_gan_reduce",
     "vo_gan_reduce_grad", "vo_glyph_batch", "vo_char_features",
     "vo_conv1d_wgrad",   "vo_colsum",        "vo_conv1d_wgrad_grouped", "vo_resblock3",
-    "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_layernorm_bwd_ex", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
+    "vo_layernorm_bwd_workspace_size", "vo_layernorm_bwd", "vo_layernorm_bwd_ex", "vo_layernorm_drop", "vo_layernorm_bwd_drop", "vo_attention_bwd_workspace_size", "vo_attention_bwd",
     "vo_length_regulate_bwd", "vo_conv1d_wgrad_bias", "vo_lrelu_mask", "vo_conv1d_workspace_size",
     "vo_bn_workspace_size", "vo_bn_train_fwd", "vo_bn_bwd", "vo_vfe_conv_workspace_size", "vo_vfe_conv_fwd",
     "vo_vfe_conv_bwd", "vo_stft_mel_bwd_workspace_size", "vo_stft_mel_bwd", "vo_period_fold_bwd", "vo_wav_cl8_bwd",

@@ -250,6 +250,43 @@ def layernorm_bwd_ex(x, gy, gamma, res, lens=None, gy2=None, eps=1e-5):
     return gh, gh32, dg, db
 
 
+def layernorm_drop(x, gamma, beta, res, p, seed, salt, lens=None, with_bf16=False, eps=1e-5):
+    """y = LN(dropout_p(x) + res) * gamma + beta, pad rows zeroed (vo_layernorm_drop): the dropout mask is
+    vo_dropout's for the same (seed, salt) on x.  y in res's dtype; with_bf16 (fp32 y): returns (y, y16)."""
+    B, T, D = x.shape
+    for t, n in ((x, "x"), (res, "res")):
+        _contig(t, n)
+    if res.shape != x.shape:
+        raise ValueError("layernorm_drop: res shape mismatch")
+    y = torch.empty(x.shape, dtype=res.dtype, device=x.device)
+    y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if with_bf16 else None
+    _lib.check(_lib.lib().vo_layernorm_drop(
+        _ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res), _ptr(gamma), _ptr(beta), _ptr(lens), B, T, D, eps, _ptr(y),
+        vo_dtype(y), _ptr(y16), float(p), _ptr(seed), int(salt), _stream(x)), "vo_layernorm_drop")
+    return (y, y16) if with_bf16 else y
+
+
+def layernorm_bwd_drop(x, gy, gamma, res, p, seed, salt, lens=None, gy2=None, eps=1e-5):
+    """Backward of ``layernorm_drop``: (gh = dL/dx through the mask in x's dtype, gres = dL/dres in res's dtype,
+    dgamma, dbeta); gy2 (bf16, optional): the gradient of the y16 copy, added in the kernel."""
+    B, T, D = x.shape
+    for t, n in ((x, "x"), (gy, "gy"), (res, "res")):
+        _contig(t, n)
+    if gy2 is not None:
+        _contig(gy2, "gy2")
+    L = _lib.lib()
+    gh = torch.empty_like(x)
+    gres = torch.empty_like(res)
+    dg = torch.empty(D, dtype=torch.float32, device=x.device)
+    db = torch.empty(D, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.vo_layernorm_bwd_workspace_size(B, T, D)) // 4, dtype=torch.float32, device=x.device)
+    _lib.check(L.vo_layernorm_bwd_drop(_ptr(x), vo_dtype(x), _ptr(res), vo_dtype(res), _ptr(gy), vo_dtype(gy),
+                                       _ptr(gy2), _ptr(gamma), _ptr(lens), B, T, D, eps, float(p), _ptr(seed), int(salt),
+                                       _ptr(gh), _ptr(gres), _ptr(dg), _ptr(db), _ptr(ws), _stream(x)),
+               "vo_layernorm_bwd_drop")
+    return gh, gres, dg, db
+
+
 # ----------------------------------------------------------------------------- attention
 
 def attention(qkv, lens, n_head, out=None, with_lse=False):

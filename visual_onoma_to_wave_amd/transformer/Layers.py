@@ -45,18 +45,27 @@ class FFTBlock(HipModule):
         qkv = AG.qkv_linear(xin, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
                             mha.w_vs.bias, cd)
         att = AG.attention(qkv, lens, mha.n_head)
-        y = AG.dropout(AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd), mha.dropout.p)
+        y = AG.linear(att, mha.fc.weight, mha.fc.bias, compute_dtype=cd)
         k1, k2 = ffn.kernel_size
-        if dual:
-            x1, x1_16 = AG.layernorm_dual(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
-        else:
-            x1 = x1_16 = AG.layernorm(y, x, mha.layer_norm.weight, mha.layer_norm.bias, lens)
+        x1, x1_16 = self._drop_norm(y, x, mha.dropout.p, mha.layer_norm, lens, dual)
         h = AG.conv1d(x1_16, ffn.w_1.weight, ffn.w_1.bias, K=k1, pad=(k1 - 1) // 2, relu=True, compute_dtype=cd)
         y2 = AG.conv1d(h, ffn.w_2.weight, ffn.w_2.bias, K=k2, pad=(k2 - 1) // 2, compute_dtype=cd)
-        y2 = AG.dropout(y2, ffn.dropout.p)
+        x2, x2_16 = self._drop_norm(y2, x1, ffn.dropout.p, ffn.layer_norm, lens, dual)
+        return x2, (x2_16 if dual else None)
+
+    @staticmethod
+    def _drop_norm(y, res, p, ln, lens, dual):
+        """LayerNorm(dropout_p(y) + res) (SubLayers.py:51-55,88-91): the dropout in the LayerNorm kernels
+        (AG.layernorm_drop) when p > 0; returns (out, the copy the next conv reads)."""
+        if p > 0.0:
+            if dual:
+                return AG.layernorm_drop(y, res, ln.weight, ln.bias, lens, p, True)
+            out = AG.layernorm_drop(y, res, ln.weight, ln.bias, lens, p, False)
+            return out, out
         if dual:
-            return AG.layernorm_dual(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens)
-        return AG.layernorm(y2, x1, ffn.layer_norm.weight, ffn.layer_norm.bias, lens), None
+            return AG.layernorm_dual(y, res, ln.weight, ln.bias, lens)
+        out = AG.layernorm(y, res, ln.weight, ln.bias, lens)
+        return out, out
 
     def forward(self, enc_input, mask=None, slf_attn_mask=None):
         self._check_inference()
