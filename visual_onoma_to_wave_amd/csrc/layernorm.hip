@@ -143,8 +143,8 @@ __global__ void __launch_bounds__(1024) layernorm_bwd_kernel(const TX* __restric
   }
   const int64_t row0 = ((int64_t)blockIdx.x * LN_BWD_NW + wv) * LN_BWD_RPW;
   float v[LN_BWD_RPW][NPL], dy[LN_BWD_RPW][NPL];
-  // (the dropout keys are named apart from the row sums s1 / s2 below: shadowed, the mask of the x gradient
-  // was drawn with a row sum as its key -- how a fused LayerNorm + dropout went wrong in round 5)
+  // (the dropout keys are named apart from the row sums s1 / s2 below: shadowed, the first version of this
+  // fusion drew the x gradient's mask with a row sum as its key -- right forward, wrong zero pattern backward)
   uint32_t dk0 = 0, dk1 = 0;
   if (dr.seed) drop_keys(dr.seed, dr.salt, dk0, dk1);
   bool live[LN_BWD_RPW];
