@@ -18,7 +18,10 @@
  *    transposes to (B, C, T) only to call Conv1d) and the one whose 8 consecutive
  *    channels form one MFMA operand fragment;
  *  - element types: VO_F32 or VO_BF16 for tensor I/O; VO_BF16 compute = bf16 MFMA with
- *    fp32 accumulation, VO_F32 compute = exact-f32 MFMA (the parity mode).
+ *    fp32 accumulation, VO_F32 compute = exact-f32 MFMA (the parity mode), VO_F32X3 compute
+ *    (fp32 I/O and fp32 packed weights, stride 1, no groups) = split-bf16 contractions: each
+ *    fp32 operand as hi + lo bf16, three bf16 MFMAs per product (<= 3 * 2^-18 relative error
+ *    per product: fp32-class, not bit-exact fp32; the mixed-precision training step's fp32 side).
  */
 #ifndef VONOMA_H_
 #define VONOMA_H_
@@ -35,7 +38,7 @@ extern "C" {
 #define VO_OK 0
 #define VO_ERR_INVALID (-1)
 
-enum vo_dtype { VO_F32 = 0, VO_BF16 = 1 };
+enum vo_dtype { VO_F32 = 0, VO_BF16 = 1, VO_F32X3 = 2 /* compute only */ };
 enum vo_act { VO_ACT_NONE = 0, VO_ACT_RELU = 1, VO_ACT_LRELU = 2, VO_ACT_TANH = 3 };
 
 /* ------------------------------------------------------------------ runtime */
@@ -86,7 +89,7 @@ typedef struct vo_conv1d_desc {
   int pre_act;  float pre_slope;
   int post_act; float post_slope;
   float out_scale;
-  int compute_dtype;  /* VO_BF16 or VO_F32 */
+  int compute_dtype;  /* VO_BF16, VO_F32 or VO_F32X3 */
   int transposed, up_stride, up_pad, up_cout, up_tout; /* polyphase ConvTranspose1d */
   int variant;        /* 0 = generic; 1..4 = HiFi-GAN MRF stage 0..3 (bf16 I/O): a kernel
                          instantiation of its own, so profiles attribute the stages   */
@@ -483,7 +486,8 @@ int vo_gan_reduce_grad_multi(int n, const VoGanTerm* terms, int dtype, const flo
  * ConvTranspose1d (Ci, Co, 2s): A = pre(x) (T_in, M = Ci), B = dY (T_up, N = Co), S = s, pad p.
  * dw fp32.  Deterministic: each row split stores its partial tile into ``workspace``
  * (vo_conv1d_wgrad_workspace_size bytes for the same B, T_A, M, N, K, groups) and a second
- * kernel adds the splits in a fixed order.  dtype: VO_BF16 or VO_F32 for both operands.
+ * kernel adds the splits in a fixed order.  dtype: VO_BF16 or VO_F32 for both operands, or VO_F32X3
+ * (fp32 operands contracted as split-bf16, see the header note; stride 1, ungrouped).
  * vo_colsum: out[c] = sum_r x[r*ld + c] (bias gradient; block partials in workspace,
  * vo_colsum_workspace_size bytes, added in order). */
 int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, int K, int groups);

@@ -303,6 +303,7 @@ def test_generator_bf16_reference_init(device, seed):
     (2, 50, 80, 512, 7, 1, 0), (2, 33, 512, 80, 5, 1, 0), (1, 384, 2448, 256, 1, 1, 1),
     # short-sequence tiles (T_out <= 16 / <= 32: encoder / phoneme-level predictors)
     (32, 12, 256, 1024, 9, 1, 1), (5, 16, 1024, 256, 1, 1, 0), (3, 17, 256, 256, 3, 1, 1), (2, 32, 256, 192, 3, 1, 0),
+    (3, 7, 256, 64, 9, 1, 1), (7, 1, 64, 512, 3, 1, 0), (6, 16, 32, 48, 5, 2, 2),
     # Co % 8 == 4: the lane's 8-channel run crosses the end of the output row
     (2, 40, 64, 20, 3, 1, 0), (3, 9, 32, 28, 5, 1, 2)])
 @pytest.mark.parametrize("dt,tol", [(torch.float32, F32_MOD), (torch.bfloat16, 1e-2)])

@@ -55,10 +55,22 @@ class HipModule(nn.Module):
                 cache["val"] = builder(device, dtype)
         return cache["val"]
 
-    def set_compute_dtype(self, dtype):
+    f32_split = False
+
+    @property
+    def contract_dtype(self):
+        """The compute dtype the training path's contractions run in: ops.F32X3 (split-bf16 over fp32
+        tensors) for an fp32 module set to f32_split, else compute_dtype."""
+        from . import ops
+        return ops.F32X3 if (self.f32_split and self.compute_dtype == torch.float32) else self.compute_dtype
+
+    def set_compute_dtype(self, dtype, f32_split=False):
+        """f32_split: an fp32 module's TRAINING contractions (train_run) as split-bf16 (ops.F32X3);
+        inference (run) stays exact fp32."""
         for m in self.modules():
             if isinstance(m, HipModule):
                 m.compute_dtype = dtype
+                m.f32_split = bool(f32_split)
         return self
 
     def _check_inference(self):

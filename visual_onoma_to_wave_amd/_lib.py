@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # tools/); the product path loads lib/libvonoma.so
 LIB_PATH = os.environ.get("VO_LIB_PATH") or os.path.join(_HERE, "lib", "libvonoma.so")
 
-VO_F32, VO_BF16 = 0, 1
+VO_F32, VO_BF16, VO_F32X3 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3
 PACK_CONV, PACK_CONVT = 0, 1
 HEAD_DURATION, HEAD_ENERGY = 0, 1

@@ -171,7 +171,8 @@ class Conv1dFn(torch.autograd.Function):
     def forward(ctx, x, w, b, K, dil, pad, relu, compute_dtype, out_dtype, bias_before_bn=False):
         Co = w.shape[0]
         src = _params_of(w) if PREPACK else None
-        wp = _packed_weight(src, compute_dtype, "fwd") if src else ops.pack_conv_weight(w, compute_dtype)
+        sd = ops.storage_dtype(compute_dtype)  # ops.F32X3: fp32 tensors and packed weights
+        wp = _packed_weight(src, sd, "fwd") if src else ops.pack_conv_weight(w, sd)
         y = ops.conv1d(x.contiguous(), wp, b.detach().float().contiguous() if b is not None else None, Co=Co,
                        K=K, dil=dil, pad=pad, post_act=ops.ACT_RELU if relu else ops.ACT_NONE,
                        out_dtype=out_dtype, compute_dtype=compute_dtype)
@@ -195,19 +196,20 @@ class Conv1dFn(torch.autograd.Function):
             # of 16 k bf16 terms
             gb = torch.zeros_like(ctx.bias_like)
             want_b = False
+        sd = ops.storage_dtype(cdt)
         if ctx.needs_input_grad[0]:
             src = _params_of(w) if PREPACK else None
-            wd = _packed_weight(src, cdt, "dgrad") if src else ops.pack_dgrad_weight(w, cdt)
-            gx = ops.conv1d(gz.to(cdt) if gz.dtype != cdt else gz, wd, None, Co=w.shape[1], K=K, dil=dil,
+            wd = _packed_weight(src, sd, "dgrad") if src else ops.pack_dgrad_weight(w, sd)
+            gx = ops.conv1d(gz.to(sd) if gz.dtype != sd else gz, wd, None, Co=w.shape[1], K=K, dil=dil,
                             pad=(K - 1) * dil - pad, T_out=x.shape[1], out_dtype=x.dtype, compute_dtype=cdt)
         if ctx.needs_input_grad[1]:
             if x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
                 # MFMA weight gradient over transposed LDS reads (vo_conv1d_wgrad), in the forward's
                 # compute dtype (an fp32 activation feeding a bf16 conv -- PostNet after its fp32
                 # BatchNorm -- was contracted in bf16 by the forward too)
-                fuse_b = want_b and gz.dtype == cdt  # bias = column sums of the same dY (no cast)
-                r = ops.conv1d_wgrad(gz.to(cdt).contiguous(), x.to(cdt).contiguous(), K, dil=dil, pad=pad,
-                                     with_bias=fuse_b)
+                fuse_b = want_b and gz.dtype == sd  # bias = column sums of the same dY (no cast)
+                r = ops.conv1d_wgrad(gz.to(sd).contiguous(), x.to(sd).contiguous(), K, dil=dil, pad=pad,
+                                     with_bias=fuse_b, split=cdt is ops.F32X3)
                 if fuse_b:
                     r, gb = r
                 gw = r.to(w.dtype)
@@ -236,7 +238,7 @@ class QKVLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wq, wk, wv, bq, bk, bv, compute_dtype):
         params = (wq, wk, wv)
-        wp = _packed_weight(params, compute_dtype, "fwd")
+        wp = _packed_weight(params, ops.storage_dtype(compute_dtype), "fwd")
         b = torch.cat([bq.detach(), bk.detach(), bv.detach()]).float()
         y = ops.conv1d(x.contiguous(), wp, b, Co=wp.shape[1], K=1, compute_dtype=compute_dtype,
                        out_dtype=x.dtype)
@@ -248,15 +250,16 @@ class QKVLinearFn(torch.autograd.Function):
     def backward(ctx, gy):
         x, wq, wk, wv = ctx.saved_tensors
         cdt = ctx.cdt
+        sd = ops.storage_dtype(cdt)
         gz = gy.contiguous()
-        gz = gz.to(cdt) if gz.dtype != cdt else gz
+        gz = gz.to(sd) if gz.dtype != sd else gz
         gx = None
         if ctx.needs_input_grad[0]:
-            wd = _packed_weight((wq, wk, wv), cdt, "dgrad")
+            wd = _packed_weight((wq, wk, wv), sd, "dgrad")
             gx = ops.conv1d(gz, wd, None, Co=wq.shape[1], K=1, T_out=x.shape[1], out_dtype=x.dtype,
                             compute_dtype=cdt)
-        fuse_b = gy.dtype == cdt  # bias = column sums of the same dY (no cast), as Conv1dFn
-        r = ops.conv1d_wgrad(gz, x.to(cdt).contiguous(), 1, with_bias=fuse_b)
+        fuse_b = gy.dtype == sd  # bias = column sums of the same dY (no cast), as Conv1dFn
+        r = ops.conv1d_wgrad(gz, x.to(sd).contiguous(), 1, with_bias=fuse_b, split=cdt is ops.F32X3)
         gw, gb = r if fuse_b else (r, ops.colsum(gy.contiguous()))
         gw = gw.to(wq.dtype).reshape(gw.shape[0], gw.shape[1])
         n = wq.shape[0]

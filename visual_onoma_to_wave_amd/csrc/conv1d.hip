@@ -78,6 +78,12 @@ template <> struct Raw8<float> {
   }
 };
 
+// VO_F32X3: the packed weights are fp32 ([K][Co][Ci], the VO_F32 packing), staged as fp32 and split
+// into hi / lo bf16 on their way into LDS (store8 / lds_put below)
+template <> struct Raw8<bx3_t> : Raw8<float> {
+  __device__ __forceinline__ void load(const bx3_t* p) { Raw8<float>::load(reinterpret_cast<const float*>(p)); }
+};
+
 // ---------------------------------------------------------------- LDS tile layout
 // bf16: 32 elements (64 B) per row; 16-byte chunk q of row r lives at chunk
 //   q ^ ((r >> (SH - 1)) & 2).  With SH = 2 the B-fragment reads (16 consecutive rows from
@@ -98,11 +104,21 @@ template <> struct Lds<float> {
   static constexpr int PITCH = 40;
   template <int SH> __device__ static __forceinline__ int off(int r, int q) { return r * 40 + 8 * q; }
 };
+// split-bf16 (VO_F32X3): the fp32 tile's geometry, each 32-byte vector slot holding [hi x 8 | lo x 8]
+template <> struct Lds<bx3_t> {
+  static constexpr int PITCH = 40;
+  template <int SH> __device__ static __forceinline__ int off(int r, int q) { return r * 40 + 8 * q; }
+};
 
 __device__ __forceinline__ void lds_put(bf16_t* p, const Raw8<bf16_t>& v) { *reinterpret_cast<uint4*>(p) = v.u; }
 __device__ __forceinline__ void lds_put(float* p, const Raw8<float>& v) {
   *reinterpret_cast<float4*>(p) = v.a;
   *reinterpret_cast<float4*>(p + 4) = v.b;
+}
+__device__ __forceinline__ void lds_put(bx3_t* p, const Raw8<bx3_t>& v) {
+  float f[8];
+  v.to_f32(f);
+  store8(p, f);
 }
 
 constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
@@ -333,10 +349,18 @@ __device__ __forceinline__ void wait_vmcnt() {
 // so a wave that waits for its weight DMA each step no longer drains the next chunk's window loads
 // (issued one chunk ahead, they got one step to land); and the step barriers are bare s_barrier
 // (LDS writes drained by lgkmcnt): __syncthreads' workgroup release fence waits vmcnt(0) too.
+// SEG (4-byte TC, stride 1, T_out <= 16): utterance-segment tiles -- each 16-row position tile j of a
+// wave is one whole utterance (b0 + its index), staged as its own window of 16 + (K-1) dil rows (rows
+// outside [0, T_in) zeroed), so the BT / 16 utterances of a workgroup share every staged weight tap.
+// The short-sequence convs (glyph encoder, variance predictors: T ~ 12) otherwise ran one utterance
+// per workgroup and re-read the whole weight once per utterance (FFN w_1 at B = 32: 302 MB of L2
+// reads for 9.4 MB of weights).  Halo <= SEG_HALO.
+constexpr int SEG_HALO = 8;
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS, bool NICE, int ROLE,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2, bool SEG = false>
 __global__ void __launch_bounds__(WCO * WT * 64)
 conv1d_kernel(ConvArgs a) {
+  static_assert(!SEG || (sizeof(TC) == 4 && S == 1 && !GL), "conv1d SEG: 4-byte compute, stride 1");
   constexpr int NT = WCO * WT * 64;
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -344,7 +368,8 @@ conv1d_kernel(ConvArgs a) {
   constexpr int VPR = KC / 8;                 // 8-element vectors per row (4)
   constexpr bool DMA = GL && NICE && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0;
   constexpr bool SPLIT = RS && DMA && (NT / 64) % 2 == 0;
-  constexpr int MAXV = SPLIT ? 1 : (((BT - 1) * S + 1 + HALO_MAX) * VPR + NT - 1) / NT;
+  constexpr int MAXV = SPLIT ? 1 : SEG ? ((BT / 16) * (16 + SEG_HALO) * VPR + NT - 1) / NT
+                                      : (((BT - 1) * S + 1 + HALO_MAX) * VPR + NT - 1) / NT;
   // SPLIT: the window waves copy each chunk's window by LDS-DMA (XPW 1-KiB pieces per wave,
   // lane-linear) into a raw staging area; at the chunk's end each lane applies the prologue
   // activation to the 16 bytes it fetched and stores them into the swizzled window buffer
@@ -355,7 +380,8 @@ conv1d_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TC* smem = reinterpret_cast<TC*>(smem_raw);
 
-  const int win_rows = (BT - 1) * S + 1 + (a.K - 1) * a.dil;  // S: conv stride
+  const int seg_rows = 16 + (a.K - 1) * a.dil;  // SEG: window rows per utterance
+  const int win_rows = SEG ? (BT / 16) * seg_rows : (BT - 1) * S + 1 + (a.K - 1) * a.dil;  // S: conv stride
   TC* const win0 = smem;
   TC* const wt0 = smem + 2 * win_rows * P;
   const int win_stride = win_rows * P;      // elements between the two window buffers
@@ -368,8 +394,8 @@ conv1d_kernel(ConvArgs a) {
   const int wave_co0 = (wave % WCO) * 16 * NI;
   const int wave_t0 = (wave / WCO) * 16 * NJ;
 
-  const int b = blockIdx.x / a.tiles_per_b;
-  const int t0 = (blockIdx.x - b * a.tiles_per_b) * BT;
+  const int b = SEG ? blockIdx.x * (BT / 16) : blockIdx.x / a.tiles_per_b;  // SEG: the tile's first utterance
+  const int t0 = SEG ? 0 : (blockIdx.x - b * a.tiles_per_b) * BT;
   const int co_blk = blockIdx.y * BCO;
 
   const TIN* __restrict__ X = reinterpret_cast<const TIN*>(a.x) + (int64_t)b * a.xbs;
@@ -403,10 +429,16 @@ conv1d_kernel(ConvArgs a) {
   for (int s = 0; s < MAXVA; ++s) {
     const int v = tid + s * NT;
     const int r = v / VPR, q = v % VPR;
-    const int row = t0 * S - a.pad + r;
-    xr[s] = r < win_rows && row >= 0 && row < a.T_in;  // row in range
     xc[s] = q * 8;
-    xg[s] = min(max(row, 0), a.T_in - 1) * a.ldx + q * 8;
+    if constexpr (SEG) {
+      const int seg = r / seg_rows, row = r - seg * seg_rows - a.pad;
+      xr[s] = r < win_rows && b + seg < a.B && row >= 0 && row < a.T_in;
+      xg[s] = (int)(min(seg, a.B - 1 - b) * a.xbs) + min(max(row, 0), a.T_in - 1) * a.ldx + q * 8;
+    } else {
+      const int row = t0 * S - a.pad + r;
+      xr[s] = r < win_rows && row >= 0 && row < a.T_in;  // row in range
+      xg[s] = min(max(row, 0), a.T_in - 1) * a.ldx + q * 8;
+    }
     xl[s] = r < win_rows ? Lds<TC>::template off<2>(r, q) : -1;
   }
   int wg[WV], wl[WV], wk[WV], wq[WV];
@@ -594,7 +626,8 @@ conv1d_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < NI; ++i)
     a_off[i] = Lds<TC>::template off<SHW>(wave_co0 + NI * 4 * (lr >> 2) + 4 * i + (lr & 3), lq);
-  const int brow0 = wave_t0 + lr;
+  const int brow0 = SEG ? (wave_t0 / 16) * seg_rows + lr : wave_t0 + lr;
+  const int jst = SEG ? seg_rows * P : 16 * S * P;  // rows between position tiles j (SEG: one utterance window)
 
   // prologue
   if (xwave) load_window(0);
@@ -622,7 +655,7 @@ conv1d_kernel(ConvArgs a) {
         const int br = brow0 * S + (k0 + t) * a.dil;
         const int boff = Lds<TC>::template off<2>(br, lq);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + 16 * S * j * P);  // +16S rows keeps the swizzle
+        for (int j = 0; j < NJ; ++j) bfr[j].load(xb + boff + (SEG ? j * jst : 16 * S * j * P));  // +16S rows keeps the swizzle
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -689,6 +722,21 @@ conv1d_kernel(ConvArgs a) {
     __syncthreads();
     ++s;
   }
+  if constexpr (SEG) {  // position tile j = utterance b + wave_t0 / 16 + j, positions 0..15
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int bj = b + wave_t0 / 16 + j;
+      if (bj >= a.B) continue;
+      f32x4 a1[NI][1];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) a1[i][0] = acc[i][j];
+      if (a.partial)
+        conv_partial_store<NI, 1>(a, a1, bj, 0, co_blk, wave_co0, 0, lane);
+      else
+        conv_epilogue<TOUT, NI, 1, EJ>(a, a1, bj, 0, co_blk, wave_co0, 0, lane);
+    }
+    return;
+  }
   if (a.partial) {
     conv_partial_store<NI, NJ>(a, acc, b, t0, co_blk, wave_co0, wave_t0, lane);
     return;
@@ -747,7 +795,8 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
   *splits = 1;
   *kcs = 0;
   if (vo_tune_get("splitk_cfg") == 1 || vo_tune_get("gen_cfg") != 0) return false;
-  if (d->compute_dtype != VO_F32 || d->x_dtype != VO_F32 || d->y_dtype != VO_F32) return false;
+  if ((d->compute_dtype != VO_F32 && d->compute_dtype != VO_F32X3) || d->x_dtype != VO_F32 || d->y_dtype != VO_F32)
+    return false;
   if (d->transposed || d->stride > 1 || d->groups > 1 || d->variant != 0) return false;
   if (d->T_out > 16 || d->Co < 64 || d->Co % 4 || d->ldy % 4) return false;
   const int n_chunks = (d->Ci + KC - 1) / KC;
@@ -838,7 +887,7 @@ __global__ void __launch_bounds__(WCO * WT * 64) lin_kernel(ConvArgs a) {
 // ------------------------------------------------------------------ host dispatch
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs);
 template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT, int TPS_BF16, int ROLE = 0,
-          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2>
+          int PRIO = 0, int ABL = 0, int S = 1, bool GL = false, bool RS = false, int EJ = 2, bool SEG = false>
 static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   constexpr int BCO = 16 * NI * WCO;
   constexpr int BT = 16 * NJ * WT;
@@ -854,14 +903,14 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   a.post_act = d->post_act; a.post_slope = d->post_slope; a.out_scale = d->out_scale;
   a.transposed = d->transposed; a.up_stride = d->up_stride; a.up_pad = d->up_pad;
   a.up_cout = d->up_cout; a.up_tout = d->up_tout;
-  a.tiles_per_b = (d->T_out + BT - 1) / BT;
+  a.tiles_per_b = SEG ? 1 : (d->T_out + BT - 1) / BT;
   a.co_tiles = (d->Co + BCO - 1) / BCO;
   a.B = d->B;
   a.ymask = d->ymask; a.ymask_slope = d->ymask_slope;
   const int groups = d->groups > 1 ? d->groups : 1;
   a.cig = d->Ci / groups;
   a.cog = d->Co / groups;
-  const int win_rows = (BT - 1) * S + 1 + (d->K - 1) * d->dil;
+  const int win_rows = SEG ? (BT / 16) * (16 + (d->K - 1) * d->dil) : (BT - 1) * S + 1 + (d->K - 1) * d->dil;
   const bool nice = d->Ci % KC == 0 && d->Co % BCO == 0;
   // role-split kernels (RS): + the raw window staging area of conv1d_kernel (XPW pieces per window wave)
   constexpr bool SPL = RS && GL && S == 1 && sizeof(TC) == 2 && sizeof(TIN) == 2 && ABL == 0 && (WCO * WT) % 2 == 0;
@@ -872,8 +921,8 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
     vo_set_error("conv1d: LDS request %zu B exceeds 160 KiB", lds);
     return VO_ERR_INVALID;
   }
-  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS, EJ>
-                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S>;
+  auto kern = nice ? conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, true, ROLE, PRIO, ABL, S, GL, RS, EJ, SEG>
+                   : conv1d_kernel<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS, false, ROLE, PRIO, ABL, S, false, false, 2, SEG>;
   a.partial = nullptr;
   a.kcs = 0;
   int splits = 1;
@@ -887,7 +936,8 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
       splits = 1;
     }
   }
-  dim3 grid((unsigned)(a.tiles_per_b * d->B), (unsigned)a.co_tiles, (unsigned)splits);
+  const unsigned gx = SEG ? (unsigned)((d->B + BT / 16 - 1) / (BT / 16)) : (unsigned)(a.tiles_per_b * d->B);
+  dim3 grid(gx, (unsigned)a.co_tiles, (unsigned)splits);
   hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
   if (a.partial) {
     const int64_t n = (int64_t)d->B * d->T_out * (d->Co / 4);
@@ -900,6 +950,10 @@ template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int
           int PRIO = 0, int ABL = 0, bool GL = false, bool RS = false, int EJ = 2>
 static int launch_cfg(const vo_conv1d_desc* d, hipStream_t st) {
   return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, TPS_BF16, ROLE, PRIO, ABL, 1, GL, RS, EJ>(d, st);
+}
+template <typename TIN, typename TC, typename TOUT, int NI, int NJ, int WCO, int WT>
+static int launch_seg(const vo_conv1d_desc* d, hipStream_t st) {
+  return launch_cfg_s<TIN, TC, TOUT, NI, NJ, WCO, WT, 1, 0, 0, 0, 1, false, false, 2, true>(d, st);
 }
 
 #ifdef VO_ABLATIONS
@@ -973,6 +1027,16 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
   const int64_t rows = (int64_t)d->B * d->T_out;
   // short sequences (the glyph encoder / phoneme-level predictors run at T_src ~ 12): one
   // 16- or 32-row time tile, waves spread over output channels
+  if constexpr (sizeof(TC) == 4) {
+    // fp32 / split-bf16 at T_out <= 16: utterance-segment tiles (SEG, see conv1d_kernel), 4 utterances
+    // x 64 output channels (32 below Co = 512); seg_cfg 3 = 8 utterances, 4 = off (the tiles below)
+    const int gc = vo_tune_get("seg_cfg");
+    if (d->T_out <= 16 && !d->transposed && d->stride <= 1 && (d->K - 1) * d->dil <= SEG_HALO && d->Co >= 32 &&
+        gc != 4 && (int64_t)d->B * d->x_bstride < ((int64_t)1 << 31)) {
+      if (gc == 3) return d->Co >= 512 ? launch_seg<TIN, TC, TOUT, 2, 4, 2, 2>(d, st) : launch_seg<TIN, TC, TOUT, 1, 4, 2, 2>(d, st);
+      return d->Co >= 512 ? launch_seg<TIN, TC, TOUT, 2, 2, 2, 2>(d, st) : launch_seg<TIN, TC, TOUT, 1, 2, 2, 2>(d, st);
+    }
+  }
   if (d->T_out <= 16 && d->Co >= 64) {
     // fp32 (glyph encoder, variance predictors at B = 32, T = 12): 32 x 16 tiles, 4x the
     // workgroups of 128 x 16: FFN w_1 66 -> 51 us, w_2 28 -> 20, predictor k3 20 -> 13
@@ -1100,6 +1164,11 @@ extern "C" int vo_conv1d(const vo_conv1d_desc* d, void* stream) {
     if (handled) return rc;
   }
   const int xi = d->x_dtype, yo = d->y_dtype;
+  if (d->compute_dtype == VO_F32X3) {  // split-bf16 fp32 contractions (vonoma.h)
+    VO_CHECK_ARG(xi == VO_F32 && yo == VO_F32 && d->stride <= 1 && d->groups <= 1 && d->variant == 0,
+                 "conv1d: VO_F32X3 compute needs fp32 I/O, stride 1, no groups");
+    return launch_types<float, bx3_t, float>(d, st);
+  }
   if (d->stride > 1 || d->groups > 1) {  // discriminator layers
     const int g = d->groups > 1 ? d->groups : 1;
     VO_CHECK_ARG(!d->transposed && d->variant == 0, "conv1d: stride/groups exclude transposed and variants");

@@ -23,6 +23,7 @@
 // the same tiles with 16x16x4 f32 MFMAs.
 
 #include <algorithm>
+#include <type_traits>
 
 #include "vo_common.h"
 
@@ -45,6 +46,8 @@ struct WgradArgs {
   bool bias;  // bias gradient (column sums of A) fused into the tap-0 / n-tile-0 workgroups
   int abl;  // timing ablation (wgrad_cfg 11): 2 = no loads
   int gpt;  // groups per tile (grouped convs with narrow groups, per-tap kernel): see wgrad_gpt
+  float* dwf;  // per-tap kernel with one row split: dW (and db) written in their final layout, no reduce
+  float* dbf;
 };
 // groups > 1 (grouped conv): grid z = group * K + tap; group g reads A columns [g M, (g+1) M)
 // and B columns [g N, (g+1) N) and writes block g of the (groups, K, M, N) result
@@ -54,6 +57,9 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 template <typename T> struct WgTile;
 template <> struct WgTile<bf16_t> { static constexpr int PITCH = 72; };  // 144-B rows: tr reads of 4 rows hit distinct banks
 template <> struct WgTile<float> { static constexpr int PITCH = 68; };
+// VO_F32X3: fp32 operands split into a hi and a lo bf16 plane of the bf16 tile's geometry (the two
+// planes of 64 x 72 bf16 fill the 64 x 72 four-byte elements the tile declares)
+template <> struct WgTile<bx3_t> { static constexpr int PITCH = 72; };
 
 __device__ __forceinline__ uint32_t lrelu_pack(uint32_t w, float s) {
   const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
@@ -95,9 +101,11 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
   const bool do_bias = p.bias && k == 0 && n0 == 0;  // workgroup-uniform
   float bsum = 0.f;
 
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
-    // ---- stage 64 rows of A (rows r0..) and of B (gathered rows of the same utterances)
-    u32x4_t va[NV], vb[NV];
+  // ---- stage 64 rows of A (rows r0..) and of B (gathered rows of the same utterances); the next chunk's
+  // loads are issued before this chunk's MFMAs (the serial chain of a split is otherwise one load round
+  // trip per chunk: the encoder's 384-row wgrads walk 6 chunks)
+  u32x4_t va[NV], vb[NV];
+  auto load_chunk = [&](int64_t r0) {
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       const int v = tid + s * 256;
@@ -118,13 +126,33 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       if (!qok || m0 + c >= Mv) va[s] = u32x4_t{0u, 0u, 0u, 0u};
       if (!bok || n0 + c >= Nv) vb[s] = u32x4_t{0u, 0u, 0u, 0u};
     }
+  };
+  if (r_begin < r_end) load_chunk(r_begin);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += WG_R) {
     __syncthreads();  // previous chunk's fragment reads are done
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       const int v = tid + s * 256;
       const int r = v / VPR, c = (v % VPR) * EV;
       u32x4_t x = va[s], y = vb[s];
-      if constexpr (sizeof(TC) == 2) {
+      if constexpr (std::is_same<TC, bx3_t>::value) {
+        float f[8] = {__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w),
+                      __uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (p.pre_a) f[e] = fmaxf(f[e], f[e] * p.slope);
+          if (p.pre_b) f[4 + e] = fmaxf(f[4 + e], f[4 + e] * p.slope);
+        }
+        uint4 hi, lo;  // (x.xy, x.zw, y.xy, y.zw) as bf16 pairs
+        split8(f, hi, lo);
+        bf16_t* ha = reinterpret_cast<bf16_t*>(sa);
+        bf16_t* hb = reinterpret_cast<bf16_t*>(sb);
+        *reinterpret_cast<uint2*>(ha + r * P + c) = make_uint2(hi.x, hi.y);
+        *reinterpret_cast<uint2*>(ha + (WG_R + r) * P + c) = make_uint2(lo.x, lo.y);
+        *reinterpret_cast<uint2*>(hb + r * P + c) = make_uint2(hi.z, hi.w);
+        *reinterpret_cast<uint2*>(hb + (WG_R + r) * P + c) = make_uint2(lo.z, lo.w);
+        continue;
+      } else if constexpr (sizeof(TC) == 2) {
         if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
         if (p.pre_b) y = u32x4_t{lrelu_pack(y.x, p.slope), lrelu_pack(y.y, p.slope), lrelu_pack(y.z, p.slope), lrelu_pack(y.w, p.slope)};
       } else {
@@ -143,21 +171,29 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       *reinterpret_cast<u32x4_t*>(sb + r * P + c) = y;
     }
     __syncthreads();
+    if (r0 + WG_R < r_end) load_chunk(r0 + WG_R);
     if (do_bias) {
       const int col = tid & 63, r16 = (tid >> 6) * 16;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) bsum += to_f32(sa[(r16 + i) * P + col]);
+      for (int i = 0; i < 16; ++i) {
+        if constexpr (std::is_same<TC, bx3_t>::value) {  // hi + lo: within 2^-18 of the fp32 value
+          const bf16_t* ha = reinterpret_cast<const bf16_t*>(sa);
+          bsum += to_f32(ha[(r16 + i) * P + col]) + to_f32(ha[(WG_R + r16 + i) * P + col]);
+        } else {
+          bsum += to_f32(sa[(r16 + i) * P + col]);
+        }
+      }
     }
 
     // ---- two 32-row k-steps
 #pragma unroll
     for (int ks = 0; ks < WG_R / 32; ++ks) {
       const int kr = ks * 32;
-      if constexpr (sizeof(TC) == 2) {
+      if constexpr (sizeof(TC) == 2 || std::is_same<TC, bx3_t>::value) {
         // fragment of 16 channels (c0..c0+15) x 8 rows (kr + 8g ..): two transposed 4-row reads
         const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-        auto frag = [&](const TC* tile, int c0) {
-          const TC* base = tile + (kr + 8 * g + q) * P + c0 + 4 * pp;
+        auto frag = [&](const bf16_t* tile, int c0) {
+          const bf16_t* base = tile + (kr + 8 * g + q) * P + c0 + 4 * pp;
           typedef __attribute__((address_space(3))) v4s lds_v4s;
           const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)base);
           const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + 4 * P));
@@ -169,11 +205,27 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
           f.v = __builtin_bit_cast(bf16x8, all);
           return f;
         };
+        const bf16_t* ta = reinterpret_cast<const bf16_t*>(sa);
+        const bf16_t* tb = reinterpret_cast<const bf16_t*>(sb);
         Frag<bf16_t> fa[2], fb[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[i] = frag(sa, wm + 16 * i);
+        for (int i = 0; i < 2; ++i) fa[i] = frag(ta, wm + 16 * i);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = frag(sb, wn + 16 * j);
+        for (int j = 0; j < 2; ++j) fb[j] = frag(tb, wn + 16 * j);
+        if constexpr (std::is_same<TC, bx3_t>::value) {  // lo planes: the small terms first
+          Frag<bf16_t> la[2], lb[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) la[i] = frag(ta + WG_R * P, wm + 16 * i);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) lb[j] = frag(tb + WG_R * P, wn + 16 * j);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              acc[i][j] = mfma(la[i], fb[j], acc[i][j]);
+              acc[i][j] = mfma(fa[i], lb[j], acc[i][j]);
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -204,9 +256,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
     __shared__ float bred[4][64];
     bred[tid >> 6][tid & 63] = bsum;
     __syncthreads();
-    if (tid < 64 && m0 + tid < Mv)
-      p.part[(int64_t)blockIdx.x * p.n_tot + p.n_w + (int64_t)grp * p.M + m0 + tid] =
-          bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+    if (tid < 64 && m0 + tid < Mv) {
+      const float v = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+      if (p.dbf)
+        p.dbf[(int64_t)grp * p.M + m0 + tid] = v;
+      else
+        p.part[(int64_t)blockIdx.x * p.n_tot + p.n_w + (int64_t)grp * p.M + m0 + tid] = v;
+    }
   }
 
   // ---- epilogue: D[m][n] (row = m: 4 (lane >> 4) + e, col = n: lane & 15) -> dW[k][m][n]
@@ -219,8 +275,12 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
         const int gm = m / p.M;  // group of the row (0 unless gpt > 1); keep the diagonal blocks
-        if (m < Mv && n < Nv && gm == n / p.N)
-          dw[(((int64_t)(grp + gm) * p.K + k) * p.M + (m - gm * p.M)) * p.N + (n - gm * p.N)] = acc[i][j][e];
+        if (m < Mv && n < Nv && gm == n / p.N) {
+          if (p.dwf)  // final (groups, M, N, K) order
+            p.dwf[(((int64_t)(grp + gm) * p.M + (m - gm * p.M)) * p.N + (n - gm * p.N)) * p.K + k] = acc[i][j][e];
+          else
+            dw[(((int64_t)(grp + gm) * p.K + k) * p.M + (m - gm * p.M)) * p.N + (n - gm * p.N)] = acc[i][j][e];
+        }
       }
 }
 
@@ -593,6 +653,8 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   VO_CHECK_ARG(a && b && dw && workspace, "conv1d_wgrad: null pointer");
   VO_CHECK_ARG(!db || !pre_a, "conv1d_wgrad: the fused bias gradient sums A as stored (pre_a must be off)");
   VO_CHECK_ARG(B > 0 && T_A > 0 && T_B > 0 && K >= 1 && S >= 1 && dil >= 1 && groups >= 1, "conv1d_wgrad: bad sizes");
+  VO_CHECK_ARG(dtype == VO_BF16 || dtype == VO_F32 || (dtype == VO_F32X3 && S == 1 && groups == 1),
+               "conv1d_wgrad: dtype %d (VO_F32X3: stride 1, ungrouped)", dtype);
   const int ev = dtype == VO_BF16 ? 8 : 4;
   VO_CHECK_ARG(M % ev == 0 && N % ev == 0 && lda % ev == 0 && ldb % ev == 0 && lda >= (int64_t)groups * M &&
                    ldb >= (int64_t)groups * N,
@@ -607,6 +669,7 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   p.n_tot = p.n_w + (db ? (int64_t)groups * M : 0);
   p.abl = vo_tune_get("wgrad_cfg") == 11 ? 2 : 0;  // 11: no loads (timing)
   p.gpt = 1;
+  p.dwf = p.dbf = nullptr;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // stride-1 bf16 convs: the multi-tap kernel (wgrad_mt 1 = the per-tap kernel, A/B)
   // (K >= 2 and utterances of >= 8 whole chunks' worth: the per-utterance chunks of short sequences --
@@ -633,11 +696,20 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   wgrad_plan(B, T_A, M, N, K, groups, &splits, &p.rows_per_split);
   VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536 && zk < 65536, "conv1d_wgrad: grid too large");
   dim3 grid((unsigned)splits, (unsigned)tiles, (unsigned)zk);
+  // one row split (short sequences: the encoder's 384 rows): the workgroups write dW / db in their final
+  // layout -- the reduce pass would only permute (K, M, N) -> (M, N, K); wgrad_cfg 13 keeps it (A/B)
+  const bool direct = splits == 1 && vo_tune_get("wgrad_cfg") != 13;
+  if (direct) {
+    p.dwf = dw;
+    p.dbf = db;
+  }
   if (dtype == VO_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, p);
+  else if (dtype == VO_F32X3)
+    hipLaunchKernelGGL(wgrad_kernel<bx3_t>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
-  wgrad_reduce_launch(workspace, (int)splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
+  if (!direct) wgrad_reduce_launch(workspace, (int)splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
   VO_RETURN_LAUNCH();
 }
 

@@ -83,7 +83,7 @@ class VariancePredictor(HipModule):
         return ops.layernorm(h, p["g2"], p["be2"]), p
 
     def train_run(self, x, mask):
-        c, cd, k = self.conv_layer, self.compute_dtype, self.kernel
+        c, cd, k = self.conv_layer, self.contract_dtype, self.kernel
         h = AG.conv1d(x, c.conv1d_1.conv.weight, c.conv1d_1.conv.bias, K=k, pad=(k - 1) // 2, relu=True,
                       compute_dtype=cd)
         h = AG.dropout(AG.layernorm(h, None, c.layer_norm_1.weight, c.layer_norm_1.bias), self.dropout)
@@ -145,8 +145,8 @@ class VarianceAdaptor(HipModule):
         self.energy_bins = nn.Parameter(bins(e_min, e_max, ve["energy_quantization"]), requires_grad=False)
         self.energy_embedding = nn.Embedding(n_bins, d)
 
-    def set_compute_dtype(self, dtype):
-        return super().set_compute_dtype(dtype)
+    def set_compute_dtype(self, dtype, f32_split=False):
+        return super().set_compute_dtype(dtype, f32_split)
 
     def run(self, x, src_lens, max_len=None, e_target=None, k_target=None, d_target=None, e_control=1.0,
             d_control=1.0, out_dtype=None):

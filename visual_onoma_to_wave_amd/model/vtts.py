@@ -35,9 +35,12 @@ class vTTS(HipModule):
             self.audiotype_emb = nn.Embedding(n_types, model_config["transformer"]["encoder_hidden"])
         self.set_precision("mixed")
 
-    def set_precision(self, mode):
+    def set_precision(self, mode, f32_split=True):
         """'mixed' (default): encoder + variance adaptor fp32, decoder / PostNet bf16;
-        'fp32': everything exact-f32 MFMA; 'bf16': everything bf16 MFMA."""
+        'fp32': everything exact-f32 MFMA; 'bf16': everything bf16 MFMA.
+        f32_split (mixed only): the training step's fp32 contractions (encoder, variance predictors) as
+        split-bf16 (ops.F32X3: three bf16 MFMAs per product, ~1e-5 relative per product) instead of exact
+        f32 MFMA; inference stays exact fp32."""
         if mode not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         front = torch.bfloat16 if mode == "bf16" else torch.float32
@@ -48,8 +51,10 @@ class vTTS(HipModule):
         # everything is bf16 -- bf16 autocast of the reference keeps LayerNorm (and so the
         # residual adds) in fp32, and a bf16 stream doubled the mixed mode's drift from fp32
         self.stream_dtype = torch.bfloat16 if mode == "bf16" else torch.float32
-        self.encoder.set_compute_dtype(front)
-        self.variance_adaptor.set_compute_dtype(front)
+        split = f32_split and mode == "mixed"
+        self.f32_split = split
+        self.encoder.set_compute_dtype(front, f32_split=split)
+        self.variance_adaptor.set_compute_dtype(front, f32_split=split)
         self.decoder.set_compute_dtype(back)
         self.postnet.set_compute_dtype(back)
         return self

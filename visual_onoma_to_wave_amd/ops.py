@@ -13,9 +13,26 @@ import torch
 
 from . import _lib, profiling
 from ._lib import (ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, HEAD_DURATION, HEAD_ENERGY,  # noqa: F401
-                   PACK_CONV, PACK_CONVT, VO_BF16, VO_F32)
+                   PACK_CONV, PACK_CONVT, VO_BF16, VO_F32, VO_F32X3)
 
 _DT = {torch.float32: VO_F32, torch.bfloat16: VO_BF16}
+
+
+class _F32X3:
+    """``compute_dtype`` of a contraction over fp32 tensors computed as split-bf16 (VO_F32X3 in
+    include/vonoma.h): each fp32 operand as hi + lo bf16, three bf16 MFMAs per product, <= 3 * 2^-18
+    relative error per product.  Tensors, packed weights and results stay fp32 (storage_dtype)."""
+
+    def __repr__(self):
+        return "ops.F32X3"
+
+
+F32X3 = _F32X3()
+
+
+def storage_dtype(cdt):
+    """The torch dtype of the tensors and packed weights of compute dtype ``cdt``."""
+    return torch.float32 if cdt is F32X3 else cdt
 
 
 def vo_dtype(t):
@@ -67,8 +84,10 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     Ci = w_packed.shape[2]
     if w_packed.shape[0] != K or w_packed.shape[1] != Co:
         raise ValueError(f"conv1d: packed weight {tuple(w_packed.shape)} != [{K}][{Co}][Ci]")
-    if w_packed.dtype != compute_dtype:
+    if w_packed.dtype != storage_dtype(compute_dtype):
         raise ValueError("conv1d: packed weight dtype must equal the compute dtype")
+    if compute_dtype is F32X3 and (x.dtype != torch.float32 or stride > 1 or groups > 1):
+        raise ValueError("conv1d: F32X3 compute needs fp32 input, stride 1, no groups")
     out_dtype = out_dtype or x.dtype
     if transposed is not None:
         s, p, cout = transposed["stride"], transposed["pad"], transposed["cout"]
@@ -106,7 +125,7 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
     d.K, d.dil, d.pad = K, dil, pad
     d.pre_act, d.pre_slope, d.post_act, d.post_slope = pre_act, pre_slope, post_act, post_slope
     d.out_scale = out_scale
-    d.compute_dtype = vo_dtype(compute_dtype)
+    d.compute_dtype = VO_F32X3 if compute_dtype is F32X3 else vo_dtype(compute_dtype)
     if transposed is not None:
         d.transposed, d.up_stride, d.up_pad, d.up_cout, d.up_tout = 1, s, p, cout, up_tout
     d.variant = variant if (x.dtype == out.dtype == compute_dtype == torch.bfloat16) else 0
@@ -118,7 +137,7 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
             raise ValueError("conv1d: ymask must match the output (shape, strides, dtype)")
         d.ymask, d.ymask_slope = ymask.data_ptr(), float(ymask_slope)
     ws = None
-    if compute_dtype == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
+    if storage_dtype(compute_dtype) == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
         # split-reduction scratch for the short fp32 convs (stream-ordered: freed after enqueue)
         nb = _lib.lib().vo_conv1d_workspace_size(ctypes.byref(d))
         if nb > 0:
@@ -1240,12 +1259,14 @@ def char_features(energy, fstats, durations, n_bins):
 
 # ----------------------------------------------------------------------------- training backward
 
-def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1, with_bias=False):
+def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=False, groups=1, with_bias=False,
+                 split=False):
     """Weight gradient on MFMA (vo_conv1d_wgrad).  Conv1d: a = dY (B, T_out, Co), b = x (B, T_in, Ci)
     -> dW (Co, Ci / groups, K).  ConvTranspose1d (transposed=True): a = x (B, T_in, Ci), b = dY
     (B, T_up, Co) -> dW (Ci, Co, K).  pre_a / pre_b: leaky-ReLU slope applied to that operand
     (None = identity).  with_bias (conv form): also the bias gradient, column sums of a, from the
-    same launch (vo_conv1d_wgrad_bias) -> (dW, db)."""
+    same launch (vo_conv1d_wgrad_bias) -> (dW, db).  split (fp32 operands, stride 1, ungrouped): contract
+    them as split-bf16 (VO_F32X3, see F32X3)."""
     _contig(a, "a")
     _contig(b, "b")
     if a.dtype != b.dtype:
@@ -1265,8 +1286,13 @@ def conv1d_wgrad(a, b, K, S=1, dil=1, pad=0, pre_a=None, pre_b=None, transposed=
     slope = pre_a if pre_a is not None else (pre_b if pre_b is not None else 0.0)
     if pre_a is not None and pre_b is not None and pre_a != pre_b:
         raise ValueError("conv1d_wgrad: one slope for both operands")
+    dt = vo_dtype(a)
+    if split:
+        if a.dtype != torch.float32 or S != 1 or groups != 1 or transposed:
+            raise ValueError("conv1d_wgrad: split needs fp32 operands, stride 1, ungrouped, conv form")
+        dt = VO_F32X3
     _lib.check(L.vo_conv1d_wgrad_bias(_ptr(a), M, T_A, _ptr(b), N, T_B, B, mg, ng, K, S, dil, pad, groups,
-                                      int(pre_a is not None), int(pre_b is not None), float(slope), vo_dtype(a),
+                                      int(pre_a is not None), int(pre_b is not None), float(slope), dt,
                                       _ptr(w), _ptr(db), _ptr(ws), _stream(a)), "vo_conv1d_wgrad")
     return (w, db) if with_bias else w
 

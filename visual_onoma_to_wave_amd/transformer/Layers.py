@@ -42,6 +42,7 @@ class FFTBlock(HipModule):
         mha, ffn, cd = self.slf_attn, self.pos_ffn, self.compute_dtype
         dual = x.dtype == torch.float32 and cd == torch.bfloat16
         xin = (x16 if x16 is not None else x.to(cd)) if dual else x
+        cd = self.contract_dtype  # ops.F32X3 for the mixed mode's fp32 encoder
         qkv = AG.qkv_linear(xin, mha.w_qs.weight, mha.w_ks.weight, mha.w_vs.weight, mha.w_qs.bias, mha.w_ks.bias,
                             mha.w_vs.bias, cd)
         att = AG.attention(qkv, lens, mha.n_head)
