@@ -456,6 +456,11 @@ conv1d_kernel(ConvArgs a) {
   }
 
   Raw8<TIN> win_r[MAXV];
+  // SEG: second register sets -- weights fetched two steps ahead, and (one-tap convs) windows two chunks ahead
+  Raw8<TIN> win_r2[SEG ? MAXV : 1];
+  bool win_ok2[SEG ? MAXV : 1];
+  Raw8<TC> w_r2[SEG ? WV : 1];
+  bool w_ok2[SEG ? WV : 1];
   constexpr int NW = NT / 64;
   constexpr int NWW = SPLIT ? NW / 2 : NW;  // waves issuing the weight DMA
   constexpr int GLN = DMA ? (TPS * BCO * VPR) / (64 * NWW) : 1;  // DMA instructions per wave per step
@@ -524,6 +529,17 @@ conv1d_kernel(ConvArgs a) {
   // chunk c + 2 stay in flight), so each window DMA has a whole chunk or more to land
   constexpr int XRAW = (NT / 128) * XPW * 64 * 8;  // elements per raw area
   static_assert(!SPLIT || XPW <= 8, "conv1d RS: wait_vmcnt<XPW>");
+  auto load_window_to = [&](auto& wr, auto& wo, int c) {
+    const int c0 = ci_lo + c * KC;
+#pragma unroll
+    for (int s = 0; s < MAXVA; ++s) {
+      wo[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
+      if constexpr (ABL == 1) {
+        if (c > 0) { wr[s].zero(); continue; }
+      }
+      wr[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
+    }
+  };
   auto load_window = [&](int c, int rb = 0) {
     const int c0 = ci_lo + c * KC;
     if constexpr (SPLIT) {  // NICE: no channel bounds; rows clamped (zeroed by the LDS pass)
@@ -540,13 +556,28 @@ conv1d_kernel(ConvArgs a) {
       }
       return;
     }
+    load_window_to(win_r, win_ok, c);
+  };
+  auto store_window_from = [&](auto& wr, auto& wo, int buf) {
+    TC* base = win0 + buf * win_stride;
 #pragma unroll
-    for (int s = 0; s < MAXVA; ++s) {
-      win_ok[s] = xr[s] && (NICE || c0 + xc[s] < a.Ci);
-      if constexpr (ABL == 1) {
-        if (c > 0) { win_r[s].zero(); continue; }
+    for (int s = 0; s < MAXV; ++s) {  // branch-free: idle slots store to the dummy row
+      TC* dst;
+      {
+        dst = xl[s] >= 0 ? base + xl[s] : dummy;
+        if (!wo[s]) wr[s].zero();
       }
-      win_r[s].load(X + xg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - xc[s])));
+      if constexpr (std::is_same<TIN, TC>::value) {
+        if (raw_window) {
+          lds_put(dst, wr[s]);
+          continue;
+        }
+      }
+      float f[8];
+      wr[s].to_f32(f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
+      store8(dst, f);
     }
   };
   auto store_window = [&](int buf, int rb = 0, bool young = false) {
@@ -570,48 +601,32 @@ conv1d_kernel(ConvArgs a) {
       }
       return;
     }
-#pragma unroll
-    for (int s = 0; s < MAXV; ++s) {  // branch-free: idle slots store to the dummy row
-      TC* dst;
-      {
-        dst = xl[s] >= 0 ? base + xl[s] : dummy;
-        if (!win_ok[s]) win_r[s].zero();
-      }
-      if constexpr (std::is_same<TIN, TC>::value) {
-        if (raw_window) {
-          lds_put(dst, win_r[s]);
-          continue;
-        }
-      }
-      float f[8];
-      win_r[s].to_f32(f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = lrelu_max(f[e], pre_s);  // pre_s in [0, 1]
-      store8(dst, f);
-    }
+    store_window_from(win_r, win_ok, buf);
   };
-  auto load_w = [&](int c, int k0) {
+  auto load_w_to = [&](auto& wr, auto& wo, int c, int k0) {
     if constexpr (DMA) return;
     const int c0 = ci_lo + c * KC;
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
       const int k = min(k0 + wk[s], a.K - 1);  // taps >= K are skipped by the MFMA loop
-      w_ok[s] = wok[s] && (NICE || c0 + wq[s] < a.Ci);
+      wo[s] = wok[s] && (NICE || c0 + wq[s] < a.Ci);
       if constexpr (ABL == 1) {
-        if (c > 0 || k0 > 0) { w_r[s].zero(); continue; }
+        if (c > 0 || k0 > 0) { wr[s].zero(); continue; }
       }
-      w_r[s].load(Wp + k * tap_stride + wg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - wq[s])));
+      wr[s].load(Wp + k * tap_stride + wg[s] + (NICE ? c0 : min(c0, a.Ci - 8 - wq[s])));
     }
   };
-  auto store_w = [&](int buf) {
+  auto store_w_from = [&](auto& wr, auto& wo, int buf) {
     if constexpr (DMA) return;
     TC* base = wt0 + buf * WSTRIDE;
 #pragma unroll
     for (int s = 0; s < WV; ++s) {
-      if (!w_ok[s]) w_r[s].zero();
-      lds_put((tid + s * NT) / VPR < TPS * BCO ? base + wl[s] : dummy, w_r[s]);
+      if (!wo[s]) wr[s].zero();
+      lds_put((tid + s * NT) / VPR < TPS * BCO ? base + wl[s] : dummy, wr[s]);
     }
   };
+  auto load_w = [&](int c, int k0) { load_w_to(w_r, w_ok, c, k0); };
+  auto store_w = [&](int buf) { store_w_from(w_r, w_ok, buf); };
 
   f32x4 acc[NI][NJ];
 #pragma unroll
@@ -666,6 +681,54 @@ conv1d_kernel(ConvArgs a) {
     }
   };
 
+  if constexpr (SEG) {
+    // Short chains (9..72 steps of 2..8 MFMAs per wave): every step of the generic loop below waited a
+    // whole load round trip (its weights are fetched at the step's start, and __syncthreads drains
+    // vmcnt).  Here step q's weights are fetched two steps ahead (register sets A / B alternate),
+    // written to LDS one step ahead, and the barriers are bare (lds_barrier): loads stay in flight
+    // across them.  One-tap convs (a step per chunk) fetch windows two chunks ahead the same way.
+    // Step q = chunk q / tsteps, tap group q % tsteps: the generic loop's order (bit-identical).
+    const int nq = n_chunks * tsteps;
+    auto wload = [&](auto& wr, auto& wo, int q) {
+      q = min(q, nq - 1);  // clamped re-fetch past the end: loads stay unconditional
+      const int c = q / tsteps;
+      load_w_to(wr, wo, c, (q - c * tsteps) * TPS);
+    };
+    if (tsteps == 1) {
+      load_window_to(win_r, win_ok, min(1, n_chunks - 1));
+      wload(w_r, w_ok, 1);
+      auto body1 = [&](int c, auto& cw, auto& cwo, auto& cx, auto& cxo, auto& nw, auto& nwo, auto& nx, auto& nxo) {
+        load_window_to(nx, nxo, min(c + 2, n_chunks - 1));
+        wload(nw, nwo, c + 2);
+        mfma_step(c, 0, c);
+        if (c + 1 < n_chunks) {
+          store_window_from(cx, cxo, (c + 1) & 1);
+          store_w_from(cw, cwo, (c + 1) & 1);
+        }
+        lds_barrier();
+      };
+      for (int c = 0; c < n_chunks; c += 2) {
+        body1(c, w_r, w_ok, win_r, win_ok, w_r2, w_ok2, win_r2, win_ok2);
+        if (c + 1 < n_chunks) body1(c + 1, w_r2, w_ok2, win_r2, win_ok2, w_r, w_ok, win_r, win_ok);
+      }
+    } else {
+      wload(w_r, w_ok, 1);
+      auto body = [&](int q, auto& cw, auto& cwo, auto& nw, auto& nwo) {
+        const int c = q / tsteps, tg = q - c * tsteps;
+        if (tg == 0) load_window(min(c + 1, n_chunks - 1));
+        wload(nw, nwo, q + 2);
+        mfma_step(c, tg, q);
+        store_w_from(cw, cwo, (q + 1) & 1);  // past the last step: a buffer no step reads
+        if (tg == tsteps - 1 && c + 1 < n_chunks) store_window((c + 1) & 1);
+        lds_barrier();
+      };
+      for (int q = 0; q < nq; q += 2) {
+        body(q, w_r, w_ok, w_r2, w_ok2);
+        if (q + 1 < nq) body(q + 1, w_r2, w_ok2, w_r, w_ok);
+      }
+    }
+    wait_vmcnt<0>();  // the clamped re-fetches land before the registers are reused by the epilogue
+  }
   int s = 0;
   if constexpr (SPLIT) {
     for (int c = 0; c < n_chunks; ++c) {
@@ -689,7 +752,7 @@ conv1d_kernel(ConvArgs a) {
     }
     if (xwave) wait_vmcnt<0>();  // the clamped re-fetches of the last chunks land before the epilogue
   }
-  for (int c = 0; c < (SPLIT ? 0 : n_chunks); ++c) {
+  for (int c = 0; c < (SPLIT || SEG ? 0 : n_chunks); ++c) {
     const bool more_chunks = c + 1 < n_chunks;
     if constexpr (!DMA) load_window(min(c + 1, n_chunks - 1));  // a whole chunk of MFMAs ahead of its use
     for (int tg = 0; tg < tsteps - 1; ++tg, ++s) {
