@@ -44,7 +44,7 @@ HOP = 256
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (no sparsity)
 F32_PEAK_TFLOPS = 157.3
-TRAFFIC_FILE = os.path.join("profiles", "traffic_r05.json")  # committed rocprofv3 PMC passes (tools/pmc_round.sh)
+TRAFFIC_FILE = os.path.join("profiles", "traffic_r06.json")  # committed rocprofv3 PMC passes (tools/pmc_round.sh)
 
 
 def parse():
@@ -342,7 +342,7 @@ MSD_CFG = [(1, 128, 15, 1, 1, 7), (128, 128, 41, 2, 4, 20), (128, 256, 41, 2, 16
            (512, 1024, 41, 4, 16, 20), (1024, 1024, 41, 1, 16, 20), (1024, 1024, 5, 1, 1, 2)]
 # dominant kernel and kernel families (time, FLOPs, fraction of peak) of the training steps in the
 # committed serialized kernel traces (tools/train_prof.sh -> tools/train_dominant.py)
-TRAIN_DOMINANT = os.path.join("profiles", "r05", "train_dominant.json")
+TRAIN_DOMINANT = os.path.join("profiles", "r06", "train_dominant.json")
 
 
 def disc_forward_flops(T, B):
