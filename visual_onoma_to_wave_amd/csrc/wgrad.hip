@@ -284,6 +284,144 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs p) {
       }
 }
 
+// K = 1 weight gradient (round 6; bf16, stride 1, no padding, ungrouped, no prologue activation): the
+// Linear layers of the C4 decoder (q/k/v 256 -> 768, fc, FFN w_2 1024 -> 256, mel_linear) at 16 k rows,
+// dW (M x N) = A^T B over the rows.  On the per-tap kernel's 64 x 64 tiles these ran at ~0.05 of the
+// bf16 peak (19 launches, ~1 ms of the C4 step): 8 MFMAs per wave per staged 16 KB and a load round trip
+// per 64-row chunk.  Here a workgroup owns a 128 x 128 tile (4 waves of 64 x 64 = 16 MFMA tiles: 16
+// MFMAs per 32-row k-step for 8 fragment pairs), both operands double-buffered in LDS with the next
+// chunk's loads in registers over the current chunk's MFMAs, bare barriers.  LDS rows are 256 B with
+// the 16-byte chunk q of row r at q ^ 2 ((r & 3) | ((r >> 3 & 1) << 2)): the transposed reads
+// (ds_read_b64_tr_b16: rows kr + 8g + q, two 8-byte column quads) hit 32 distinct bank pairs per half
+// wave, the staging stores 8 distinct chunks per 8 lanes.  Bias gradient (column sums of A) fused into
+// the n-tile-0 workgroups from the staged registers.  Partials / reduce / determinism as the per-tap
+// kernel (tap-major partials with K = 1 are (M, N): an unsplit launch writes dW directly).
+constexpr int K1_T = 128;  // output tile (M and N)
+constexpr int K1_R = 64;   // rows per chunk
+__device__ __forceinline__ int k1_swz(int r, int q) { return q ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
+
+__global__ void __launch_bounds__(256, 2) wgrad_k1_kernel(WgradArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t sa[2][K1_R * K1_T];
+  __shared__ __attribute__((aligned(16))) bf16_t sb[2][K1_R * K1_T];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
+  const int tiles_n = (p.N + K1_T - 1) / K1_T;
+  const int m0 = (blockIdx.y / tiles_n) * K1_T, n0 = (blockIdx.y % tiles_n) * K1_T;
+  const int64_t rows = (int64_t)p.Bn * p.T_A;
+  const int64_t r_begin = (int64_t)blockIdx.x * p.rows_per_split;
+  const int64_t r_end = min(rows, r_begin + p.rows_per_split);
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.a);
+  const bf16_t* Bs = reinterpret_cast<const bf16_t*>(p.bsrc);
+  const bool do_bias = p.bias && n0 == 0;  // workgroup-uniform
+
+  // staging slot s of thread t: row r = (t + 256 s) >> 4, 16-byte chunk c = t & 15 (8 columns)
+  const int sc = tid & 15, sr0 = tid >> 4;
+  const int ma = min(m0 + 8 * sc, p.M - 8), nb = min(n0 + 8 * sc, p.N - 8);
+  const bool mok = m0 + 8 * sc < p.M, nok = n0 + 8 * sc < p.N;
+  uint4 ra[4], rb[4];
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t q = r0 + sr0 + 16 * s;
+      const bool ok = q < r_end;
+      const int64_t qq = ok ? q : r_begin;
+      ra[s] = *reinterpret_cast<const uint4*>(A + qq * p.lda + ma);
+      rb[s] = *reinterpret_cast<const uint4*>(Bs + qq * p.ldb + nb);
+      if (!ok || !mok) ra[s] = make_uint4(0u, 0u, 0u, 0u);
+      if (!ok || !nok) rb[s] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int r = sr0 + 16 * s;
+      *reinterpret_cast<uint4*>(&sa[buf][r * K1_T + k1_swz(r, sc) * 8]) = ra[s];
+      *reinterpret_cast<uint4*>(&sb[buf][r * K1_T + k1_swz(r, sc) * 8]) = rb[s];
+      if (do_bias) {
+        const uint32_t w[4] = {ra[s].x, ra[s].y, ra[s].z, ra[s].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bsum[2 * e] += __uint_as_float(w[e] << 16);
+          bsum[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+        }
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment of 16 channels (c0..c0+15) x 8 rows (kr + 8g ..): two transposed 4-row reads (lane li:
+  // row kr + 8g + (li >> 2), the 8-byte column quad c0 + 4 (li & 3))
+  const int g = lane >> 4, li = lane & 15, fq = li >> 2, fp = li & 3;
+  auto frag = [&](const bf16_t* tile, int kr, int c0) {
+    const int r = kr + 8 * g + fq, col = c0 + 4 * fp;
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + r * K1_T + k1_swz(r, col >> 3) * 8 + (col & 7)));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4s*)(tile + (r + 4) * K1_T + k1_swz(r + 4, col >> 3) * 8 + (col & 7)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const v8s all = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    Frag<bf16_t> f;
+    f.v = __builtin_bit_cast(bf16x8, all);
+    return f;
+  };
+
+  const int nchunks = (int)((r_end - r_begin + K1_R - 1) / K1_R);
+  load(r_begin);
+  store(0);
+  if (nchunks > 1) load(r_begin + K1_R);
+  lds_barrier();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+#pragma unroll
+    for (int ks = 0; ks < K1_R / 32; ++ks) {
+      Frag<bf16_t> fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag(sa[buf], 32 * ks, wm + 16 * i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag(sb[buf], 32 * ks, wn + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+    }
+    if (c + 1 < nchunks) {
+      store(buf ^ 1);  // chunk c + 1 (its buffer was read in chunk c - 1, before the last barrier)
+      if (c + 2 < nchunks) load(r_begin + (int64_t)(c + 2) * K1_R);
+    }
+    lds_barrier();
+  }
+
+  if (do_bias) {  // 16 row-threads per 8-column chunk: one LDS reduction in thread order (deterministic)
+    float* red = reinterpret_cast<float*>(&sa[0][0]);  // [16 row-threads][128 columns], after the last barrier
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[sr0 * K1_T + 8 * sc + e] = bsum[e];
+    __syncthreads();
+    if (tid < K1_T && m0 + tid < p.M) {
+      float v = 0.f;
+      for (int q = 0; q < 16; ++q) v += red[q * K1_T + tid];
+      if (p.dbf)
+        p.dbf[m0 + tid] = v;
+      else
+        p.part[(int64_t)blockIdx.x * p.n_tot + p.n_w + m0 + tid] = v;
+    }
+  }
+  float* dw = p.dwf ? p.dwf : p.part + (int64_t)blockIdx.x * p.n_tot;  // K = 1: (M, N) either way
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm + 16 * i + 4 * g + e, n = n0 + wn + 16 * j + li;
+        if (m < p.M && n < p.N) dw[(int64_t)m * p.N + n] = acc[i][j][e];
+      }
+}
+
 // Multi-tap weight gradient (round 3; stride-1 convs, bf16): the per-tap kernel above restages
 // both operands for every tap -- a K = 11 conv reads dY and x eleven times and feeds 8 MFMAs per
 // wave per staged 16 KB (C5's MRF weight gradients ran at 0.05-0.18 PF/s).  Here a workgroup owns
@@ -609,6 +747,20 @@ static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int d
   pl->splits = (int)((total + pl->cps - 1) / pl->cps);
 }
 
+// K = 1 plan (wgrad_k1_kernel): ~512 workgroups (two per CU; wgrad_cfg 15 = 256, 16 = 1024), at least 4
+// chunks of 64 rows per split
+static void k1_plan(int B, int T_A, int M, int N, int64_t* splits_out, int* rps_out) {
+  const int64_t tiles = (int64_t)((M + K1_T - 1) / K1_T) * ((N + K1_T - 1) / K1_T);
+  const int64_t rows = (int64_t)B * T_A;
+  const int wc = vo_tune_get("wgrad_cfg");
+  const int64_t target = wc == 15 ? 256 : wc == 16 ? 1024 : 512;
+  int64_t splits = (target + tiles - 1) / tiles;
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, rows / (4 * K1_R)));
+  const int rps = (int)(((rows + splits - 1) / splits + K1_R - 1) / K1_R * K1_R);
+  *splits_out = (rows + rps - 1) / rps;
+  *rps_out = rps;
+}
+
 extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, int K, int groups) {
   if (B <= 0 || T_A <= 0 || M <= 0 || N <= 0 || K <= 0 || groups <= 0) return 0;
   int64_t splits;
@@ -617,6 +769,12 @@ extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, 
   MtPlan mt;
   wgrad_mt_plan(B, T_A, M, N, K, groups, 1, &mt);
   splits = std::max<int64_t>(splits, mt.splits);
+  if (K == 1 && groups == 1) {
+    int64_t k1s;
+    int k1r;
+    k1_plan(B, T_A, M, N, &k1s, &k1r);
+    splits = std::max<int64_t>(splits, k1s);
+  }
   return splits * ((int64_t)groups * K * M * N + (int64_t)groups * M) * (int64_t)sizeof(float);
 }
 
@@ -671,6 +829,22 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   p.gpt = 1;
   p.dwf = p.dbf = nullptr;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // K = 1 (Linear layers, bf16): the 128 x 128 tile kernel (wgrad_cfg 14 = the per-tap kernel, A/B)
+  if (dtype == VO_BF16 && K == 1 && S == 1 && pad == 0 && groups == 1 && !pre_a && !pre_b && T_A == T_B &&
+      vo_tune_get("wgrad_cfg") != 14 && p.abl == 0) {
+    int64_t splits;
+    k1_plan(B, T_A, M, N, &splits, &p.rows_per_split);
+    const int tiles = ((M + K1_T - 1) / K1_T) * ((N + K1_T - 1) / K1_T);
+    VO_CHECK_ARG(splits < (1 << 30) && tiles < 65536, "conv1d_wgrad: grid too large");
+    const bool direct = splits == 1;
+    if (direct) {
+      p.dwf = dw;
+      p.dbf = db;
+    }
+    hipLaunchKernelGGL(wgrad_k1_kernel, dim3((unsigned)splits, (unsigned)tiles), dim3(256), 0, st, p);
+    if (!direct) wgrad_reduce_launch(workspace, (int)splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
+    VO_RETURN_LAUNCH();
+  }
   // stride-1 bf16 convs: the multi-tap kernel (wgrad_mt 1 = the per-tap kernel, A/B)
   // (K >= 2 and utterances of >= 8 whole chunks' worth: the per-utterance chunks of short sequences --
   // the MPD's period columns, T_A = 10-34 -- are mostly padding: 207 us per call against the per-tap
