@@ -709,7 +709,10 @@ static void wgrad_plan(int B, int T_A, int M, int N, int K, int groups, int64_t*
   const int wc = vo_tune_get("wgrad_cfg");
   const int64_t target = wc == 1 ? 4096 : wc == 2 ? 8192 : wc == 3 ? 16384 : 1024;
   int64_t splits = std::max<int64_t>(1, (target + (int64_t)tiles * zk - 1) / ((int64_t)tiles * zk));
-  splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (4 * WG_R)));
+  // short sequences (<= 4096 rows: the encoder's 384, split-bf16 / fp32): one chunk per split is allowed --
+  // their 6-chunk serial chains were a load round trip each (31.6 us per launch); wgrad_cfg 17 keeps >= 4
+  const int min_chunks = (rows <= 4096 && wc != 17) ? 1 : 4;
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (min_chunks * WG_R)));
   const int64_t max_rows = wc == 4 ? 2048 : wc == 5 ? 8192 : wc == 6 ? (int64_t)1 << 40 : 4096;
   splits = std::max<int64_t>(splits, (rows + max_rows - 1) / max_rows);
   const int rps = (int)(((rows + splits - 1) / splits + WG_R - 1) / WG_R * WG_R);
