@@ -47,3 +47,31 @@ def test_wgrad_k1_vs_per_tap_and_float64(B, T, Ci, Co, bias):
     if bias:
         assert torch.equal(outs[0][1], again[1])
         assert rel_l2(outs[0][1].double().cpu(), gy.double().sum((0, 1))) < 1e-6
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,K,out_dt", [
+    (32, 512, 1024, 256, 9, torch.bfloat16),  # the C4 decoder's FFN w_1 input gradient
+    (16, 1000, 1024, 128, 9, torch.float32), (9, 911, 512, 64, 5, torch.bfloat16), (32, 512, 2048, 256, 1, torch.bfloat16)])
+def test_conv1d_bf16_split_reduction(B, T, Ci, Co, K, out_dt):
+    """Deep bf16 convs into <= 256 channels run on the 256 x 256 tile with their chunks split over workgroups
+    (fp32 partials added in split order): against torch fp32 (bf16 bar 1e-2), against the unsplit tiles
+    (splitk_cfg 3) within the output rounding, and deterministic run to run."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import _lib, ops
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(B + T + Ci + Co)
+    x = torch.randn(B, T, Ci, generator=g).to(torch.bfloat16)
+    w = torch.randn(Co, Ci, K, generator=g) / (Ci * K) ** 0.5
+    wp = ops.pack_conv_weight(w.cuda(), torch.bfloat16)
+    ref = F.conv1d(x.float().transpose(1, 2), w.bfloat16().float(), padding=K // 2).transpose(1, 2)
+    kw = dict(Co=Co, K=K, pad=K // 2, out_dtype=out_dt, compute_dtype=torch.bfloat16)
+    try:
+        got = ops.conv1d(x.cuda(), wp, None, **kw)
+        again = ops.conv1d(x.cuda(), wp, None, **kw)
+        assert L.vo_tune(b"splitk_cfg", 3) == 0
+        unsplit = ops.conv1d(x.cuda(), wp, None, **kw)
+    finally:
+        L.vo_tune(b"splitk_cfg", 0)
+    assert torch.equal(got, again)
+    assert rel_l2(got.float().cpu(), ref) < 1e-2
+    assert rel_l2(got.float().cpu(), unsplit.float().cpu()) < (4e-3 if out_dt == torch.bfloat16 else 1e-5)

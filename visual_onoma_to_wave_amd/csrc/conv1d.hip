@@ -809,6 +809,7 @@ conv1d_kernel(ConvArgs a) {
 
 // split reduction, second pass: y = epilogue(sum_z partial[z] + bias) with the partials added
 // in split order; the epilogue (activation, residual, scale, accumulate) is conv_epilogue's
+template <typename TOUT>
 __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int splits) {
   const int cg = a.Co / 4;
   const int64_t rows = (int64_t)a.B * a.T_out;
@@ -835,7 +836,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int
   const int64_t off = (int64_t)b * a.ybs + (int64_t)t * a.ldy + c;
   if (a.res1) {
     float rr[4];
-    load4(reinterpret_cast<const float*>(a.res1) + off, rr);
+    load4(reinterpret_cast<const TOUT*>(a.res1) + off, rr);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] += rr[e];
   }
@@ -843,21 +844,44 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int
   for (int e = 0; e < 4; ++e) v[e] *= a.out_scale;
   if (a.res2) {
     float rr[4];
-    load4(reinterpret_cast<const float*>(a.res2) + off, rr);
+    load4(reinterpret_cast<const TOUT*>(a.res2) + off, rr);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] += rr[e];
   }
-  store4(reinterpret_cast<float*>(a.y) + off, v);
+  store4(reinterpret_cast<TOUT*>(a.y) + off, v);
 }
 
 // fp32 convs over short sequences (T_out <= 16 rows: glyph encoder, variance predictors at
 // T_src ~ 12) are a serial chain of (Ci / 32) * K pipeline steps per workgroup, each bound by
 // a load round trip (FFN w_1: 72 steps, 51 us for 1.8 GFLOP).  Split the chunks so a workgroup
 // runs about 4 steps; the partials are added by conv_splitk_reduce_kernel.  splitk_cfg 1 = off.
+// bf16 deep reductions into narrow outputs (the C4 decoder's FFN w_1 input gradient: 1024 -> 256, k = 9,
+// 16 k rows: a 9216-deep reduction, 106 us on 64 x 128 tiles): the 256 x 256 tile with its chunks split
+// over ~256 workgroups, the fp32 partials added in split order by conv_splitk_reduce_kernel.  Plain convs
+// only (no bias, activation, residual, scale or mask).  splitk_cfg 3 = off (A/B).
+static bool splitk_bf16_ok(const vo_conv1d_desc* d) {
+  return d->compute_dtype == VO_BF16 && d->x_dtype == VO_BF16 && !d->transposed && d->stride <= 1 && d->groups <= 1 &&
+         d->variant == 0 && !d->bias && !d->res1 && !d->res2 && !d->ymask && d->pre_act == VO_ACT_NONE &&
+         d->post_act == VO_ACT_NONE && d->out_scale == 1.f && d->Co <= 256 && d->Co % 64 == 0 && d->Ci % KC == 0 &&
+         (int64_t)(d->Ci / KC) * d->K >= 64 && (int64_t)d->B * d->T_out >= 8192 && d->ldy == d->Co &&
+         vo_tune_get("splitk_cfg") != 3 && vo_tune_get("splitk_cfg") != 1 && vo_tune_get("gen_cfg") == 0;
+}
+
 static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
   *splits = 1;
   *kcs = 0;
   if (vo_tune_get("splitk_cfg") == 1 || vo_tune_get("gen_cfg") != 0) return false;
+  if (d->compute_dtype == VO_BF16) {
+    if (!splitk_bf16_ok(d)) return false;
+    const int n_chunks = d->Ci / KC;
+    const int64_t tiles = (int64_t)d->B * ((d->T_out + 255) / 256) * ((d->Co + 255) / 256);
+    int s = (int)std::min<int64_t>(n_chunks / 4, std::max<int64_t>(2, (256 + tiles - 1) / tiles));
+    if (s < 2) return false;
+    const int k = (n_chunks + s - 1) / s;
+    *splits = (n_chunks + k - 1) / k;
+    *kcs = k;
+    return *splits >= 2;
+  }
   if ((d->compute_dtype != VO_F32 && d->compute_dtype != VO_F32X3) || d->x_dtype != VO_F32 || d->y_dtype != VO_F32)
     return false;
   if (d->transposed || d->stride > 1 || d->groups > 1 || d->variant != 0) return false;
@@ -989,7 +1013,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   a.partial = nullptr;
   a.kcs = 0;
   int splits = 1;
-  if constexpr (sizeof(TC) == 4 && S == 1) {
+  if constexpr (S == 1) {
     int kcs = 0;
     if (d->workspace && splitk_plan(d, &splits, &kcs) &&
         d->workspace_bytes >= (int64_t)splits * d->B * d->T_out * d->Co * (int64_t)sizeof(float)) {
@@ -1004,7 +1028,7 @@ static int launch_cfg_s(const vo_conv1d_desc* d, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(WCO * WT * 64), lds, st, a);
   if (a.partial) {
     const int64_t n = (int64_t)d->B * d->T_out * (d->Co / 4);
-    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, splits);
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel<TOUT>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, splits);
   }
   VO_RETURN_LAUNCH();
 }
@@ -1145,6 +1169,9 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     if (gq == 17) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 1>(d, st);  // 64 x 128, TPS 1
   }
 #endif
+  if constexpr (sizeof(TC) == 2) {
+    if (d->workspace && splitk_bf16_ok(d)) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // split 256 x 256
+  }
   if constexpr (sizeof(TC) == 2) {
     // decoder shapes at B*T = 16384 rows (tools/ab_sb.py gen): wide outputs (FFN w_1 k9 1024,
     // fused q/k/v 768) -> 256 x 256 tiles (-18 %); 1x1 convs to 256 channels -> 64 x 128

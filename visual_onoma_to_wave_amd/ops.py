@@ -137,8 +137,13 @@ def conv1d(x, w_packed, bias, *, Co, K, dil=1, pad=0, T_out=None, out=None, out_
             raise ValueError("conv1d: ymask must match the output (shape, strides, dtype)")
         d.ymask, d.ymask_slope = ymask.data_ptr(), float(ymask_slope)
     ws = None
-    if storage_dtype(compute_dtype) == torch.float32 and T_rows <= 16 and transposed is None and stride <= 1 and groups <= 1:
-        # split-reduction scratch for the short fp32 convs (stream-ordered: freed after enqueue)
+    plain = (transposed is None and stride <= 1 and groups <= 1)
+    deep_bf16 = (compute_dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and bias is None and res1 is None and
+                 res2 is None and ymask is None and pre_act == ACT_NONE and post_act == ACT_NONE and out_scale == 1.0 and
+                 Co <= 256 and Ci * K >= 2048 and B * T_rows >= 8192)
+    if plain and ((storage_dtype(compute_dtype) == torch.float32 and T_rows <= 16) or deep_bf16):
+        # split-reduction scratch: the short fp32 convs, the deep bf16 convs into <= 256 channels
+        # (stream-ordered: freed after enqueue)
         nb = _lib.lib().vo_conv1d_workspace_size(ctypes.byref(d))
         if nb > 0:
             ws = torch.empty(nb // 4, dtype=torch.float32, device=x.device)
