@@ -75,3 +75,4 @@ def test_conv1d_bf16_split_reduction(B, T, Ci, Co, K, out_dt):
     assert torch.equal(got, again)
     assert rel_l2(got.float().cpu(), ref) < 1e-2
     assert rel_l2(got.float().cpu(), unsplit.float().cpu()) < (4e-3 if out_dt == torch.bfloat16 else 1e-5)
+
