@@ -889,8 +889,8 @@ static bool splitk_plan(const vo_conv1d_desc* d, int* splits, int* kcs) {
   const int n_chunks = (d->Ci + KC - 1) / KC;
   if (n_chunks * d->K < 16) return false;
   // ~4 steps per split (bench step 13.78 ms vs 13.85 with ~8 and 13.93 unsplit,
-  // tools/bench_splitk_ab.sh); splitk_cfg 2 = ~8
-  const int target = vo_tune_get("splitk_cfg") == 2 ? 8 : 4;
+  // tools/bench_splitk_ab.sh); splitk_cfg 2 = ~8, 4 = ~16
+  const int target = vo_tune_get("splitk_cfg") == 2 ? 8 : vo_tune_get("splitk_cfg") == 4 ? 16 : 4;
   const int k = std::max(1, target / d->K);
   const int s = (n_chunks + k - 1) / k;
   if (s < 2) return false;
