@@ -76,3 +76,35 @@ def test_conv1d_bf16_split_reduction(B, T, Ci, Co, K, out_dt):
     assert rel_l2(got.float().cpu(), ref) < 1e-2
     assert rel_l2(got.float().cpu(), unsplit.float().cpu()) < (4e-3 if out_dt == torch.bfloat16 else 1e-5)
 
+
+
+@pytest.mark.parametrize("B,T,Ci,Co,K,S,g,pad", [
+    # the MSD's grouped strided layers (k = 41, stride 2 / 4, groups 4 / 16), an MPD-style stride 3, ragged T
+    (4, 4096, 128, 128, 41, 2, 4, 20), (4, 4096, 128, 256, 41, 2, 16, 20), (4, 2048, 256, 512, 41, 4, 16, 20),
+    (3, 2731, 32, 128, 5, 3, 1, 2), (2, 1000, 64, 64, 7, 2, 1, 3), (2, 777, 128, 256, 41, 2, 16, 20)])
+def test_wgrad_multitap_strided_vs_per_tap(B, T, Ci, Co, K, S, g, pad):
+    """Strided convs on the multi-tap kernel (window 64 S + 64 rows, B row = A row x S + tap) against the
+    per-tap kernel (wgrad_mt 2) on the same bf16 operands, <= 1e-6 rel-L2, and against torch; deterministic."""
+    import torch.nn.functional as F
+    from visual_onoma_to_wave_amd import _lib, ops
+    L = _lib.lib()
+    gen = torch.Generator().manual_seed(B * T + K + Co + S)
+    x = torch.randn(B, T, Ci, generator=gen).to(torch.bfloat16)
+    T_out = (T + 2 * pad - K) // S + 1
+    gy = torch.randn(B, T_out, Co, generator=gen).to(torch.bfloat16)
+    xa, gya = x.cuda(), gy.cuda()
+    kw = dict(S=S, pad=pad, pre_b=0.1, groups=g)
+    try:
+        assert L.vo_tune(b"wgrad_mt", 2) == 0
+        ref = ops.conv1d_wgrad(gya, xa, K, **kw)
+        assert L.vo_tune(b"wgrad_mt", 0) == 0
+        got = ops.conv1d_wgrad(gya, xa, K, **kw)
+        again = ops.conv1d_wgrad(gya, xa, K, **kw)
+    finally:
+        L.vo_tune(b"wgrad_mt", 0)
+    assert torch.equal(got, again)
+    assert rel_l2(got.cpu(), ref.cpu()) < 1e-6, rel_l2(got.cpu(), ref.cpu())
+    xt = F.leaky_relu(x.float(), 0.1).to(torch.bfloat16).float()
+    tw = torch.nn.grad.conv1d_weight(xt.transpose(1, 2), (Co, Ci // g, K), gy.float().transpose(1, 2), stride=S,
+                                     padding=pad, groups=g)
+    assert rel_l2(got.cpu(), tw) < 1e-5

@@ -437,24 +437,29 @@ __global__ void __launch_bounds__(256, 2) wgrad_k1_kernel(WgradArgs p) {
 constexpr int WM_R = 64;       // rows per chunk
 constexpr int WM_MAXW = 128;   // window rows: 64 + (nk - 1) * dil <= 128
 
-template <int TM, int KG>
+// Round 6: strided convs (the MSD's grouped stride-2 / 4 layers, k = 41: on the per-tap kernel each tap
+// restaged both operands -- a 147-chunk serial chain of 8 MFMAs per 12 KB staged): SW > 1 sizes the window
+// for stride S <= SW, 64 SW + 64 rows; A row r of a chunk meets window row r S + kk dil for tap kk (the
+// transposed reads name their row per lane, so the stride costs nothing in the reads).
+template <int TM, int KG, int SW = 1>
 __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunks_per_b, int chunks_per_split,
                                                          int ntg) {
+  constexpr int WMW = SW == 1 ? WM_MAXW : 64 * SW + 64;  // window capacity (rows)
   constexpr int P = TM == 64 ? 72 : 48;  // pitch (elements): the 4 rows of a transposed read on distinct banks
   constexpr int WT = TM / 2;             // wave sub-tile (2 x 2 waves)
   constexpr int MI = WT / 16;            // MFMA tiles per wave and dimension
   constexpr int VPR = TM / 8;            // 16-byte vectors per staged row
   constexpr int NVA = WM_R * VPR / 256;  // A vectors per thread
-  constexpr int NVB = WM_MAXW * VPR / 256;  // B window vectors per thread (upper bound)
+  constexpr int NVB = (WMW * VPR + 255) / 256;  // B window vectors per thread (upper bound)
   __shared__ __attribute__((aligned(16))) bf16_t sa[WM_R * P];
-  __shared__ __attribute__((aligned(16))) bf16_t sb[WM_MAXW * P];
+  __shared__ __attribute__((aligned(16))) bf16_t sb[WMW * P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave & 1) * WT, wn = (wave >> 1) * WT;
   const int tiles_n = (p.N + TM - 1) / TM;
   const int m0 = (blockIdx.y / tiles_n) * TM, n0 = (blockIdx.y % tiles_n) * TM;
   const int tg = blockIdx.z % ntg, grp = blockIdx.z / ntg;
   const int k0 = tg * KG, nk = min(KG, p.K - k0);
-  const int WR = WM_R + (nk - 1) * p.dil;  // window rows of this tap run
+  const int WR = (WM_R - 1) * p.S + 1 + (nk - 1) * p.dil;  // window rows of this tap run
   const int c_begin = blockIdx.x * chunks_per_split;
   const int c_end = min(p.Bn * chunks_per_b, c_begin + chunks_per_split);
   const bf16_t* A = reinterpret_cast<const bf16_t*>(p.a) + (int64_t)grp * p.M;
@@ -483,10 +488,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
       const int t = min(t0 + r, p.T_A - 1);
       va[s] = *reinterpret_cast<const u32x4_t*>(A + ((int64_t)b * p.T_A + t) * p.lda + min(m0 + col, p.M - 8));
     }
-    const int tb0 = t0 - p.pad + k0 * p.dil;
+    const int tb0 = t0 * p.S - p.pad + k0 * p.dil;
 #pragma unroll
     for (int s = 0; s < NVB; ++s) {
-      const int v = tid + s * 256, w = v / VPR, col = (v % VPR) * 8;
+      const int v = tid + s * 256, w = min(v / VPR, WMW - 1), col = (v % VPR) * 8;
       const int tb = min(max(tb0 + w, 0), p.T_B - 1);
       vb[s] = *reinterpret_cast<const u32x4_t*>(Bs + ((int64_t)b * p.T_B + tb) * p.ldb + min(n0 + col, p.N - 8));
     }
@@ -502,7 +507,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
       if (p.pre_a) x = u32x4_t{lrelu_pack(x.x, p.slope), lrelu_pack(x.y, p.slope), lrelu_pack(x.z, p.slope), lrelu_pack(x.w, p.slope)};
       *reinterpret_cast<u32x4_t*>(sa + r * P + col) = x;
     }
-    const int tb0 = t0 - p.pad + k0 * p.dil;
+    const int tb0 = t0 * p.S - p.pad + k0 * p.dil;
 #pragma unroll
     for (int s = 0; s < NVB; ++s) {
       const int v = tid + s * 256, w = v / VPR, col = (v % VPR) * 8;
@@ -528,6 +533,18 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
     f.v = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     return f;
   };
+  // B fragment of A rows arow0 + 8 g .. (+ 8) for tap kk: window rows (A row) S + kk dil
+  auto frag_b = [&](int arow0, int kk, int c0) {
+    if constexpr (SW == 1) return frag(sb, arow0 + kk * p.dil, c0);
+    const int r = arow0 + 8 * g + q;
+    const bf16_t* lo_p = sb + (r * p.S + kk * p.dil) * P + c0 + 4 * pp;
+    const bf16_t* hi_p = sb + ((r + 4) * p.S + kk * p.dil) * P + c0 + 4 * pp;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)lo_p);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)hi_p);
+    Frag<bf16_t> f;
+    f.v = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return f;
+  };
 
   auto compute = [&]() {
     if (do_bias) {
@@ -547,7 +564,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
         if (kk < nk) {  // uniform
           Frag<bf16_t> fb[MI];
 #pragma unroll
-          for (int j = 0; j < MI; ++j) fb[j] = frag(sb, ks * 32 + kk * p.dil, wn + 16 * j);
+          for (int j = 0; j < MI; ++j) fb[j] = frag_b(ks * 32, kk, wn + 16 * j);
 #pragma unroll
           for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -726,7 +743,7 @@ static void wgrad_plan(int B, int T_A, int M, int N, int K, int groups, int64_t*
 // rest of the parallelism comes from splits.  dil bounds a run's window (64 + (KG - 1) dil <= 128
 // rows); the splits never grow with dil, so the plan at dil = 1 sizes the workspace.
 struct MtPlan { int tm, kg, ntg, chunks_per_b, cps, splits; };
-static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int dil, MtPlan* pl) {
+static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int dil, MtPlan* pl, int S = 1) {
   pl->tm = (M <= 32 && N <= 32) ? 32 : 64;
   const int64_t tiles = (int64_t)((M + pl->tm - 1) / pl->tm) * ((N + pl->tm - 1) / pl->tm) * groups;
   pl->chunks_per_b = (T_A + WM_R - 1) / WM_R;
@@ -735,7 +752,9 @@ static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int d
   const int64_t operand = rows * ((int64_t)M + N) * groups * 2;
   const int64_t per_split = ((int64_t)groups * K * M * N + (int64_t)groups * M) * 4;
   const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(total, std::max<int64_t>(operand, 16 << 20) / per_split));
-  const int kgmax = std::min(pl->tm == 64 ? 8 : 11, 1 + 64 / std::max(dil, 1));  // TM 64 x 9+ taps spill
+  // TM 64 x 9+ taps spill (strided: 5, the larger window's staging registers); the window (stride S: 64 S + 64
+  // rows) bounds a run to 1 + 64 / dil taps either way
+  const int kgmax = std::min(pl->tm == 64 ? (S > 1 ? 5 : 8) : 11, 1 + 64 / std::max(dil, 1));
   const int forced = vo_tune_get("wgrad_kg");  // A/B: taps per run
   int ntg = (int)std::max<int64_t>(1, (256 + tiles * smax - 1) / (tiles * smax));
   int kg = forced > 0 ? forced : (K + ntg - 1) / ntg;
@@ -781,29 +800,33 @@ extern "C" int64_t vo_conv1d_wgrad_workspace_size(int B, int T_A, int M, int N, 
   return splits * ((int64_t)groups * K * M * N + (int64_t)groups * M) * (int64_t)sizeof(float);
 }
 
-template <int TM, int KG>
+template <int TM, int KG, int SW>
 static void wgrad_mt_launch(const WgradArgs& p, const MtPlan& pl, int groups, hipStream_t st) {
   const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
-  hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG>), dim3((unsigned)pl.splits, (unsigned)tiles, (unsigned)(pl.ntg * groups)),
-                     dim3(256), 0, st, p, pl.chunks_per_b, pl.cps, pl.ntg);
+  hipLaunchKernelGGL((wgrad_mt_kernel<TM, KG, SW>), dim3((unsigned)pl.splits, (unsigned)tiles,
+                     (unsigned)(pl.ntg * groups)), dim3(256), 0, st, p, pl.chunks_per_b, pl.cps, pl.ntg);
 }
-template <int TM>
+template <int TM, int SW>
 static void wgrad_mt_dispatch(const WgradArgs& p, const MtPlan& pl, int groups, hipStream_t st) {
   switch (pl.kg) {
-    case 1: return wgrad_mt_launch<TM, 1>(p, pl, groups, st);
-    case 2: return wgrad_mt_launch<TM, 2>(p, pl, groups, st);
-    case 3: return wgrad_mt_launch<TM, 3>(p, pl, groups, st);
-    case 4: return wgrad_mt_launch<TM, 4>(p, pl, groups, st);
-    case 5: return wgrad_mt_launch<TM, 5>(p, pl, groups, st);
-    case 6: return wgrad_mt_launch<TM, 6>(p, pl, groups, st);
-    case 7: return wgrad_mt_launch<TM, 7>(p, pl, groups, st);
-    case 8: return wgrad_mt_launch<TM, 8>(p, pl, groups, st);
+    case 1: return wgrad_mt_launch<TM, 1, SW>(p, pl, groups, st);
+    case 2: return wgrad_mt_launch<TM, 2, SW>(p, pl, groups, st);
+    case 3: return wgrad_mt_launch<TM, 3, SW>(p, pl, groups, st);
+    case 4: return wgrad_mt_launch<TM, 4, SW>(p, pl, groups, st);
+    case 5: return wgrad_mt_launch<TM, 5, SW>(p, pl, groups, st);
   }
-  if constexpr (TM == 32) {  // TM 64 runs at most 8 taps (wgrad_mt_plan)
+  if constexpr (TM == 32 || SW == 1) {  // TM 64 runs at most 8 taps, 5 when strided (wgrad_mt_plan)
     switch (pl.kg) {
-      case 9: return wgrad_mt_launch<32, 9>(p, pl, groups, st);
-      case 10: return wgrad_mt_launch<32, 10>(p, pl, groups, st);
-      default: return wgrad_mt_launch<32, 11>(p, pl, groups, st);
+      case 6: return wgrad_mt_launch<TM, 6, SW>(p, pl, groups, st);
+      case 7: return wgrad_mt_launch<TM, 7, SW>(p, pl, groups, st);
+      case 8: return wgrad_mt_launch<TM, 8, SW>(p, pl, groups, st);
+    }
+  }
+  if constexpr (TM == 32) {
+    switch (pl.kg) {
+      case 9: return wgrad_mt_launch<32, 9, SW>(p, pl, groups, st);
+      case 10: return wgrad_mt_launch<32, 10, SW>(p, pl, groups, st);
+      default: return wgrad_mt_launch<32, 11, SW>(p, pl, groups, st);
     }
   }
 }
@@ -855,14 +878,18 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   const int64_t padded = (int64_t)((T_A + WM_R - 1) / WM_R) * WM_R;
   // (K = 1 on the multi-tap kernel measured 4-13 % slower at the C4 decoder's 1x1 shapes)
   const bool mt_ok = K >= 2 && 8 * (padded - T_A) <= T_A;
-  if (dtype == VO_BF16 && S == 1 && mt_ok && vo_tune_get("wgrad_mt") != 1 && p.abl == 0) {
+  // strided convs (S <= 4: the MSD's grouped layers) on the multi-tap kernel's wider windows (wgrad_mt 2 = off)
+  const bool mt_stride = S == 1 || (S <= 4 && vo_tune_get("wgrad_mt") != 2);
+  if (dtype == VO_BF16 && mt_stride && mt_ok && vo_tune_get("wgrad_mt") != 1 && p.abl == 0) {
     MtPlan pl;
-    wgrad_mt_plan(B, T_A, M, N, K, groups, dil, &pl);
+    wgrad_mt_plan(B, T_A, M, N, K, groups, dil, &pl, S);
     VO_CHECK_ARG(pl.splits < (1 << 30) && pl.ntg * groups < 65536, "conv1d_wgrad: grid too large");
-    if (pl.tm == 32)
-      wgrad_mt_dispatch<32>(p, pl, groups, st);
+    if (S == 1)
+      pl.tm == 32 ? wgrad_mt_dispatch<32, 1>(p, pl, groups, st) : wgrad_mt_dispatch<64, 1>(p, pl, groups, st);
+    else if (S == 2)
+      pl.tm == 32 ? wgrad_mt_dispatch<32, 2>(p, pl, groups, st) : wgrad_mt_dispatch<64, 2>(p, pl, groups, st);
     else
-      wgrad_mt_dispatch<64>(p, pl, groups, st);
+      pl.tm == 32 ? wgrad_mt_dispatch<32, 4>(p, pl, groups, st) : wgrad_mt_dispatch<64, 4>(p, pl, groups, st);
     wgrad_reduce_launch(workspace, pl.splits, p.n_w, p.n_tot, M, N, K, dw, db, st);
     VO_RETURN_LAUNCH();
   }
