@@ -81,7 +81,9 @@ def test_conv1d_bf16_split_reduction(B, T, Ci, Co, K, out_dt):
 @pytest.mark.parametrize("B,T,Ci,Co,K,S,g,pad", [
     # the MSD's grouped strided layers (k = 41, stride 2 / 4, groups 4 / 16), an MPD-style stride 3, ragged T
     (4, 4096, 128, 128, 41, 2, 4, 20), (4, 4096, 128, 256, 41, 2, 16, 20), (4, 2048, 256, 512, 41, 4, 16, 20),
-    (3, 2731, 32, 128, 5, 3, 1, 2), (2, 1000, 64, 64, 7, 2, 1, 3), (2, 777, 128, 256, 41, 2, 16, 20)])
+    (3, 2731, 32, 128, 5, 3, 1, 2), (2, 1000, 64, 64, 7, 2, 1, 3), (2, 777, 128, 256, 41, 2, 16, 20),
+    # short utterances (T_out 65..257, up to half of each chunk padding: many-tap convs only)
+    (8, 1025, 256, 512, 41, 4, 16, 20), (8, 257, 512, 1024, 41, 4, 16, 20), (4, 128, 1024, 1024, 41, 1, 16, 20)])
 def test_wgrad_multitap_strided_vs_per_tap(B, T, Ci, Co, K, S, g, pad):
     """Strided convs on the multi-tap kernel (window 64 S + 64 rows, B row = A row x S + tap) against the
     per-tap kernel (wgrad_mt 2) on the same bf16 operands, <= 1e-6 rel-L2, and against torch; deterministic."""

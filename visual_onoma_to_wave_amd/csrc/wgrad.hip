@@ -877,7 +877,10 @@ extern "C" int vo_conv1d_wgrad_bias(const void* a, int lda, int T_A, const void*
   // kernel's flattened rows)
   const int64_t padded = (int64_t)((T_A + WM_R - 1) / WM_R) * WM_R;
   // (K = 1 on the multi-tap kernel measured 4-13 % slower at the C4 decoder's 1x1 shapes)
-  const bool mt_ok = K >= 2 && 8 * (padded - T_A) <= T_A;
+  // (many-tap convs -- the MSD's k = 41 layers at T_A = 65..257 -- also with up to half the chunk rows padding:
+  // the per-tap kernel restages both operands per tap, 41 times; wgrad_mt 3 = the 1/8 rule only)
+  const bool mt_ok = K >= 2 && (8 * (padded - T_A) <= T_A ||
+                                (K >= 16 && padded <= 2 * (int64_t)T_A && vo_tune_get("wgrad_mt") != 3));
   // strided convs (S <= 4: the MSD's grouped layers) on the multi-tap kernel's wider windows (wgrad_mt 2 = off)
   const bool mt_stride = S == 1 || (S <= 4 && vo_tune_get("wgrad_mt") != 2);
   if (dtype == VO_BF16 && mt_stride && mt_ok && vo_tune_get("wgrad_mt") != 1 && p.abl == 0) {
