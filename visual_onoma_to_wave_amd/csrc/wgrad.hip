@@ -763,7 +763,9 @@ static void wgrad_mt_plan(int B, int T_A, int M, int N, int K, int groups, int d
   if (forced <= 0) kg = (K + ntg - 1) / ntg;  // balanced runs (K = 9 at 8 taps max: 5 + 4, not 8 + 1)
   pl->kg = kg;
   pl->ntg = ntg;
-  const int64_t want = std::max<int64_t>(1, (512 + tiles * ntg - 1) / (tiles * ntg));
+  const int wc = vo_tune_get("wgrad_cfg");  // A/B: 19 / 20 = ~2048 / ~1024 workgroups
+  const int64_t wtarget = wc == 19 ? 2048 : wc == 20 ? 1024 : 512;
+  const int64_t want = std::max<int64_t>(1, (wtarget + tiles * ntg - 1) / (tiles * ntg));
   const int64_t splits = std::min(smax, want);
   pl->cps = (int)((total + splits - 1) / splits);
   pl->splits = (int)((total + pl->cps - 1) / pl->cps);
