@@ -110,3 +110,4 @@ def test_wgrad_multitap_strided_vs_per_tap(B, T, Ci, Co, K, S, g, pad):
     tw = torch.nn.grad.conv1d_weight(xt.transpose(1, 2), (Co, Ci // g, K), gy.float().transpose(1, 2), stride=S,
                                      padding=pad, groups=g)
     assert rel_l2(got.cpu(), tw) < 1e-5
+
