@@ -1191,6 +1191,9 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       // 256 k9 at 16384 rows: 125 -> 106 us, tools/probes/dgrad_tiles.py): 64 x 128, twice the workgroups
       const int64_t t128 = (int64_t)d->B * ((d->T_out + 127) / 128) * ((d->Co + 127) / 128);
       if (d->Co <= 256 && d->Co % 64 == 0 && t128 < 512) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);
+      // wide convs with fewer than 256 128 x 128 tiles (C5's MPD over joined period columns, 1024 -> 1024
+      // k = 5 at 2-5 k rows: 136-312 workgroups) on 64 x 128 tiles too: C5 24.07 -> 23.75 ms (tile_cfg 1 = off)
+      if (vo_tune_get("tile_cfg") != 1 && d->Co % 64 == 0 && t128 < 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);
     }
     // mid-width convs (PostNet 512 -> 512 k5, conv_pre 80 -> 512 k7 at 16384 rows): 128 x 256
     // tiles (twice the rows per staged weight tap): 512 k5 67.9 -> 63.4 us, 80 k7 27.6 -> 27.0,

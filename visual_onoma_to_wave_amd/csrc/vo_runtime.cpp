@@ -23,7 +23,7 @@ extern "C" int vo_version(void) { return VO_ABI_VERSION; }
 // experiment knobs (kernel-variant selection for A/B runs); unknown keys read as 0.
 // VO_TUNE="pair_cfg=1,conv_cfg=1" presets them for a whole process (bench A/B).
 static const char* const kKnobs[] = {"pair_cfg", "conv_cfg", "gen_cfg", "wgrad_cfg", "rb3_cfg", "att_cfg", "ups_cfg", "post_cfg", "splitk_cfg",
-                                      "wgrad_mt", "wgrad_kg", "att_xcd", "pc_cfg", "rs_cfg", "lin_cfg", "seg_cfg"};
+                                      "wgrad_mt", "wgrad_kg", "att_xcd", "pc_cfg", "rs_cfg", "lin_cfg", "seg_cfg", "tile_cfg"};
 static int g_knobs[sizeof(kKnobs) / sizeof(kKnobs[0])] = {};
 
 static bool is_ablation(const char* key, int value);
