@@ -451,8 +451,20 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
   constexpr int VPR = TM / 8;            // 16-byte vectors per staged row
   constexpr int NVA = WM_R * VPR / 256;  // A vectors per thread
   constexpr int NVB = (WMW * VPR + 255) / 256;  // B window vectors per thread (upper bound)
+  // strided windows at TM = 32 (96-byte rows): the rows a half-wave's transposed reads name are (r + 8g + q) S +
+  // kk -- at S = 2 the two 16-lane groups (rows 16 apart) hit the same banks, at S = 4 also q and q + 2 (2.2
+  // conflicts per LDS instruction measured).  Row R is placed at R P + ROFF(R): 32 B more per 16 rows (S = 2),
+  // 64 B per 8 rows + 32 B per 32 rows (S = 4) -- monotonic (no two rows overlap), and the lanes' 32-byte slots
+  // of a half-wave land on 8 distinct bank slots
+  constexpr bool SWZ = SW > 1 && TM == 32;
+  auto roff = [&](int R) -> int {
+    if constexpr (!SWZ) return R * P;
+    if constexpr (SW == 2) return R * P + 16 * (R >> 4);
+    return R * P + 32 * (R >> 3) + 16 * (R >> 5);
+  };
+  constexpr int SB_EXTRA = SWZ ? 32 * (WMW / 8 + 1) + 16 * (WMW / 32 + 1) : 0;
   __shared__ __attribute__((aligned(16))) bf16_t sa[WM_R * P];
-  __shared__ __attribute__((aligned(16))) bf16_t sb[WMW * P];
+  __shared__ __attribute__((aligned(16))) bf16_t sb[WMW * P + SB_EXTRA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave & 1) * WT, wn = (wave >> 1) * WT;
   const int tiles_n = (p.N + TM - 1) / TM;
@@ -516,7 +528,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
         const int tb = tb0 + w;
         if (tb < 0 || tb >= p.T_B || n0 + col >= p.N) y = u32x4_t{0u, 0u, 0u, 0u};
         if (p.pre_b) y = u32x4_t{lrelu_pack(y.x, p.slope), lrelu_pack(y.y, p.slope), lrelu_pack(y.z, p.slope), lrelu_pack(y.w, p.slope)};
-        *reinterpret_cast<u32x4_t*>(sb + w * P + col) = y;
+        *reinterpret_cast<u32x4_t*>(sb + roff(w) + col) = y;
       }
     }
   };
@@ -537,8 +549,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_mt_kernel(WgradArgs p, int chunk
   auto frag_b = [&](int arow0, int kk, int c0) {
     if constexpr (SW == 1) return frag(sb, arow0 + kk * p.dil, c0);
     const int r = arow0 + 8 * g + q;
-    const bf16_t* lo_p = sb + (r * p.S + kk * p.dil) * P + c0 + 4 * pp;
-    const bf16_t* hi_p = sb + ((r + 4) * p.S + kk * p.dil) * P + c0 + 4 * pp;
+    const bf16_t* lo_p = sb + roff(r * p.S + kk * p.dil) + c0 + 4 * pp;
+    const bf16_t* hi_p = sb + roff((r + 4) * p.S + kk * p.dil) + c0 + 4 * pp;
     const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)lo_p);
     const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)hi_p);
     Frag<bf16_t> f;
