@@ -1189,7 +1189,10 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
       // (unless that leaves fewer than 128 workgroups: the MPD's joined period columns, ~4-5k rows x
       // 1024 channels, got 68-80 -- there the 128 x 128 tile below)
       const int64_t t256 = (int64_t)d->B * ((d->T_out + 255) / 256) * (d->Co / 256);
-      if (vo_tune_get("gen_cfg") != 11 && d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
+      // (utterances of >= 256 rows: at T_out = 128 -- the MSD's 1024-channel layers -- half of every 256-row
+      // tile was padding: C5 23.68 -> 23.43 ms with them on the tiles below; tile_cfg 9 = the round-5 rule)
+      const bool t_ok = d->T_out >= 256 || vo_tune_get("tile_cfg") == 9;
+      if (vo_tune_get("gen_cfg") != 11 && t_ok && d->Co >= 768 && d->Co % 256 == 0 && t256 >= 128) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256
       if (vo_tune_get("gen_cfg") < 9 && d->K == 1 && d->Co <= 256) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);         // 64 x 128
       // Co <= 256 k > 1 with fewer than 512 128 x 128 tiles (the C4 decoder's FFN w_1 input gradient, 1024 ->
       // 256 k9 at 16384 rows: 125 -> 106 us, tools/probes/dgrad_tiles.py): 64 x 128, twice the workgroups
@@ -1209,6 +1212,10 @@ static int launch_types(const vo_conv1d_desc* d, hipStream_t st) {
     if (gc == 10) return launch_cfg<TIN, TC, TOUT, 4, 4, 4, 2, 2>(d, st);  // 256 x 128
     if (gc == 11) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);  // 64 x 128 (A/B)
     if (gc == 12 && d->Co % 256 == 0) return launch_cfg<TIN, TC, TOUT, 4, 8, 4, 2, 2>(d, st);  // 256 x 256 (A/B)
+  }
+  if constexpr (sizeof(TC) == 2) {  // bf16: 64 x 128 in place of the 128 x 128 default (C5 23.68 -> 23.52 ms, C4 and
+                                    // inference shapes unaffected); tile_cfg 9 = the round-5 rule
+    if (vo_tune_get("tile_cfg") != 9) return launch_cfg<TIN, TC, TOUT, 2, 4, 2, 2, 2>(d, st);
   }
   return launch_cfg<TIN, TC, TOUT, 4, 4, 2, 2, 2>(d, st);                    // 128 x 128
 }
